@@ -1,0 +1,189 @@
+#!/usr/bin/env python3
+"""Benchmark of the MPPI rollout-and-reduce hot path (BASELINE.json metric).
+
+One "step" = one full MPPI control step of the hot path on device over one
+batch of synthetic noise: K x T rollouts + running / terminal cost + soft-min
+weights + weighted noise sum (control.py:81-118) + median filter, u += w_eps
+and shift (control.py:122-149), so consecutive steps chain on the updated
+nominal control exactly like the reference's receding horizon.  N = 1: one
+launch per step (fused last-workgroup update).  N > 1 (torchrun, one process
+per GPU, RCCL): rollout launch -> one all_gather of the 130-double device
+partials over xGMI -> merge + update launch.  Weak scaling: K per GPU is fixed
+(default 65536 = BASELINE config 3 at N = 1, config 4's K = 524288 at N = 8).
+
+Inputs: run.py constants (dt 0.006, lambda 100, alpha 0.98, Sigma 20 I,
+weights [.5 .5 5 5] / [5 5 50 50]), start pose of run.py, the first window of
+xydq_circle.txt, noise N(0, Sigma) from the device Philox generator, 10
+distinct buffers rotated so their total (335 MB at K=65536 T=64) exceeds the
+256 MiB Infinity Cache.  Everything is resident in HBM before timing starts.
+
+Prints ONE JSON line on rank 0.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+import torch
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+from mppi_robotarm_amd.engine import RolloutEngine  # noqa: E402
+from mppi_robotarm_amd.params import ArmParams, X0_RUNPY  # noqa: E402
+
+HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md, chip-level parameters)
+BYTES_PER_STATE_STEP = 8  # fp32 eps[t][k][0:2] read once
+
+
+def parse():
+    p = argparse.ArgumentParser()
+    p.add_argument("--gpus", type=int, default=1)
+    p.add_argument("--steps", type=int, default=200)
+    p.add_argument("--warmup", type=int, default=20)
+    p.add_argument("--K", type=int, default=65536, help="samples per GPU")
+    p.add_argument("--T", type=int, default=64)
+    p.add_argument("--nbuf", type=int, default=10, help="rotated noise buffers")
+    p.add_argument("--lps", type=int, default=0, help="lanes per sample (0 = auto)")
+    p.add_argument("--cpu-seconds", type=float, default=10.0, help="CPU baseline budget (0 = skip)")
+    p.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "traffic.json"))
+    return p.parse_args()
+
+
+def cpu_baseline(args, window, x0, u):
+    """C oracle restatement (OpenMP over samples) on the host cores, rank 0, N = 1."""
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import coracle  # checker / baseline only
+    arm = ArmParams()
+    K, T = args.K, args.T
+    rng = np.random.default_rng(7)
+    eps = (rng.standard_normal((K, T, 2)) * np.sqrt(20.0)).astype(np.float32)
+    lam = 100.0
+    t0 = time.perf_counter()
+    n = 0
+    while True:
+        S = coracle.rollout_costs(x0, u, eps, window, 0.006, lam, 0.98, np.eye(2) * 20.0,
+                                  [0.5, 0.5, 5.0, 5.0], [5.0, 5.0, 50.0, 50.0], arm)
+        coracle.weighted_noise(S, eps, lam)
+        n += 1
+        el = time.perf_counter() - t0
+        if el >= args.cpu_seconds:
+            break
+    return {"value": K * T * n / el, "unit": "state-steps/s", "cores": coracle.max_threads(),
+            "kind": "port",
+            "sample": f"{n} full steps of K={K} T={T} (rollout+cost+softmin+weighted noise), "
+                      f"C fp64 restatement oracle/mppi_oracle.c, OpenMP, {el:.1f} s"}
+
+
+def main():
+    args = parse()
+    rank = int(os.environ.get("RANK", "0"))
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    torch.cuda.set_device(local_rank)
+    if world > 1:
+        import torch.distributed as dist
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
+    K, T = args.K, args.T
+    K_total, k_offset = K * world, K * rank
+    eng = RolloutEngine(K, T, 0.006, 100.0, 0.98, np.eye(2) * 20.0, [0.5, 0.5, 5.0, 5.0],
+                        [5.0, 5.0, 50.0, 50.0], 0.0, ArmParams(), K_total=K_total, k_offset=k_offset,
+                        device=local_rank, lanes_per_sample=args.lps)
+    path = np.load(os.path.join(ROOT, "tests", "golden", "paths.npz"))["xydq_circle"][:, :4]
+    window = path[0:30]
+    x0 = X0_RUNPY.copy()
+    u = np.array([[10.0, -2.0]] * T)
+    eng.set_step_inputs(x0, window, u)
+    noise = [eng.philox_noise(1234, i) for i in range(args.nbuf)]
+    partial = eng.new_partial()
+    gathered = torch.empty(world * eng.partial_len, dtype=torch.float64, device=eng.device)
+    stream = torch.cuda.current_stream()
+
+    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(args.steps)]
+
+    def step(i, timed=False):
+        if timed:
+            ev[i][0].record(stream)
+        if world == 1:
+            eng.rollout(noise[i % args.nbuf], fused_update=True)
+            if timed:
+                ev[i][1].record(stream)
+        else:
+            eng.rollout(noise[i % args.nbuf], partial_out=partial)
+            if timed:
+                ev[i][1].record(stream)
+            dist.all_gather_into_tensor(gathered, partial)
+            eng.merge(gathered, world, fused_update=True)
+
+    for i in range(args.warmup):
+        step(i)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for i in range(args.steps):
+        step(i, timed=True)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    elapsed = time.perf_counter() - t0
+    kern_ms = sum(a.elapsed_time(b) for a, b in ev) / args.steps
+    if world > 1:
+        tt = torch.tensor([elapsed, kern_ms], dtype=torch.float64, device=eng.device)
+        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+        elapsed, kern_ms = float(tt[0]), float(tt[1])
+    u_final = eng.nominal()
+    assert np.all(np.isfinite(u_final)), "non-finite nominal control"
+
+    if rank == 0:
+        ms_per_step = elapsed * 1e3 / args.steps
+        value = K_total * T * args.steps / elapsed
+        alg_bytes = BYTES_PER_STATE_STEP * K * T
+        achieved = alg_bytes / (kern_ms * 1e-3) / 1e9
+        traffic = None
+        if os.path.exists(args.traffic_json):
+            try:
+                tj = json.load(open(args.traffic_json))
+                if tj.get("K") == K and tj.get("T") == T:
+                    traffic = tj.get("hbm_bytes_per_launch")
+            except Exception:
+                traffic = None
+        out = {
+            "metric": "MPPI rollouts/sec (K×T state-steps/s) + control-step latency, K=65536 T=64",
+            "value": value,
+            "unit": "state-steps/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": ms_per_step,
+            "rollouts_per_s": K_total * args.steps / elapsed,
+            "control_step_latency_ms": ms_per_step,
+            "kernel_ms": kern_ms,
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "f32",
+            "data": "synthetic",
+            "config": {"workload": f"2-DoF arm MPPI step, K={K_total} (K/GPU={K}) T={T}, run.py constants, "
+                                   f"xydq_circle.txt window, Philox N(0,20I) noise x{args.nbuf} buffers",
+                       "K_total": K_total, "K_per_gpu": K, "T": T, "lanes_per_sample": eng.lanes_per_sample,
+                       "parallelism": f"samples sharded x{world}, RCCL all_gather of partials" if world > 1
+                       else "single device, fused update"},
+            "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                         "frac": achieved / HBM_PEAK_GBS, "traffic": traffic},
+        }
+        if world == 1 and args.cpu_seconds > 0:
+            out["cpu_baseline"] = cpu_baseline(args, window, x0, u)
+        print(json.dumps(out))
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,131 @@
+/* mppi_rocm.h — C ABI of the MI355X (gfx950) MPPI rollout-and-reduce engine.
+ *
+ * Drop-in boundary.  The reference (junofficial/mppi_RobotArm) has no FFI: its
+ * boundary is the Python method
+ *     MPPIControllerForPathTracking.calc_control_input(observed_x)
+ *         -> (u0, u_seq, optimal_traj, sampled_traj_list)          control.py:67-152
+ * The Python mirror of that class (mppi_robotarm_amd/controller.py) keeps the
+ * O(T) host work of control.py:70-78 and :120-152 and calls the entry points
+ * below for the O(K*T) work of control.py:81-118 (ctypes stub: INTEGRATION.md).
+ *
+ * Conventions: plain C types only.  Device buffers are raw device pointers
+ * (the Python side holds them as PyTorch-ROCm tensors); `stream` is a
+ * hipStream_t passed as void*.  Every call returns 0 on success or a negative
+ * MPPI_E_* code; mppi_last_error() returns the message of the calling thread's
+ * last failure.  Calls on one context are serialised on its stream; a context
+ * is not re-entrant (the reference controller is stateful and single-threaded,
+ * control.py:59,65).
+ */
+#ifndef MPPI_ROCM_H
+#define MPPI_ROCM_H
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define MPPI_MAX_T 128       /* horizon limit of the device parameter block          */
+#define MPPI_SEARCH_LEN 30   /* waypoints per search window, control.py:203           */
+
+#define MPPI_OK 0
+#define MPPI_E_ARG -1        /* bad argument (shape, null pointer, range)             */
+#define MPPI_E_HIP -2        /* HIP runtime error (message says which call)            */
+#define MPPI_E_SINGULAR -3   /* singular Sigma: the reference raises LinAlgError at   */
+                             /* control.py:106 (np.linalg.inv)                          */
+
+/* rollout flags */
+#define MPPI_FLAG_FUSED_UPDATE 1u  /* last workgroup also runs median filter, u += w_eps, */
+                                   /* shift (control.py:122-149) on device                */
+
+/* Arm constants.  m1..g: sys_params.py:1-13, read by _F (control.py:11-18,
+ * 241-251).  fk_l1/fk_l2: the link lengths the cost's forward kinematics uses,
+ * self.l1 = self.l2 = 1 (control.py:55-56, 178-179, 205-206) — kept separate. */
+typedef struct {
+    double m1, m2, l1, l2, lc1, lc2, g;
+    double fk_l1, fk_l2;
+} mppi_arm_params;
+
+/* Constructor arguments of MPPIControllerForPathTracking (control.py:21-35)
+ * plus the shard geometry of this device. */
+typedef struct {
+    int K_local;               /* samples simulated on this device                     */
+    int T;                     /* horizon_step_T, 1..MPPI_MAX_T                        */
+    int K_total;               /* number_of_samples_K over all devices                 */
+    int k_offset;              /* global index of this device's first sample            */
+    double delta_t;            /* control.py:53                                         */
+    double param_lambda;       /* control.py:43                                         */
+    double param_alpha;        /* control.py:44; gamma = lambda (1 - alpha), :45        */
+    double param_exploration;  /* control.py:42,98                                      */
+    double sigma[4];           /* row-major 2x2 noise covariance, control.py:46         */
+    double stage_cost_weight[4];
+    double terminal_cost_weight[4];
+    mppi_arm_params arm;
+    int lanes_per_sample;      /* 0 = auto (1, 2 or 4 lanes of a wave per sample)      */
+} mppi_config;
+
+typedef struct mppi_ctx mppi_ctx;
+
+/* Context: device scratch (workgroup partial slabs, arrival counter, step
+ * parameter block) is allocated here; no call below allocates.  Fails with
+ * MPPI_E_SINGULAR for a singular Sigma. */
+int mppi_ctx_create(const mppi_config *cfg, int device, void *stream, mppi_ctx **out);
+void mppi_ctx_destroy(mppi_ctx *ctx);
+const char *mppi_last_error(void);
+int mppi_set_stream(mppi_ctx *ctx, void *stream);
+int mppi_ctx_info(const mppi_ctx *ctx, int *lanes_per_sample, int *blocks, int *threads_per_block);
+
+/* Per control step inputs (control.py:70-75): observed state x0[4], the search
+ * window ref_path[prev:prev+W, 0:4] (W = min(30, N - prev), row-major W x 4),
+ * and the nominal control sequence u[T][2] (self.u_prev).  Async H2D on the
+ * context stream from a pinned staging block.  u may be NULL to keep the
+ * device-resident nominal (device closed loop, MPPI_FLAG_FUSED_UPDATE). */
+int mppi_set_step_inputs(mppi_ctx *ctx, const double *x0, const double *window, int W,
+                         const double *u);
+
+/* The hot path, control.py:81-118, one launch:
+ *   noise_dev   fp32 device noise eps[t][k][d] for this device's samples,
+ *               layout [T][K_local][2] (time-major: each step is one coalesced row);
+ *   S_dev       optional fp64 [K_local] per-sample cost S (control.py:81-109);
+ *   partial_dev optional fp64 [2 + 2T] device partial {rho, eta, N[T][2]} with
+ *               rho = min S, eta = sum exp(-(S-rho)/lambda), N = sum exp(.) eps —
+ *               the operand of the cross-device exchange;
+ *   flags       MPPI_FLAG_FUSED_UPDATE: finish the step on device (single device).
+ * The weighted noise w_eps = N / eta (control.py:112-118) is left in the
+ * context (mppi_get_weighted_noise). */
+int mppi_rollout(mppi_ctx *ctx, const float *noise_dev, double *S_dev, double *partial_dev,
+                 unsigned flags);
+
+/* Merge n device partials (fp64 [n][2 + 2T], e.g. the all-gather of every
+ * rank's partial_dev) with a log-sum-exp rescale into w_eps; with
+ * MPPI_FLAG_FUSED_UPDATE also run the update of control.py:122-149 on device. */
+int mppi_merge_partials(mppi_ctx *ctx, const double *partials_dev, int n, unsigned flags);
+
+/* D2H (synchronising) reads of the last step's results. */
+int mppi_get_weighted_noise(mppi_ctx *ctx, double *w_eps_host /* [T][2] */);
+int mppi_get_nominal(mppi_ctx *ctx, double *u_host /* [T][2] */);
+
+/* Trajectory re-roll (control.py:129-145), fp32 states out_dev[K][T][4] for
+ * samples [0, K) of this device:  control(t) = base[(t + T - 1) % T]
+ *   (+ eps[(t + T - 1) % T][k] if noise_dev != NULL, exploitation split as
+ *   control.py:98), i.e. the reference's off-by-one u[t-1] / v[k, t-1].
+ * base_u: host fp64 [T][2], or NULL for the nominal uploaded by the last
+ * mppi_set_step_inputs (the pre-update u of the sampled re-roll). */
+int mppi_rollout_traj(mppi_ctx *ctx, const double *base_u, const float *noise_dev, int K,
+                      float *out_dev);
+
+/* Counter-based Philox4x32-10 Gaussian noise with covariance Sigma (replaces
+ * np.random.multivariate_normal, control.py:163, for device-resident runs; not
+ * bit-equal to NumPy).  Values depend only on (seed, step, t, global k), so a
+ * shard generates exactly its slice of the unsharded draw.  Layout [T][K_local][2]. */
+int mppi_noise_philox(mppi_ctx *ctx, unsigned long long seed, unsigned long long step,
+                      float *out_dev);
+
+int mppi_sync(mppi_ctx *ctx);
+
+/* Diagnostics: in a -DMPPI_STAMPS build the rollout kernel writes a per-workgroup
+ * timeline (8 uint64 per workgroup) to dbg_dev; product builds ignore it. */
+int mppi_debug_set_buffer(mppi_ctx *ctx, void *dbg_dev);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* MPPI_ROCM_H */

@@ -1,0 +1,93 @@
+"""ctypes binding of the C ABI in ``include/mppi_rocm.h`` (libmppi_rocm.so).
+
+The library is built in-tree by ``mppi_robotarm_amd.build.build_native()``
+(``hipcc --offload-arch=gfx950``).  There is no fallback: if the shared object
+is missing or does not load, importing the engine raises, loudly.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.environ.get("MPPI_LIB_PATH") or os.path.join(HERE, "_lib", "libmppi_rocm.so")
+
+MPPI_MAX_T = 128
+MPPI_SEARCH_LEN = 30
+MPPI_OK = 0
+MPPI_E_ARG = -1
+MPPI_E_HIP = -2
+MPPI_E_SINGULAR = -3
+MPPI_FLAG_FUSED_UPDATE = 1
+
+# every symbol the header declares (tests check the library exports all of them)
+EXPORTS = (
+    "mppi_ctx_create", "mppi_ctx_destroy", "mppi_last_error", "mppi_set_stream", "mppi_ctx_info",
+    "mppi_set_step_inputs", "mppi_rollout", "mppi_merge_partials", "mppi_get_weighted_noise",
+    "mppi_get_nominal", "mppi_rollout_traj", "mppi_noise_philox", "mppi_sync", "mppi_debug_set_buffer",
+)
+
+
+class ArmParamsC(C.Structure):
+    _fields_ = [(n, C.c_double) for n in ("m1", "m2", "l1", "l2", "lc1", "lc2", "g", "fk_l1", "fk_l2")]
+
+
+class ConfigC(C.Structure):
+    _fields_ = [
+        ("K_local", C.c_int), ("T", C.c_int), ("K_total", C.c_int), ("k_offset", C.c_int),
+        ("delta_t", C.c_double), ("param_lambda", C.c_double), ("param_alpha", C.c_double),
+        ("param_exploration", C.c_double), ("sigma", C.c_double * 4),
+        ("stage_cost_weight", C.c_double * 4), ("terminal_cost_weight", C.c_double * 4),
+        ("arm", ArmParamsC), ("lanes_per_sample", C.c_int),
+    ]
+
+
+class MPPIError(RuntimeError):
+    """A failed C-ABI call (message from mppi_last_error)."""
+
+
+_lib = None
+
+
+def load():
+    """Load libmppi_rocm.so (raises OSError if it is missing — no fallback)."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIB_PATH):
+        raise OSError(f"{LIB_PATH} is missing: build it with `python -c 'import __graft_entry__ as g; g.build()'`")
+    L = C.CDLL(LIB_PATH)
+    vp, dp, fp, ip = C.c_void_p, C.POINTER(C.c_double), C.c_void_p, C.POINTER(C.c_int)
+    sig = {
+        "mppi_ctx_create": ([C.POINTER(ConfigC), C.c_int, vp, C.POINTER(vp)], C.c_int),
+        "mppi_ctx_destroy": ([vp], None),
+        "mppi_last_error": ([], C.c_char_p),
+        "mppi_set_stream": ([vp, vp], C.c_int),
+        "mppi_ctx_info": ([vp, ip, ip, ip], C.c_int),
+        "mppi_set_step_inputs": ([vp, dp, dp, C.c_int, dp], C.c_int),
+        "mppi_rollout": ([vp, fp, vp, vp, C.c_uint], C.c_int),
+        "mppi_merge_partials": ([vp, vp, C.c_int, C.c_uint], C.c_int),
+        "mppi_get_weighted_noise": ([vp, dp], C.c_int),
+        "mppi_get_nominal": ([vp, dp], C.c_int),
+        "mppi_rollout_traj": ([vp, dp, fp, C.c_int, fp], C.c_int),
+        "mppi_noise_philox": ([vp, C.c_ulonglong, C.c_ulonglong, fp], C.c_int),
+        "mppi_sync": ([vp], C.c_int),
+        "mppi_debug_set_buffer": ([vp, vp], C.c_int),
+    }
+    for name, (args, res) in sig.items():
+        fn = getattr(L, name)
+        fn.argtypes = args
+        fn.restype = res
+    _lib = L
+    return L
+
+
+def check(rc: int, what: str) -> None:
+    if rc != MPPI_OK:
+        msg = load().mppi_last_error().decode(errors="replace")
+        if rc == MPPI_E_SINGULAR:
+            import numpy as np
+            raise np.linalg.LinAlgError(msg)
+        if rc == MPPI_E_ARG:
+            raise ValueError(f"{what}: {msg}")
+        raise MPPIError(f"{what} failed ({rc}): {msg}")

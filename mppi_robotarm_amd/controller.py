@@ -1,0 +1,235 @@
+"""Drop-in ``MPPIControllerForPathTracking`` backed by the MI355X engine.
+
+Same constructor arguments (control.py:21-35, including the ``visualze``
+spelling), same ``calc_control_input(observed_x)`` contract (control.py:67-152):
+
+  * host, fp64 NumPy (O(T) work, exactly as the reference):
+      nearest-waypoint update + end-of-path ``IndexError`` (control.py:75-78),
+      noise draw ``np.random.multivariate_normal`` on the legacy global RNG
+      (control.py:154-164, same stream as the reference),
+      ``np.linalg.inv(Sigma)`` (``LinAlgError`` as at control.py:106),
+      median filter via ``scipy.ndimage.median_filter`` (control.py:319-327),
+      ``u += w_eps`` in place, shift, and the aliasing return
+      (``u0`` is a view of the shifted ``u_prev``; ``u_seq is self.u_prev``);
+  * device, HIP (O(K*T) work): rollouts, costs, soft-min weights, weighted
+    noise sum (control.py:81-118) and the trajectory re-rolls
+    (control.py:129-145).
+
+Extra keyword arguments (all optional): ``device``, ``verbose`` (the three
+progress prints of control.py:227-229, on by default like the reference),
+``noise`` ("numpy" = reference RNG stream, or "device" = on-device Philox),
+``seed`` (device noise), ``lanes_per_sample``, ``arm`` (ArmParams) and
+``process_group`` (shard the samples over the ranks of a torch.distributed
+group; one RCCL all-gather of the per-device partials per step).
+"""
+from __future__ import annotations
+
+from typing import Tuple
+
+import numpy as np
+import torch
+from scipy.ndimage import median_filter
+
+from .engine import RolloutEngine
+from .params import ArmParams
+
+SEARCH_IDX_LEN = 30  # control.py:203
+
+
+class MPPIControllerForPathTracking:
+    def __init__(
+            self,
+            delta_t: float = 0.01,
+            ref_path: float = 0,
+            horizon_step_T: int = 20,
+            number_of_samples_K: int = 500,
+            param_exploration: float = 0.0,
+            param_lambda: float = 50.0,
+            param_alpha: float = 1.0,
+            sigma: np.ndarray = np.array([[10.0, 10.0], [100.0, 100.0]]),
+            stage_cost_weight: np.ndarray = np.array([10.0, 10.0, 10.0, 10.0]),
+            terminal_cost_weight: np.ndarray = np.array([10.0, 10.0, 10.0, 10.0]),
+            visualize_optimal_traj=True,
+            visualze_sampled_trajs=False,
+            *,
+            device: int | None = None,
+            verbose: bool = True,
+            noise: str = "numpy",
+            seed: int = 0,
+            lanes_per_sample: int = 0,
+            arm: ArmParams | None = None,
+            process_group=None,
+    ) -> None:
+        self.dim_x = 4
+        self.dim_u = 2
+        self.T = horizon_step_T
+        self.K = number_of_samples_K
+        self.param_exploration = param_exploration
+        self.param_lambda = param_lambda
+        self.param_alpha = param_alpha
+        self.param_gamma = self.param_lambda * (1.0 - (self.param_alpha))
+        self.Sigma = sigma
+        self.stage_cost_weight = stage_cost_weight
+        self.terminal_cost_weight = terminal_cost_weight
+        self.visualize_optimal_traj = visualize_optimal_traj
+        self.visualze_sampled_trajs = visualze_sampled_trajs
+        self.delta_t = delta_t
+        self.ref_path = ref_path
+        self.l1 = 1
+        self.l2 = 1
+        self.u_prev = np.array([[10.0, -2.0] for i in range(self.T)])
+        self.prev_waypoints_idx = 0
+
+        if noise not in ("numpy", "device"):
+            raise ValueError("noise must be 'numpy' or 'device'")
+        self.verbose = verbose
+        self.noise_source = noise
+        self.seed = int(seed)
+        self.arm = ArmParams(fk_l1=float(self.l1), fk_l2=float(self.l2)) if arm is None else arm
+        self.process_group = process_group
+        self._lanes_per_sample = lanes_per_sample
+        self._device = device
+        self._engine = None
+        self._step_count = 0
+        self.keep_costs = False        # set True to keep per-sample S (self.last_S)
+        self.last_S = None
+
+    # ------------------------------------------------------------ engine
+    def _shard(self):
+        if self.process_group is None:
+            return 1, 0
+        import torch.distributed as dist
+        return dist.get_world_size(self.process_group), dist.get_rank(self.process_group)
+
+    def _get_engine(self) -> RolloutEngine:
+        if self._engine is None:
+            world, rank = self._shard()
+            if self.K < world:
+                raise ValueError("number_of_samples_K must be >= the number of ranks")
+            base, rem = divmod(self.K, world)
+            K_local = base + (1 if rank < rem else 0)
+            k_offset = rank * base + min(rank, rem)
+            device = self._device if self._device is not None else torch.cuda.current_device()
+            self._engine = RolloutEngine(
+                K_local, self.T, self.delta_t, self.param_lambda, self.param_alpha, self.Sigma,
+                self.stage_cost_weight, self.terminal_cost_weight, self.param_exploration, self.arm,
+                K_total=self.K, k_offset=k_offset, device=device, lanes_per_sample=self._lanes_per_sample)
+            self._noise_dev = self._engine.new_noise()
+            self._partial = self._engine.new_partial()
+            self._S_dev = torch.empty(K_local, dtype=torch.float64, device=self._engine.device)
+            if world > 1:
+                self._gathered = torch.empty(world * self._engine.partial_len, dtype=torch.float64,
+                                             device=self._engine.device)
+        return self._engine
+
+    # ------------------------------------------------------------ API
+    def calc_control_input(self, observed_x: np.ndarray) -> Tuple[float, np.ndarray]:
+        """calculate optimal control input (control.py:67-152)"""
+        u = self.u_prev
+        x0 = observed_x
+        self._get_nearest_waypoint(x0[0], x0[1], update_prev_idx=True)
+        if self.prev_waypoints_idx >= self.ref_path.shape[0] - 1:
+            print("[ERROR] Reached the end of the reference path.")
+            raise IndexError
+        if self.K < 1:
+            raise ValueError("zero-size array to reduction operation minimum which has no identity")
+
+        if self.noise_source == "numpy":
+            epsilon = self._calc_epsilon(self.Sigma, self.K, self.T, self.dim_u)
+        else:
+            epsilon = None
+            self._check_sigma(self.Sigma, self.dim_u)
+        np.linalg.inv(self.Sigma)                          # LinAlgError exactly as control.py:106
+        eng = self._get_engine()
+        if epsilon is not None:
+            lo = eng.k_offset
+            eng.upload_noise(epsilon[lo:lo + eng.K_local], out=self._noise_dev)
+        else:
+            eng.philox_noise(self.seed, self._step_count, out=self._noise_dev)
+        self._step_count += 1
+
+        window = self.ref_path[self.prev_waypoints_idx:(self.prev_waypoints_idx + SEARCH_IDX_LEN)]
+        eng.set_step_inputs(np.asarray(x0, dtype=np.float64), window, u)
+        world, _ = self._shard()
+        if world == 1:
+            eng.rollout(self._noise_dev, S_out=self._S_dev if self.keep_costs else None)
+        else:
+            import torch.distributed as dist
+            eng.rollout(self._noise_dev, S_out=self._S_dev if self.keep_costs else None, partial_out=self._partial)
+            dist.all_gather_into_tensor(self._gathered, self._partial, group=self.process_group)
+            eng.merge(self._gathered, world)
+        w_epsilon = eng.weighted_noise()
+        if self.keep_costs:
+            self.last_S = self._S_dev.cpu().numpy()
+
+        w_epsilon = self._moving_median_filter(xx=w_epsilon, window_size=10)
+        u += w_epsilon
+
+        optimal_traj = np.zeros((self.T, self.dim_x))
+        if self.visualize_optimal_traj:
+            optimal_traj = eng.trajectories(base_u=u, K=1)[0].double().cpu().numpy()
+
+        sampled_traj_list = np.zeros((self.K, self.T, self.dim_x))
+        if self.visualze_sampled_trajs:
+            tr = eng.trajectories(base_u=None, noise=self._noise_dev)   # pre-update u, v[k, t-1]
+            if world > 1:
+                import torch.distributed as dist
+                parts = [None] * world
+                dist.all_gather_object(parts, (eng.k_offset, tr.cpu().numpy()), group=self.process_group)
+                for off, arr in parts:
+                    sampled_traj_list[off:off + arr.shape[0]] = arr
+            else:
+                sampled_traj_list[:] = tr.double().cpu().numpy()
+
+        self.u_prev[:-1] = u[1:]
+        self.u_prev[-1] = u[-1]
+        return u[0], u, optimal_traj, sampled_traj_list
+
+    # ------------------------------------------------------------ host helpers (reference semantics)
+    @staticmethod
+    def _check_sigma(sigma, size_dim_u):
+        if sigma.shape[0] != sigma.shape[1] or sigma.shape[0] != size_dim_u or size_dim_u < 1:
+            print("[ERROR] sigma must be a square matrix with the size of size_dim_u.")
+            raise ValueError
+
+    def _calc_epsilon(self, sigma: np.ndarray, size_sample: int, size_time_step: int, size_dim_u: int) -> np.ndarray:
+        """sample epsilon (control.py:154-164) — the reference's RNG stream"""
+        self._check_sigma(sigma, size_dim_u)
+        mu = np.full((size_dim_u), 0.0)
+        return np.random.multivariate_normal(mu, sigma, (size_sample, size_time_step))
+
+    def _g(self, v: np.ndarray) -> float:
+        """clamp input (disabled in the reference, control.py:166-172)"""
+        return v
+
+    def _get_nearest_waypoint(self, q1: float, q2: float, update_prev_idx: bool = False):
+        """search the closest waypoint (control.py:200-232), host fp64"""
+        prev_idx = self.prev_waypoints_idx
+        x = self.l1 * np.cos(q1) + self.l2 * np.cos(q1 + q2)
+        y = self.l1 * np.sin(q1) + self.l2 * np.sin(q1 + q2)
+        win = self.ref_path[prev_idx:(prev_idx + SEARCH_IDX_LEN)]
+        d = ((x - win[:, 0]) ** 2 + (y - win[:, 1]) ** 2) * 100
+        nearest_idx = int(np.argmin(d)) + prev_idx
+        ref_x = self.ref_path[nearest_idx, 0]
+        ref_y = self.ref_path[nearest_idx, 1]
+        ref_dq1 = self.ref_path[nearest_idx, 2]
+        ref_dq2 = self.ref_path[nearest_idx, 3]
+        if update_prev_idx:
+            if self.verbose:
+                print(f"0     prev_idx = {prev_idx}")
+                print(f"0     nearest_idx = {nearest_idx}")
+                print("======================updated=======================")
+            self.prev_waypoints_idx = nearest_idx
+        return nearest_idx, ref_x, ref_y, ref_dq1, ref_dq2
+
+    def _moving_median_filter(self, xx: np.ndarray, window_size: int) -> np.ndarray:
+        """median smoothing per input dimension (control.py:319-327)"""
+        out = np.zeros(xx.shape)
+        for d in range(xx.shape[1]):
+            out[:, d] = median_filter(xx[:, d], size=window_size, mode='reflect')
+        return out
+
+    def close(self):
+        if self._engine is not None:
+            self._engine.close()
+            self._engine = None

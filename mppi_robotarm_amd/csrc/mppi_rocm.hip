@@ -1,0 +1,994 @@
+// mppi_rocm.hip — MI355X (gfx950, CDNA4) MPPI rollout-and-reduce engine.
+//
+// The hot path of junofficial/mppi_RobotArm control.py:81-118 (K samples x T
+// steps of: Gaussian control perturbation -> 2-link arm forward dynamics
+// (_F, control.py:234-263) -> windowed nearest-waypoint stage cost (_c /
+// _get_nearest_waypoint, control.py:174-232) + control cost (control.py:106)
+// -> terminal cost (control.py:109) -> soft-min weights (control.py:297-314)
+// -> weighted noise sum (control.py:115-118)), written for CDNA4 directly:
+//
+//  * rollout_kernel<LPS>: LPS lanes of a 64-wide wave per sample (1, 2 or 4).
+//    The serial T loop runs per lane in fp32 registers; the 30-waypoint
+//    argmin is split over the LPS lanes of a sample and closed with DPP
+//    quad_perm min (no LDS, no MFMA: the work is element-wise VALU).  The
+//    per-step noise row eps[t][k][:] is one coalesced 8-B-per-lane load,
+//    prefetched two steps ahead.  S accumulates in fp64.
+//  * the block epilogue turns its samples into a log-sum-exp partial
+//    {rho_b, eta_b, N_b[T][2]} (only samples with non-zero weight are
+//    visited), publishes it with an agent-scope release + arrival counter,
+//    and the last-arriving workgroup merges every partial (agent acquire),
+//    so one launch covers control.py:81-118.  With MPPI_FLAG_FUSED_UPDATE
+//    that workgroup also applies the median filter / update / shift of
+//    control.py:122-149 into the ping-pong step block for the next launch.
+//  * merge_kernel: the same merge over the all-gathered per-device partials
+//    (multi-GPU), traj_kernel: trajectory re-roll (control.py:129-145),
+//    philox_noise_kernel: counter-based Gaussian noise.
+//
+// C ABI: include/mppi_rocm.h.
+#include <hip/hip_runtime.h>
+
+#include <math.h>
+#include <stdint.h>
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+
+#include <string>
+
+#include "mppi_rocm.h"
+
+namespace {
+
+constexpr int kThreads = 256;
+constexpr int kMaxT = MPPI_MAX_T;
+constexpr int kSlots = 32;  // window slots (>= MPPI_SEARCH_LEN), index fits 5 bits
+constexpr float kPadKey = 1.0e30f;
+
+// Device-resident per-step parameter block (ping-pong pair in the context).
+struct alignas(16) DevStep {
+    float4 win[kSlots];   // rx, ry, rdq1, rdq2 of window slot j (lookup after argmin)
+    float4 key[kSlots];   // rx', ry', c' = rx'^2 + ry'^2 (centred), 0; pads c' = 1e30
+    float4 x0;            // q1, q2, dq1, dq2
+    float4 ctr;           // window centre (cx, cy), W, unused
+    float4 ua[kMaxT];     // u0, u1, a0, a1 (a = (gamma u_t)^T Sigma^-1), fp32
+    double u[kMaxT][2];   // nominal control sequence, fp64 (device closed loop)
+};
+
+// Launch constants (kernel argument, by value).
+struct KConst {
+    int K_local, T, k_offset, k_exploit, nblocks, pad0;
+    float dt, fk1, fk2;
+    float A, B, D, E, P, Q;          // dynamics coefficients (see dyn_step)
+    float sw[4], tw[4];              // stage / terminal weights x 10000
+    double lambda, inv_lambda, gamma;
+    double sig_inv[4];
+};
+
+// ------------------------------------------------------------------ helpers
+
+// Hardware v_sin_f32 / v_cos_f32 (argument pre-scaled by 1/(2 pi)): 30 % faster
+// rollouts than OCML's sincosf at K=65536 T=64, parity unchanged (S rel-err
+// budget 5e-5 in tests/test_gpu_parity.py).  -DMPPI_ACCURATE_TRIG selects sincosf.
+__device__ __forceinline__ void sincos_f32(float x, float* s, float* c) {
+#ifdef MPPI_ACCURATE_TRIG
+    sincosf(x, s, c);
+#else
+    __sincosf(x, s, c);
+#endif
+}
+
+template <int CTRL>
+__device__ __forceinline__ float dpp_f32(float v) {
+    return __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), CTRL, 0xF, 0xF, false));
+}
+
+__device__ __forceinline__ int lanes_below(unsigned long long mask) {
+    return __builtin_amdgcn_mbcnt_hi((unsigned)(mask >> 32),
+                                     __builtin_amdgcn_mbcnt_lo((unsigned)mask, 0u));
+}
+
+__device__ __forceinline__ double wave_min_f64(double v) {
+    for (int o = 32; o > 0; o >>= 1) v = fmin(v, __shfl_xor(v, o));
+    return v;
+}
+
+__device__ __forceinline__ double wave_sum_f64(double v) {
+    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
+    return v;
+}
+
+// One semi-implicit Euler step of _F (control.py:234-263) in closed form:
+//   M = [[A + B c2, D + E c2], [D + E c2, D]]   (M22 = m2 lc2^2 + l2 = D)
+//   h = E s2,  G = [P c1 + Q c12, Q c12],  C dq = [-h dq2 (2 dq1 + dq2), h dq1^2]
+//   ddq = M^-1 (v - C dq - G);  dq += ddq dt;  q += dq dt
+// c2/s2 come from the angle-difference identities of the cached sincos of
+// q1 and q1 + q2, so each step evaluates exactly two sincos (of the NEW q),
+// which the next step's dynamics and this step's kinematics share.
+struct ArmState {
+    float q1, q2, dq1, dq2;
+    float s1, c1, s12, c12;
+};
+
+__device__ __forceinline__ void dyn_step(ArmState& x, float v1, float v2, const KConst& c) {
+    const float c2 = fmaf(x.c12, x.c1, x.s12 * x.s1);
+    const float s2 = fmaf(x.s12, x.c1, -x.c12 * x.s1);
+    const float M11 = fmaf(c.B, c2, c.A);
+    const float M12 = fmaf(c.E, c2, c.D);
+    const float h = c.E * s2;
+    const float G2 = c.Q * x.c12;
+    const float G1 = fmaf(c.P, x.c1, G2);
+    const float r1 = fmaf(h * x.dq2, fmaf(2.f, x.dq1, x.dq2), v1 - G1);
+    const float r2 = fmaf(-h * x.dq1, x.dq1, v2 - G2);
+    const float det = fmaf(M11, c.D, -M12 * M12);
+    const float rdet = __builtin_amdgcn_rcpf(det);
+    const float ddq1 = fmaf(c.D, r1, -M12 * r2) * rdet;
+    const float ddq2 = fmaf(M11, r2, -M12 * r1) * rdet;
+    x.dq1 = fmaf(ddq1, c.dt, x.dq1);
+    x.dq2 = fmaf(ddq2, c.dt, x.dq2);
+    x.q1 = fmaf(x.dq1, c.dt, x.q1);
+    x.q2 = fmaf(x.dq2, c.dt, x.q2);
+    sincos_f32(x.q1, &x.s1, &x.c1);
+    sincos_f32(x.q1 + x.q2, &x.s12, &x.c12);
+}
+
+// --------------------------------------------------- merge + update helpers
+
+constexpr int kMaxWaves = 16;       // up to 1024-thread workgroups
+constexpr int kMergeChunk = 1024;
+constexpr int kGroup = 16;          // workgroups per first-level merge group
+// A partial whose rescale factor s = exp((rho - rho_i) / lambda) is below 2^-64
+// changes eta and N by less than 2^-64 * 512 relative to the leading term
+// (which has s = 1 and eta >= 1): far below the fp64 resolution of the result.
+constexpr double kMergeFloor = 5.421010862427522e-20;  // 2^-64
+
+// Rows {rho, eta, N[2T]} handed between workgroups of one launch travel
+// write-through: every store and every load of them is a `sc1` buffer access
+// (MI355X guide G16, "Valid forms" row 1), so neither side needs an
+// agent-scope fence (~1.7 us each) — only each storing wave's vmcnt drain, a
+// workgroup barrier and one relaxed agent atomic per workgroup.
+typedef unsigned int u32x2 __attribute__((__vector_size__(2 * sizeof(unsigned int))));
+constexpr int kSC1 = 16;  // buffer aux bit: sc1
+
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t rows_rsrc(const double* p, int bytes) {
+    return __builtin_amdgcn_make_buffer_rsrc(const_cast<double*>(p), 0, bytes, 0x00020000);
+}
+__device__ __forceinline__ double ld_wt(__amdgpu_buffer_rsrc_t r, int idx) {
+    return __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(r, idx * 8, 0, kSC1));
+}
+__device__ __forceinline__ void st_wt(__amdgpu_buffer_rsrc_t r, int idx, double v) {
+    __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u32x2, v), r, idx * 8, 0, kSC1);
+}
+
+struct MergeScratch {
+    double red[kMaxWaves];
+    int cnt[kMaxWaves];
+    int list_i[kMergeChunk];
+    double list_s[kMergeChunk];
+    double weps[2 * kMaxT];
+    double unew[2 * kMaxT];
+    double rho, eta;
+    int n, nrel;
+};
+
+template <int NT>
+__device__ __forceinline__ double block_min_f64(double v, MergeScratch& sm) {
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    v = wave_min_f64(v);
+    if (lane == 0) sm.red[wave] = v;
+    __syncthreads();
+    double r = sm.red[0];
+#pragma unroll
+    for (int w = 1; w < NT / 64; ++w) r = fmin(r, sm.red[w]);
+    __syncthreads();
+    return r;
+}
+
+// Merge n rows {rho, eta, N[2T]} (row stride 2 + 2T, read write-through from
+// `rows`) with a log-sum-exp rescale: rho = min rho_i,
+// s_i = exp((rho - rho_i) / lambda), eta = sum s_i eta_i, N = sum s_i N_i over
+// the rows with s_i >= 2^-64, in ascending row order (deterministic).
+// The merged row goes to out_wt (write-through, next merge level) or out_row
+// (plain, read after the launch); with `final`, w_eps = N / eta
+// (control.py:112-118) goes to sm.weps and w_eps_out.
+template <int NT>
+__device__ void merge_rows_block(__amdgpu_buffer_rsrc_t rows, int row0, int n, const KConst& c, MergeScratch& sm,
+                                 const __amdgpu_buffer_rsrc_t* out_wt, int out_idx, double* out_row, bool final,
+                                 double* w_eps_out) {
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int stride = 2 + 2 * c.T;
+    const int ncol = 2 * c.T + 1;  // col 0 = eta, col 1 + j = N[j]
+    double m = INFINITY;
+    for (int i = tid; i < n; i += NT) m = fmin(m, ld_wt(rows, (row0 + i) * stride));
+    const double rho = block_min_f64<NT>(m, sm);
+    if (tid == 0) sm.nrel = 0;
+    double acc0 = 0.0, acc1 = 0.0;  // columns tid and tid + NT (2T + 1 <= 257)
+    for (int chunk = 0; chunk < n; chunk += kMergeChunk) {
+        const int cend = min(n, chunk + kMergeChunk);
+        if (tid == 0) sm.n = 0;
+        __syncthreads();
+        for (int base = chunk; base < cend; base += NT) {
+            const int i = base + tid;
+            double s = 0.0;
+            if (i < cend) s = exp((rho - ld_wt(rows, (row0 + i) * stride)) * c.inv_lambda);
+            const bool keep = (i < cend) && (s >= kMergeFloor);
+            const unsigned long long bal = __ballot(keep);
+            if (lane == 0) sm.cnt[wave] = __popcll(bal);
+            __syncthreads();
+            int off = sm.n;
+            for (int w = 0; w < wave; ++w) off += sm.cnt[w];
+            if (keep) {
+                const int pos = off + lanes_below(bal);
+                sm.list_i[pos] = i;
+                sm.list_s[pos] = s;
+            }
+            __syncthreads();
+            if (tid == 0) {
+                int tot = sm.n;
+                for (int w = 0; w < NT / 64; ++w) tot += sm.cnt[w];
+                sm.n = tot;
+            }
+            __syncthreads();
+        }
+        const int nl = sm.n;
+        if (tid < ncol)
+            for (int l = 0; l < nl; ++l)
+                acc0 = fma(sm.list_s[l], ld_wt(rows, (row0 + sm.list_i[l]) * stride + 1 + tid), acc0);
+        if (tid + NT < ncol)
+            for (int l = 0; l < nl; ++l)
+                acc1 = fma(sm.list_s[l], ld_wt(rows, (row0 + sm.list_i[l]) * stride + 1 + tid + NT), acc1);
+        if (tid == 0) sm.nrel += nl;
+        __syncthreads();
+    }
+    auto put = [&](int col, double v) {  // col 0 = rho, 1 = eta, 2 + j = N[j]
+        if (out_wt) st_wt(*out_wt, out_idx * stride + col, v);
+        if (out_row) out_row[col] = v;
+    };
+    if (tid == 0) {
+        sm.eta = acc0;
+        put(0, rho);
+        put(1, acc0);
+    } else if (tid < ncol) {
+        sm.weps[tid - 1] = acc0;
+        put(1 + tid, acc0);
+    }
+    if (tid + NT < ncol) {
+        sm.weps[tid + NT - 1] = acc1;
+        put(1 + tid + NT, acc1);
+    }
+    __syncthreads();
+    if (final) {
+        const double eta = sm.eta;
+        for (int j = tid; j < 2 * c.T; j += NT) {
+            const double w = sm.weps[j] / eta;
+            sm.weps[j] = w;
+            if (w_eps_out) w_eps_out[j] = w;
+        }
+        __syncthreads();
+    }
+}
+
+// Arrive on `counter` after this workgroup's write-through stores; true in
+// every thread of the workgroup that arrived last (which re-arms the counter).
+template <int NT>
+__device__ __forceinline__ bool arrive_last(unsigned* counter, unsigned expected, unsigned* s_flag) {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every storing wave drains its sc1 stores
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        const unsigned prev = __hip_atomic_fetch_add(counter, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        const bool last = prev == expected - 1;
+        if (last) __hip_atomic_store(counter, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        *s_flag = last ? 1u : 0u;
+    }
+    __syncthreads();
+    return *s_flag != 0;
+}
+
+// Median filter (scipy.ndimage.median_filter(size=10, mode='reflect'),
+// control.py:319-327, valid for T >= 5), u += w_eps (control.py:126), shift
+// (control.py:148-149) and the fp32 per-step constants of the next launch.
+// u_cur: this thread's element cur->u[t][d] (t = tid / 2, d = tid % 2), read
+// at kernel entry.
+template <int NT>
+__device__ void nominal_update_block(const DevStep* cur, DevStep* nxt, const KConst& c, MergeScratch& sm,
+                                     double u_cur) {
+    const int tid = threadIdx.x;
+    const int T = c.T;
+    if (tid < 2 * T) {
+        const int t = tid >> 1, d = tid & 1;
+        double v[10];
+#pragma unroll
+        for (int i = 0; i < 10; ++i) {
+            int m = t - 5 + i;
+            m %= 2 * T;
+            if (m < 0) m += 2 * T;
+            if (m >= T) m = 2 * T - 1 - m;
+            v[i] = sm.weps[2 * m + d];
+        }
+        double med = v[0];
+#pragma unroll
+        for (int i = 0; i < 10; ++i) {  // element of rank 5 (upper median)
+            int less = 0, leq = 0;
+#pragma unroll
+            for (int j = 0; j < 10; ++j) {
+                less += v[j] < v[i];
+                leq += v[j] <= v[i];
+            }
+            if (less <= 5 && 5 < leq) med = v[i];
+        }
+        sm.unew[tid] = u_cur + med;
+    }
+    __syncthreads();
+    if (tid < T) {
+        const int src = tid + 1 < T ? tid + 1 : T - 1;
+        const double u0 = sm.unew[2 * src], u1 = sm.unew[2 * src + 1];
+        nxt->u[tid][0] = u0;
+        nxt->u[tid][1] = u1;
+        const double g0 = c.gamma * u0, g1 = c.gamma * u1;
+        const double a0 = g0 * c.sig_inv[0] + g1 * c.sig_inv[2];
+        const double a1 = g0 * c.sig_inv[1] + g1 * c.sig_inv[3];
+        nxt->ua[tid] = make_float4((float)u0, (float)u1, (float)a0, (float)a1);
+    }
+    if (tid < kSlots) {
+        nxt->win[tid] = cur->win[tid];
+        nxt->key[tid] = cur->key[tid];
+    }
+    if (tid == 0) {
+        nxt->x0 = cur->x0;
+        nxt->ctr = cur->ctr;
+    }
+}
+
+// ------------------------------------------------------------ rollout kernel
+
+// Noise row load for step t.  Each prefetch is followed by an empty asm
+// statement with a memory clobber: a scheduling boundary that keeps the load
+// where it is written (otherwise the scheduler sinks it next to its use and
+// every step pays the full memory latency).
+#ifdef MPPI_ABL_NONOISE  // diagnostic ablation: no noise traffic (wrong results)
+__device__ __forceinline__ float2 noise_ld(const float2* p) {
+    const unsigned a = (unsigned)(uintptr_t)p;
+    return make_float2((float)(a & 255u) * 0.01f - 1.2f, (float)((a >> 8) & 255u) * 0.01f - 1.2f);
+}
+#else
+__device__ __forceinline__ float2 noise_ld(const float2* p) { return *p; }
+#endif
+#define PIN_LOADS() asm volatile("" ::: "memory")
+
+// The per-step constants are read through the constant address space: scalar
+// (SMEM) loads that stay scalar across the scheduling boundaries above.  The
+// block is written only by host copies or by the PREVIOUS launch (ping-pong).
+typedef __attribute__((address_space(4))) const float cfloat;
+__device__ __forceinline__ float4 const_ld4(cfloat* p) { return make_float4(p[0], p[1], p[2], p[3]); }
+
+template <int LPS>
+struct Search {
+    static constexpr int SL = (MPPI_SEARCH_LEN + LPS - 1) / LPS;  // window slots per lane
+    float krx[SL], kry[SL], kc[SL];
+    int sub;
+    float cx, cy;
+
+    // Nearest waypoint of the shared window (control.py:208-215):
+    //   argmin_j |p - r_j|^2 = argmin_j (|r'_j|^2 - 2 p'.r'_j) (window-centred),
+    // the slot index packed into the 5 low mantissa bits so one min per slot
+    // carries the argmin; the LPS lanes of a sample close it with DPP.
+    __device__ __forceinline__ unsigned nearest(float px, float py) const {
+        const float ax = -2.f * (px - cx), ay = -2.f * (py - cy);
+        float best = 3.0e38f;
+#pragma unroll
+        for (int i = 0; i < SL; ++i) {
+            const float key = fmaf(ax, krx[i], fmaf(ay, kry[i], kc[i]));
+            const unsigned kb = (__float_as_uint(key) & ~31u) | (unsigned)(sub * SL + i);
+            best = fminf(best, __uint_as_float(kb));
+        }
+        if (LPS >= 2) best = fminf(best, dpp_f32<0xB1>(best));  // quad_perm xor 1
+        if (LPS >= 4) best = fminf(best, dpp_f32<0x4E>(best));  // quad_perm xor 2
+        return __float_as_uint(best) & 31u;
+    }
+};
+
+__device__ __forceinline__ float weighted_sq(float ex, float ey, float e1, float e2, const float* w) {
+    return fmaf(w[0], ex * ex, fmaf(w[1], ey * ey, fmaf(w[2], e1 * e1, w[3] * e2 * e2)));
+}
+
+// Diagnostic builds only (-DMPPI_STAMPS, a separate .so): per-workgroup
+// timeline in s_memrealtime ticks (100 MHz) + counters.  Never in the product.
+#ifdef MPPI_STAMPS
+#define STAMP(slot, val) do { if (dbg && threadIdx.x == 0) dbg[(size_t)blockIdx.x * 16 + (slot)] = (val); } while (0)
+#define NOW() __builtin_amdgcn_s_memrealtime()
+#else
+#define STAMP(slot, val) do { (void)dbg; } while (0)
+#define NOW() 0ull
+#endif
+
+constexpr int kPF = 4;  // noise rows in flight per lane
+
+template <int LPS, int NT>
+__global__ __launch_bounds__(NT) void rollout_kernel(
+    const KConst c, const DevStep* __restrict__ st, const float2* __restrict__ noise,
+    double* __restrict__ S_out, double* __restrict__ slab, double* __restrict__ gslab,
+    unsigned* __restrict__ counters, double* __restrict__ partial_out, double* __restrict__ w_eps_out,
+    DevStep* __restrict__ nxt, unsigned flags, unsigned long long* __restrict__ dbg) {
+    __shared__ float4 s_win[kSlots];
+    __shared__ float s_redf[NT / 64];
+    __shared__ int s_cnt[NT / 64];
+    __shared__ int s_k[NT];
+    __shared__ float s_e[NT];
+    __shared__ unsigned s_flag;
+    __shared__ MergeScratch sm;
+
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int k_raw = (blockIdx.x * NT + tid) / LPS;
+    const bool valid = k_raw < c.K_local;
+    const int k = valid ? k_raw : c.K_local - 1;
+    const float exf = (c.k_offset + k) < c.k_exploit ? 1.f : 0.f;  // control.py:98-101
+    const int K = c.K_local, T = c.T;
+
+    STAMP(0, NOW());
+#ifdef MPPI_STAMPS
+    STAMP(8, (unsigned long long)__builtin_amdgcn_s_getreg(0xF804));   // HW_ID
+    STAMP(9, (unsigned long long)__builtin_amdgcn_s_getreg(0xF814));   // XCC_ID
+#endif
+    // nominal element for the fused update, fetched now so its latency is hidden
+    const double u_cur = ((flags & MPPI_FLAG_FUSED_UPDATE) && tid < 2 * T) ? st->u[tid >> 1][tid & 1] : 0.0;
+    if (tid < kSlots) s_win[tid] = st->win[tid];
+    Search<LPS> sr;
+    if (LPS == 1) {
+        // lane-opaque zero: keeps the 30 window slots in VGPRs (as uniform
+        // values they would go to SGPRs and spill)
+        int z;
+        asm volatile("v_mov_b32 %0, 0" : "=v"(z));
+        sr.sub = z;
+    } else {
+        sr.sub = tid & (LPS - 1);
+    }
+#pragma unroll
+    for (int i = 0; i < Search<LPS>::SL; ++i) {
+        const float4 kk = st->key[sr.sub * Search<LPS>::SL + i];
+        sr.krx[i] = kk.x;
+        sr.kry[i] = kk.y;
+        sr.kc[i] = kk.z;
+    }
+    sr.cx = st->ctr.x;
+    sr.cy = st->ctr.y;
+    const float4 x0 = st->x0;
+    ArmState x;
+    x.q1 = x0.x;
+    x.q2 = x0.y;
+    x.dq1 = x0.z;
+    x.dq2 = x0.w;
+    sincos_f32(x.q1, &x.s1, &x.c1);
+    sincos_f32(x.q1 + x.q2, &x.s12, &x.c12);
+    const float2* np = noise + k;
+    cfloat* cua = (cfloat*)(st->ua);
+    float2 ring[kPF];   // noise rows eps[t][k] in flight
+    float4 uring[kPF];  // per-step constants (u_t, a_t), uniform
+#pragma unroll
+    for (int j = 0; j < kPF; ++j) {
+        const int tj = j < T ? j : T - 1;
+        ring[j] = noise_ld(np + (size_t)tj * K);
+        uring[j] = const_ld4(cua + 4 * tj);
+    }
+    __syncthreads();
+
+    // Horizon loop (control.py:95-109): v = u + eps -> _F -> end effector ->
+    // nearest waypoint -> stage cost + control cost, S in fp64.
+    double S = 0.0;
+    float ex = 0.f, ey = 0.f, e1 = 0.f, e2 = 0.f;
+    auto step = [&](int t) {
+        const int slot = t % kPF;
+        const float2 e = ring[slot];
+        const float4 ua = uring[slot];
+        const int tl = t + kPF < T ? t + kPF : T - 1;
+        ring[slot] = noise_ld(np + (size_t)tl * K);
+        uring[slot] = const_ld4(cua + 4 * tl);
+        PIN_LOADS();
+        const float v1 = fmaf(exf, ua.x, e.x);  // u[t] + eps (exploit) or eps, control.py:99-101
+        const float v2 = fmaf(exf, ua.y, e.y);
+        dyn_step(x, v1, v2, c);
+        const float px = fmaf(c.fk1, x.c1, c.fk2 * x.c12);  // control.py:178-179
+        const float py = fmaf(c.fk1, x.s1, c.fk2 * x.s12);
+        const float4 r = s_win[sr.nearest(px, py)];
+        ex = px - r.x;
+        ey = py - r.y;
+        e1 = x.dq1 - r.z;
+        e2 = x.dq2 - r.w;
+        const float g = fmaf(ua.z, v1, ua.w * v2);  // (gamma u^T Sigma^-1) v, control.py:106
+        S += (double)(weighted_sq(ex, ey, e1, e2, c.sw) + g);
+    };
+    int t = 0;
+    for (; t + kPF <= T; t += kPF) {
+#pragma unroll
+        for (int j = 0; j < kPF; ++j) step(t + j);
+    }
+    for (; t < T; ++t) step(t);
+    S += (double)weighted_sq(ex, ey, e1, e2, c.tw);  // terminal cost, control.py:109
+
+    STAMP(1, NOW());
+    const bool owner = valid && sr.sub == 0;
+    if (S_out && owner) S_out[k] = S;
+
+    // ---- workgroup partial: rho_b, eta_b, N_b (control.py:112-118 over this block)
+    const double rho_b = block_min_f64<NT>(owner ? S : INFINITY, sm);
+    // weights below 2^-64 of the block's best are dropped (see kMergeFloor)
+    const float wgt = owner ? __expf((float)((rho_b - S) * c.inv_lambda)) : 0.f;
+    const bool nz = wgt >= 5.421010862e-20f;
+    const unsigned long long bal = __ballot(nz);
+    float esum = nz ? wgt : 0.f;
+    for (int o = 32; o > 0; o >>= 1) esum += __shfl_xor(esum, o);
+    if (lane == 0) {
+        s_cnt[wave] = __popcll(bal);
+        s_redf[wave] = esum;
+    }
+    __syncthreads();
+    int off = 0, nl = 0;
+    double eta_b = 0.0;
+#pragma unroll
+    for (int w = 0; w < NT / 64; ++w) {
+        off += (w < wave) ? s_cnt[w] : 0;
+        nl += s_cnt[w];
+        eta_b += (double)s_redf[w];
+    }
+    if (nz) {
+        const int pos = off + lanes_below(bal);
+        s_k[pos] = k;
+        s_e[pos] = wgt;
+    }
+    __syncthreads();
+    const int stride = 2 + 2 * T;
+    const int nrows = c.nblocks;
+    const int ngroups = (nrows + kGroup - 1) / kGroup;
+    const __amdgpu_buffer_rsrc_t slab_r = rows_rsrc(slab, nrows * stride * 8);
+    const __amdgpu_buffer_rsrc_t gslab_r = rows_rsrc(gslab, ngroups * stride * 8);
+    const float* nf = reinterpret_cast<const float*>(noise);
+    for (int col = tid; col < 2 * T; col += NT) {
+        const float* base = nf + (size_t)(col >> 1) * K * 2 + (col & 1);
+        double acc = 0.0;
+        for (int l = 0; l < nl; ++l) acc = fma((double)s_e[l], (double)base[(size_t)s_k[l] * 2], acc);
+        st_wt(slab_r, blockIdx.x * stride + 2 + col, acc);
+    }
+    if (tid == 0) {
+        st_wt(slab_r, blockIdx.x * stride, rho_b);
+        st_wt(slab_r, blockIdx.x * stride + 1, eta_b);
+    }
+    STAMP(2, NOW());
+    STAMP(5, (unsigned long long)nl);
+    // ---- level 1: the last workgroup of each group of kGroup merges the group
+    const int g = blockIdx.x / kGroup;
+    const int gsz = min(kGroup, nrows - g * kGroup);
+    if (!arrive_last<NT>(counters + g, (unsigned)gsz, &s_flag)) return;
+    STAMP(3, NOW());
+    merge_rows_block<NT>(slab_r, g * kGroup, gsz, c, sm, &gslab_r, g, nullptr, false, nullptr);
+    // ---- level 2: the last group merges the group rows and finishes the step
+    if (!arrive_last<NT>(counters + ngroups, (unsigned)ngroups, &s_flag)) return;
+    STAMP(4, NOW());
+    merge_rows_block<NT>(gslab_r, 0, ngroups, c, sm, nullptr, 0, partial_out, true, w_eps_out);
+    STAMP(6, (unsigned long long)sm.nrel);
+    if (flags & MPPI_FLAG_FUSED_UPDATE) nominal_update_block<NT>(st, nxt, c, sm, u_cur);
+    STAMP(7, NOW());
+}
+
+constexpr int kMergeThreads = 256;
+
+__global__ __launch_bounds__(kMergeThreads) void merge_kernel(const KConst c, const double* parts, int n,
+                                                              double* w_eps_out, const DevStep* cur,
+                                                              DevStep* nxt, unsigned flags) {
+    __shared__ MergeScratch sm;
+    const int tid = threadIdx.x;
+    const double u_cur = ((flags & MPPI_FLAG_FUSED_UPDATE) && tid < 2 * c.T) ? cur->u[tid >> 1][tid & 1] : 0.0;
+    const __amdgpu_buffer_rsrc_t r = rows_rsrc(parts, n * (2 + 2 * c.T) * 8);
+    merge_rows_block<kMergeThreads>(r, 0, n, c, sm, nullptr, 0, nullptr, true, w_eps_out);
+    if (flags & MPPI_FLAG_FUSED_UPDATE) nominal_update_block<kMergeThreads>(cur, nxt, c, sm, u_cur);
+}
+
+// Trajectory re-roll (control.py:129-145): control(t) = base[(t-1) mod T] (+ eps).
+__global__ __launch_bounds__(kThreads) void traj_kernel(const KConst c, const DevStep* __restrict__ st,
+                                                        const float2* __restrict__ base,
+                                                        const float2* __restrict__ noise, int Kn,
+                                                        float4* __restrict__ out) {
+    const int k = blockIdx.x * kThreads + threadIdx.x;
+    if (k >= Kn) return;
+    const int T = c.T;
+    const float exf = noise ? ((c.k_offset + k) < c.k_exploit ? 1.f : 0.f) : 1.f;
+    const float4 x0 = st->x0;
+    ArmState x;
+    x.q1 = x0.x;
+    x.q2 = x0.y;
+    x.dq1 = x0.z;
+    x.dq2 = x0.w;
+    sincos_f32(x.q1, &x.s1, &x.c1);
+    sincos_f32(x.q1 + x.q2, &x.s12, &x.c12);
+    for (int t = 0; t < T; ++t) {
+        const int ti = t == 0 ? T - 1 : t - 1;
+        const float2 b = base[ti];
+        float v1 = b.x, v2 = b.y;
+        if (noise) {
+            const float2 e = noise[(size_t)ti * c.K_local + k];
+            v1 = fmaf(exf, b.x, e.x);
+            v2 = fmaf(exf, b.y, e.y);
+        }
+        dyn_step(x, v1, v2, c);
+        out[(size_t)k * T + t] = make_float4(x.q1, x.q2, x.dq1, x.dq2);
+    }
+}
+
+// Philox4x32-10 (Salmon et al., SC'11) + Box-Muller; eps = L z, L = chol(Sigma).
+__device__ __forceinline__ uint4 philox4x32_10(uint4 ctr, uint2 key) {
+#pragma unroll
+    for (int r = 0; r < 10; ++r) {
+        const unsigned lo0 = 0xD2511F53u * ctr.x, hi0 = __umulhi(0xD2511F53u, ctr.x);
+        const unsigned lo1 = 0xCD9E8D57u * ctr.z, hi1 = __umulhi(0xCD9E8D57u, ctr.z);
+        ctr = make_uint4(hi1 ^ ctr.y ^ key.x, lo1, hi0 ^ ctr.w ^ key.y, lo0);
+        key.x += 0x9E3779B9u;
+        key.y += 0xBB67AE85u;
+    }
+    return ctr;
+}
+
+__global__ __launch_bounds__(kThreads) void philox_noise_kernel(int K_local, int T, long long k_offset,
+                                                                unsigned long long seed,
+                                                                unsigned long long step, float L00,
+                                                                float L10, float L11, float2* out) {
+    const long long idx = (long long)blockIdx.x * kThreads + threadIdx.x;
+    const int tp = (T + 1) / 2;
+    if (idx >= (long long)K_local * tp) return;
+    const int k = (int)(idx % K_local);
+    const int t0 = 2 * (int)(idx / K_local);
+    const unsigned long long kg = (unsigned long long)(k_offset + k);
+    const uint4 ctr = make_uint4((unsigned)kg, (unsigned)(kg >> 32), (unsigned)t0, (unsigned)step);
+    const uint2 key = make_uint2((unsigned)seed, (unsigned)(seed >> 32) ^ (unsigned)(step >> 32));
+    const uint4 r = philox4x32_10(ctr, key);
+    const float inv = 2.3283064365386963e-10f;  // 2^-32
+    const float u0 = ((float)r.x + 1.0f) * inv, u1 = (float)r.y * inv;
+    const float u2 = ((float)r.z + 1.0f) * inv, u3 = (float)r.w * inv;
+    float s, co;
+    const float ra = sqrtf(-2.0f * logf(fminf(u0, 1.0f)));
+    sincospif(2.0f * u1, &s, &co);
+    const float z0 = ra * co, z1 = ra * s;
+    const float rb = sqrtf(-2.0f * logf(fminf(u2, 1.0f)));
+    sincospif(2.0f * u3, &s, &co);
+    const float z2 = rb * co, z3 = rb * s;
+    out[(size_t)t0 * K_local + k] = make_float2(L00 * z0, fmaf(L10, z0, L11 * z1));
+    if (t0 + 1 < T) out[(size_t)(t0 + 1) * K_local + k] = make_float2(L00 * z2, fmaf(L10, z2, L11 * z3));
+}
+
+}  // namespace
+
+// ================================================================ host side
+
+struct mppi_ctx {
+    mppi_config cfg;
+    int device = 0;
+    hipStream_t stream = nullptr;
+    int lps = 1, nt = 256, nblocks = 0;
+    KConst kc;
+    DevStep* d_step = nullptr;  // [2] ping-pong
+    int cur = 0;
+    DevStep* h_step = nullptr;  // pinned staging
+    hipEvent_t staged = nullptr;
+    double* d_slab = nullptr;
+    double* d_gslab = nullptr;
+    unsigned* d_counter = nullptr;  // [ngroups + 1] arrival counters
+    double* d_weps = nullptr;
+    double* h_buf = nullptr;    // pinned D2H staging, 2 * kMaxT doubles
+    float2* d_base = nullptr;   // traj base controls
+    float2* h_base = nullptr;   // pinned
+    double sig_inv[4];
+    unsigned long long* d_dbg = nullptr;  // diagnostic stamp buffer (MPPI_STAMPS builds)
+};
+
+namespace {
+thread_local std::string g_err;
+
+int fail(int code, const std::string& msg) {
+    g_err = msg;
+    return code;
+}
+
+#define HIP_TRY(expr)                                                                 \
+    do {                                                                              \
+        hipError_t e_ = (expr);                                                       \
+        if (e_ != hipSuccess)                                                         \
+            return fail(MPPI_E_HIP, std::string(#expr) + ": " + hipGetErrorString(e_)); \
+    } while (0)
+
+int launch_check(const char* what) {
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return fail(MPPI_E_HIP, std::string(what) + ": " + hipGetErrorString(e));
+    return MPPI_OK;
+}
+
+int auto_lps(int K_local) {
+    // Measured on MI355X (tools/ubench_valu.hip): one wave issues a VALU op at
+    // most every ~8 cycles, 2 waves/SIMD reach ~4.4, 4 waves ~3.0.  Splitting
+    // the window search over 2 lanes per sample doubles the wave count at
+    // ~1.5x the instructions per sample: worth it below 2 waves per SIMD.
+    const long long waves1 = ((long long)K_local + 63) / 64;
+    if (waves1 >= 2048) return 1;
+    if (waves1 >= 256) return 2;
+    return 4;
+}
+}  // namespace
+
+extern "C" {
+
+const char* mppi_last_error(void) { return g_err.c_str(); }
+
+int mppi_ctx_create(const mppi_config* cfg, int device, void* stream, mppi_ctx** out) {
+    if (!cfg || !out) return fail(MPPI_E_ARG, "null argument");
+    *out = nullptr;
+    if (cfg->T < 1 || cfg->T > MPPI_MAX_T) return fail(MPPI_E_ARG, "T must be in [1, 128]");
+    if (cfg->K_local < 1 || cfg->K_total < cfg->K_local || cfg->k_offset < 0 ||
+        cfg->k_offset + (long long)cfg->K_local > cfg->K_total)
+        return fail(MPPI_E_ARG, "bad sample geometry (K_local, K_total, k_offset)");
+    const double* S = cfg->sigma;
+    const double det = S[0] * S[3] - S[1] * S[2];
+    if (det == 0.0 || !isfinite(det)) return fail(MPPI_E_SINGULAR, "Singular matrix");
+    mppi_ctx* c = new mppi_ctx();
+    c->cfg = *cfg;
+    c->device = device;
+    c->stream = (hipStream_t)stream;
+    c->sig_inv[0] = S[3] / det;
+    c->sig_inv[1] = -S[1] / det;
+    c->sig_inv[2] = -S[2] / det;
+    c->sig_inv[3] = S[0] / det;
+    int lps = cfg->lanes_per_sample > 0 ? cfg->lanes_per_sample : auto_lps(cfg->K_local);
+    if (lps != 1 && lps != 2 && lps != 4) {
+        delete c;
+        return fail(MPPI_E_ARG, "lanes_per_sample must be 0, 1, 2 or 4");
+    }
+    c->lps = lps;
+    // 512-thread workgroups when the grid fills every CU with one of them (8 waves:
+    // two per SIMD); 256 otherwise.  MPPI_BLOCK=256|512 overrides (diagnostics).
+    const long long lanes = (long long)cfg->K_local * lps;
+    c->nt = lanes >= 512LL * 256 ? 512 : 256;
+    if (const char* ev = getenv("MPPI_BLOCK")) c->nt = atoi(ev) == 512 ? 512 : 256;
+    c->nblocks = (int)((lanes + c->nt - 1) / c->nt);
+    if (c->nblocks > 1024 * 1024) {
+        delete c;
+        return fail(MPPI_E_ARG, "too many samples");
+    }
+    const mppi_arm_params& a = cfg->arm;
+    KConst& k = c->kc;
+    memset(&k, 0, sizeof(k));
+    k.K_local = cfg->K_local;
+    k.T = cfg->T;
+    k.k_offset = cfg->k_offset;
+    {
+        const double thr = (1.0 - cfg->param_exploration) * (double)cfg->K_total;  // control.py:98
+        long long kx = thr <= 0.0 ? 0 : (long long)ceil(thr);
+        if (kx > cfg->K_total) kx = cfg->K_total;
+        k.k_exploit = (int)kx;
+    }
+    k.nblocks = c->nblocks;
+    k.dt = (float)cfg->delta_t;
+    k.fk1 = (float)a.fk_l1;
+    k.fk2 = (float)a.fk_l2;
+    k.A = (float)(a.m1 * a.lc1 * a.lc1 + a.l1 + a.m2 * (a.l1 * a.l1 + a.lc2 * a.lc2) + a.l2);
+    k.B = (float)(2.0 * a.m2 * a.l1 * a.lc2);
+    k.D = (float)(a.m2 * a.lc2 * a.lc2 + a.l2);
+    k.E = (float)(a.m2 * a.l1 * a.lc2);
+    k.P = (float)((a.m1 * a.lc1 + a.m2 * a.l1) * a.g);
+    k.Q = (float)(a.m2 * a.lc2 * a.g);
+    for (int i = 0; i < 4; ++i) {
+        k.sw[i] = (float)(cfg->stage_cost_weight[i] * 10000.0);     // control.py:185
+        k.tw[i] = (float)(cfg->terminal_cost_weight[i] * 10000.0);  // control.py:198
+    }
+    k.lambda = cfg->param_lambda;
+    k.inv_lambda = 1.0 / cfg->param_lambda;
+    k.gamma = cfg->param_lambda * (1.0 - cfg->param_alpha);  // control.py:45
+    for (int i = 0; i < 4; ++i) k.sig_inv[i] = c->sig_inv[i];
+
+    auto cleanup_fail = [&](int rc) {
+        mppi_ctx_destroy(c);
+        return rc;
+    };
+    hipError_t e;
+    if ((e = hipSetDevice(device)) != hipSuccess) return cleanup_fail(fail(MPPI_E_HIP, std::string("hipSetDevice: ") + hipGetErrorString(e)));
+    const size_t slab = (size_t)c->nblocks * (2 + 2 * cfg->T) * sizeof(double);
+    const int ngroups = (c->nblocks + kGroup - 1) / kGroup;
+    const size_t gslab = (size_t)ngroups * (2 + 2 * cfg->T) * sizeof(double);
+    const size_t ctr_bytes = ((size_t)(ngroups + 1) * sizeof(unsigned) + 255) & ~(size_t)255;
+    if ((e = hipMalloc(&c->d_step, 2 * sizeof(DevStep))) != hipSuccess ||
+        (e = hipMalloc(&c->d_slab, slab)) != hipSuccess ||
+        (e = hipMalloc(&c->d_gslab, gslab)) != hipSuccess ||
+        (e = hipMalloc(&c->d_counter, ctr_bytes)) != hipSuccess ||
+        (e = hipMalloc(&c->d_weps, 2 * kMaxT * sizeof(double))) != hipSuccess ||
+        (e = hipMalloc(&c->d_base, kMaxT * sizeof(float2))) != hipSuccess ||
+        (e = hipHostMalloc(&c->h_step, sizeof(DevStep), hipHostMallocDefault)) != hipSuccess ||
+        (e = hipHostMalloc(&c->h_buf, 2 * kMaxT * sizeof(double), hipHostMallocDefault)) != hipSuccess ||
+        (e = hipHostMalloc(&c->h_base, kMaxT * sizeof(float2), hipHostMallocDefault)) != hipSuccess ||
+        (e = hipEventCreateWithFlags(&c->staged, hipEventDisableTiming)) != hipSuccess ||
+        (e = hipMemset(c->d_counter, 0, ctr_bytes)) != hipSuccess ||
+        (e = hipMemset(c->d_step, 0, 2 * sizeof(DevStep))) != hipSuccess ||
+        (e = hipMemset(c->d_weps, 0, 2 * kMaxT * sizeof(double))) != hipSuccess ||
+        (e = hipDeviceSynchronize()) != hipSuccess)
+        return cleanup_fail(fail(MPPI_E_HIP, std::string("allocation: ") + hipGetErrorString(e)));
+    memset(c->h_step, 0, sizeof(DevStep));
+    *out = c;
+    return MPPI_OK;
+}
+
+void mppi_ctx_destroy(mppi_ctx* c) {
+    if (!c) return;
+    if (c->stream) (void)hipStreamSynchronize(c->stream);
+    (void)hipDeviceSynchronize();
+    (void)hipFree(c->d_step);
+    (void)hipFree(c->d_slab);
+    (void)hipFree(c->d_counter);
+    (void)hipFree(c->d_gslab);
+    (void)hipFree(c->d_weps);
+    (void)hipFree(c->d_base);
+    if (c->h_step) (void)hipHostFree(c->h_step);
+    if (c->h_buf) (void)hipHostFree(c->h_buf);
+    if (c->h_base) (void)hipHostFree(c->h_base);
+    if (c->staged) (void)hipEventDestroy(c->staged);
+    delete c;
+}
+
+int mppi_set_stream(mppi_ctx* c, void* stream) {
+    if (!c) return fail(MPPI_E_ARG, "null context");
+    c->stream = (hipStream_t)stream;
+    return MPPI_OK;
+}
+
+int mppi_ctx_info(const mppi_ctx* c, int* lps, int* blocks, int* threads) {
+    if (!c) return fail(MPPI_E_ARG, "null context");
+    if (lps) *lps = c->lps;
+    if (blocks) *blocks = c->nblocks;
+    if (threads) *threads = c->nt;
+    return MPPI_OK;
+}
+
+int mppi_set_step_inputs(mppi_ctx* c, const double* x0, const double* window, int W, const double* u) {
+    if (!c || !x0 || !window) return fail(MPPI_E_ARG, "null argument");
+    if (W < 1 || W > MPPI_SEARCH_LEN) return fail(MPPI_E_ARG, "window rows must be in [1, 30]");
+    HIP_TRY(hipEventSynchronize(c->staged));  // staging block free again
+    DevStep* h = c->h_step;
+    double cx = 0.0, cy = 0.0;
+    for (int j = 0; j < W; ++j) {
+        cx += window[4 * j];
+        cy += window[4 * j + 1];
+    }
+    cx /= W;
+    cy /= W;
+    for (int j = 0; j < kSlots; ++j) {
+        if (j < W) {
+            const double* r = window + 4 * j;
+            h->win[j] = make_float4((float)r[0], (float)r[1], (float)r[2], (float)r[3]);
+            const double rx = r[0] - cx, ry = r[1] - cy;
+            h->key[j] = make_float4((float)rx, (float)ry, (float)(rx * rx + ry * ry), 0.f);
+        } else {
+            h->win[j] = make_float4(0.f, 0.f, 0.f, 0.f);
+            h->key[j] = make_float4(0.f, 0.f, kPadKey, 0.f);
+        }
+    }
+    h->x0 = make_float4((float)x0[0], (float)x0[1], (float)x0[2], (float)x0[3]);
+    h->ctr = make_float4((float)cx, (float)cy, (float)W, 0.f);
+    size_t bytes = offsetof(DevStep, ua);
+    if (u) {
+        const KConst& k = c->kc;
+        for (int t = 0; t < c->cfg.T; ++t) {
+            const double u0 = u[2 * t], u1 = u[2 * t + 1];
+            const double g0 = k.gamma * u0, g1 = k.gamma * u1;  // ((gamma u^T) Sigma^-1), control.py:106
+            const double a0 = g0 * k.sig_inv[0] + g1 * k.sig_inv[2];
+            const double a1 = g0 * k.sig_inv[1] + g1 * k.sig_inv[3];
+            h->ua[t] = make_float4((float)u0, (float)u1, (float)a0, (float)a1);
+            h->u[t][0] = u0;
+            h->u[t][1] = u1;
+        }
+        bytes = sizeof(DevStep);
+    }
+    HIP_TRY(hipMemcpyAsync(c->d_step + c->cur, h, bytes, hipMemcpyHostToDevice, c->stream));
+    HIP_TRY(hipEventRecord(c->staged, c->stream));
+    return MPPI_OK;
+}
+
+int mppi_rollout(mppi_ctx* c, const float* noise_dev, double* S_dev, double* partial_dev, unsigned flags) {
+    if (!c || !noise_dev) return fail(MPPI_E_ARG, "null argument");
+    if ((flags & MPPI_FLAG_FUSED_UPDATE) && c->cfg.T < 5)
+        return fail(MPPI_E_ARG, "device median filter needs T >= 5 (use the host update)");
+    const DevStep* cur = c->d_step + c->cur;
+    DevStep* nxt = c->d_step + (c->cur ^ 1);
+    const float2* nz = reinterpret_cast<const float2*>(noise_dev);
+#define MPPI_LAUNCH(L, NTH)                                                                                   \
+    hipLaunchKernelGGL((rollout_kernel<L, NTH>), dim3(c->nblocks), dim3(NTH), 0, c->stream, c->kc, cur, nz,   \
+                       S_dev, c->d_slab, c->d_gslab, c->d_counter, partial_dev, c->d_weps, nxt, flags, c->d_dbg)
+    if (c->nt == 512) {
+        if (c->lps == 1) MPPI_LAUNCH(1, 512);
+        else if (c->lps == 2) MPPI_LAUNCH(2, 512);
+        else MPPI_LAUNCH(4, 512);
+    } else {
+        if (c->lps == 1) MPPI_LAUNCH(1, 256);
+        else if (c->lps == 2) MPPI_LAUNCH(2, 256);
+        else MPPI_LAUNCH(4, 256);
+    }
+#undef MPPI_LAUNCH
+    const int rc = launch_check("rollout_kernel");
+    if (rc == MPPI_OK && (flags & MPPI_FLAG_FUSED_UPDATE)) c->cur ^= 1;
+    return rc;
+}
+
+int mppi_merge_partials(mppi_ctx* c, const double* partials_dev, int n, unsigned flags) {
+    if (!c || !partials_dev || n < 1) return fail(MPPI_E_ARG, "bad argument");
+    if ((flags & MPPI_FLAG_FUSED_UPDATE) && c->cfg.T < 5)
+        return fail(MPPI_E_ARG, "device median filter needs T >= 5 (use the host update)");
+    const DevStep* cur = c->d_step + c->cur;
+    DevStep* nxt = c->d_step + (c->cur ^ 1);
+    hipLaunchKernelGGL(merge_kernel, dim3(1), dim3(kMergeThreads), 0, c->stream, c->kc, partials_dev, n,
+                       c->d_weps, cur, nxt, flags);
+    const int rc = launch_check("merge_kernel");
+    if (rc == MPPI_OK && (flags & MPPI_FLAG_FUSED_UPDATE)) c->cur ^= 1;
+    return rc;
+}
+
+int mppi_get_weighted_noise(mppi_ctx* c, double* w_eps_host) {
+    if (!c || !w_eps_host) return fail(MPPI_E_ARG, "null argument");
+    const size_t bytes = 2 * (size_t)c->cfg.T * sizeof(double);
+    HIP_TRY(hipMemcpyAsync(c->h_buf, c->d_weps, bytes, hipMemcpyDeviceToHost, c->stream));
+    HIP_TRY(hipStreamSynchronize(c->stream));
+    memcpy(w_eps_host, c->h_buf, bytes);
+    return MPPI_OK;
+}
+
+int mppi_get_nominal(mppi_ctx* c, double* u_host) {
+    if (!c || !u_host) return fail(MPPI_E_ARG, "null argument");
+    const size_t bytes = 2 * (size_t)c->cfg.T * sizeof(double);
+    HIP_TRY(hipMemcpyAsync(c->h_buf, (const char*)(c->d_step + c->cur) + offsetof(DevStep, u), bytes,
+                           hipMemcpyDeviceToHost, c->stream));
+    HIP_TRY(hipStreamSynchronize(c->stream));
+    memcpy(u_host, c->h_buf, bytes);
+    return MPPI_OK;
+}
+
+int mppi_rollout_traj(mppi_ctx* c, const double* base_u, const float* noise_dev, int K, float* out_dev) {
+    if (!c || !out_dev || K < 1 || K > c->cfg.K_local) return fail(MPPI_E_ARG, "bad argument");
+    const DevStep* cur = c->d_step + c->cur;
+    const float2* base;
+    if (base_u) {
+        HIP_TRY(hipEventSynchronize(c->staged));
+        for (int t = 0; t < c->cfg.T; ++t) c->h_base[t] = make_float2((float)base_u[2 * t], (float)base_u[2 * t + 1]);
+        HIP_TRY(hipMemcpyAsync(c->d_base, c->h_base, c->cfg.T * sizeof(float2), hipMemcpyHostToDevice, c->stream));
+        HIP_TRY(hipEventRecord(c->staged, c->stream));
+        base = c->d_base;
+    } else {
+        // nominal u0,u1 of the current step block: ua[t].xy, read with stride 16 B
+        HIP_TRY(hipMemcpy2DAsync(c->d_base, sizeof(float2), (const char*)cur + offsetof(DevStep, ua), sizeof(float4),
+                                 sizeof(float2), c->cfg.T, hipMemcpyDeviceToDevice, c->stream));
+        base = c->d_base;
+    }
+    const int blocks = (K + kThreads - 1) / kThreads;
+    hipLaunchKernelGGL(traj_kernel, dim3(blocks), dim3(kThreads), 0, c->stream, c->kc, cur, base,
+                       reinterpret_cast<const float2*>(noise_dev), K, reinterpret_cast<float4*>(out_dev));
+    return launch_check("traj_kernel");
+}
+
+int mppi_noise_philox(mppi_ctx* c, unsigned long long seed, unsigned long long step, float* out_dev) {
+    if (!c || !out_dev) return fail(MPPI_E_ARG, "null argument");
+    const double* S = c->cfg.sigma;
+    // Cholesky of the symmetric part (np.random.multivariate_normal expects SPD Sigma)
+    const double s01 = 0.5 * (S[1] + S[2]);
+    if (!(S[0] > 0.0)) return fail(MPPI_E_ARG, "Sigma not positive definite");
+    const double L00 = sqrt(S[0]), L10 = s01 / L00, d = S[3] - L10 * L10;
+    if (!(d >= 0.0)) return fail(MPPI_E_ARG, "Sigma not positive semi-definite");
+    const double L11 = sqrt(d);
+    const long long n = (long long)c->cfg.K_local * ((c->cfg.T + 1) / 2);
+    const int blocks = (int)((n + kThreads - 1) / kThreads);
+    hipLaunchKernelGGL(philox_noise_kernel, dim3(blocks), dim3(kThreads), 0, c->stream, c->cfg.K_local,
+                       c->cfg.T, (long long)c->cfg.k_offset, seed, step, (float)L00, (float)L10, (float)L11,
+                       reinterpret_cast<float2*>(out_dev));
+    return launch_check("philox_noise_kernel");
+}
+
+int mppi_debug_set_buffer(mppi_ctx* c, void* dbg_dev) {
+    if (!c) return fail(MPPI_E_ARG, "null context");
+    c->d_dbg = (unsigned long long*)dbg_dev;
+    return MPPI_OK;
+}
+
+int mppi_sync(mppi_ctx* c) {
+    if (!c) return fail(MPPI_E_ARG, "null context");
+    HIP_TRY(hipStreamSynchronize(c->stream));
+    return MPPI_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,188 @@
+"""RolloutEngine — Python handle on one device context of the HIP engine.
+
+PyTorch-ROCm is used only to own device memory and streams: noise buffers,
+per-sample costs, partials and trajectories are torch tensors whose
+``data_ptr()`` crosses the C ABI (include/mppi_rocm.h).  All work is issued on
+the torch current stream of the engine's device, so ``torch.cuda.Event``
+timing and RCCL collectives order with it naturally.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import math
+
+import numpy as np
+import torch
+
+from . import _native as N
+from .params import ArmParams
+
+
+def _dptr(a: np.ndarray):
+    return a.ctypes.data_as(C.POINTER(C.c_double))
+
+
+class RolloutEngine:
+    """Owns one ``mppi_ctx`` (one device, one shard of samples)."""
+
+    def __init__(self, K_local: int, T: int, delta_t: float, param_lambda: float, param_alpha: float,
+                 sigma, stage_cost_weight, terminal_cost_weight, param_exploration: float = 0.0,
+                 arm: ArmParams = ArmParams(), K_total: int | None = None, k_offset: int = 0,
+                 device: int | torch.device | None = None, lanes_per_sample: int = 0):
+        self._lib = N.load()
+        if device is None:
+            device = torch.cuda.current_device()
+        self.device = torch.device("cuda", device if isinstance(device, int) else device.index)
+        self.K_local, self.T = int(K_local), int(T)
+        self.K_total = int(K_total if K_total is not None else K_local)
+        self.k_offset = int(k_offset)
+        cfg = N.ConfigC()
+        cfg.K_local, cfg.T, cfg.K_total, cfg.k_offset = self.K_local, self.T, self.K_total, self.k_offset
+        cfg.delta_t = float(delta_t)
+        cfg.param_lambda = float(param_lambda)
+        cfg.param_alpha = float(param_alpha)
+        cfg.param_exploration = float(param_exploration)
+        sig = np.asarray(sigma, dtype=np.float64).reshape(2, 2)
+        for i, v in enumerate(sig.ravel()):
+            cfg.sigma[i] = float(v)
+        for i in range(4):
+            cfg.stage_cost_weight[i] = float(stage_cost_weight[i])
+            cfg.terminal_cost_weight[i] = float(terminal_cost_weight[i])
+        for f in ("m1", "m2", "l1", "l2", "lc1", "lc2", "g", "fk_l1", "fk_l2"):
+            setattr(cfg.arm, f, float(getattr(arm, f)))
+        cfg.lanes_per_sample = int(lanes_per_sample)
+        self.sigma = sig
+        self.param_lambda = float(param_lambda)
+        with torch.cuda.device(self.device):
+            self.stream = torch.cuda.current_stream(self.device)
+            ctx = C.c_void_p()
+            N.check(self._lib.mppi_ctx_create(C.byref(cfg), self.device.index,
+                                              C.c_void_p(self.stream.cuda_stream), C.byref(ctx)),
+                    "mppi_ctx_create")
+        self._ctx = ctx
+        lps, blocks, threads = C.c_int(), C.c_int(), C.c_int()
+        N.check(self._lib.mppi_ctx_info(ctx, C.byref(lps), C.byref(blocks), C.byref(threads)), "mppi_ctx_info")
+        self.lanes_per_sample, self.blocks, self.threads = lps.value, blocks.value, threads.value
+        self.partial_len = 2 + 2 * self.T
+        self._weps = np.zeros((self.T, 2))
+
+    # -- lifetime -----------------------------------------------------------
+    def close(self) -> None:
+        if getattr(self, "_ctx", None):
+            self._lib.mppi_ctx_destroy(self._ctx)
+            self._ctx = None
+
+    def __del__(self):  # pragma: no cover - best effort
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def _sync_stream(self):
+        """Follow torch's current stream (it may change between calls)."""
+        s = torch.cuda.current_stream(self.device)
+        if s.cuda_stream != self.stream.cuda_stream:
+            self.stream = s
+            N.check(self._lib.mppi_set_stream(self._ctx, C.c_void_p(s.cuda_stream)), "mppi_set_stream")
+
+    # -- buffers ------------------------------------------------------------
+    def new_noise(self) -> torch.Tensor:
+        """Device noise buffer, layout [T][K_local][2] fp32."""
+        return torch.empty((self.T, self.K_local, 2), dtype=torch.float32, device=self.device)
+
+    def new_partial(self) -> torch.Tensor:
+        return torch.empty(self.partial_len, dtype=torch.float64, device=self.device)
+
+    def upload_noise(self, eps_kt: np.ndarray, out: torch.Tensor | None = None) -> torch.Tensor:
+        """Reference-order noise (K_local, T, 2) -> device [T][K_local][2] fp32."""
+        out = self.new_noise() if out is None else out
+        host = torch.from_numpy(np.ascontiguousarray(np.asarray(eps_kt).transpose(1, 0, 2), dtype=np.float32))
+        out.copy_(host.pin_memory(), non_blocking=True)
+        return out
+
+    # -- the hot path -------------------------------------------------------
+    def set_step_inputs(self, x0, window, u=None) -> None:
+        self._sync_stream()
+        x0 = np.ascontiguousarray(np.asarray(x0, dtype=np.float64).ravel()[:4])
+        win = np.ascontiguousarray(np.asarray(window, dtype=np.float64)[:, :4])
+        if win.ndim != 2 or win.shape[0] < 1 or win.shape[0] > N.MPPI_SEARCH_LEN:
+            raise ValueError("window must have 1..30 rows of [x, y, dq1, dq2]")
+        uu = None
+        if u is not None:
+            uu = np.ascontiguousarray(np.asarray(u, dtype=np.float64).reshape(self.T, 2))
+        N.check(self._lib.mppi_set_step_inputs(self._ctx, _dptr(x0), _dptr(win), win.shape[0],
+                                               _dptr(uu) if uu is not None else None),
+                "mppi_set_step_inputs")
+        self._keep = (x0, win, uu)  # keep host arrays alive until the async copy ran
+
+    def rollout(self, noise: torch.Tensor, S_out: torch.Tensor | None = None,
+                partial_out: torch.Tensor | None = None, fused_update: bool = False) -> None:
+        self._sync_stream()
+        self._check_noise(noise)
+        if S_out is not None:
+            assert S_out.dtype == torch.float64 and S_out.numel() >= self.K_local and S_out.device == self.device
+        if partial_out is not None:
+            assert partial_out.dtype == torch.float64 and partial_out.numel() >= self.partial_len
+        N.check(self._lib.mppi_rollout(self._ctx, C.c_void_p(noise.data_ptr()),
+                                       C.c_void_p(S_out.data_ptr()) if S_out is not None else None,
+                                       C.c_void_p(partial_out.data_ptr()) if partial_out is not None else None,
+                                       N.MPPI_FLAG_FUSED_UPDATE if fused_update else 0),
+                "mppi_rollout")
+
+    def merge(self, partials: torch.Tensor, n: int, fused_update: bool = False) -> None:
+        self._sync_stream()
+        assert partials.dtype == torch.float64 and partials.is_contiguous()
+        assert partials.numel() >= n * self.partial_len
+        N.check(self._lib.mppi_merge_partials(self._ctx, C.c_void_p(partials.data_ptr()), int(n),
+                                              N.MPPI_FLAG_FUSED_UPDATE if fused_update else 0),
+                "mppi_merge_partials")
+
+    def weighted_noise(self) -> np.ndarray:
+        """w_eps (T, 2) fp64 of the last rollout / merge (synchronising)."""
+        out = np.zeros((self.T, 2))
+        N.check(self._lib.mppi_get_weighted_noise(self._ctx, _dptr(out)), "mppi_get_weighted_noise")
+        return out
+
+    def nominal(self) -> np.ndarray:
+        out = np.zeros((self.T, 2))
+        N.check(self._lib.mppi_get_nominal(self._ctx, _dptr(out)), "mppi_get_nominal")
+        return out
+
+    def trajectories(self, base_u=None, noise: torch.Tensor | None = None, K: int | None = None) -> torch.Tensor:
+        """(K, T, 4) fp32 states of the off-by-one re-roll (control.py:129-145)."""
+        self._sync_stream()
+        K = self.K_local if K is None else int(K)
+        out = torch.empty((K, self.T, 4), dtype=torch.float32, device=self.device)
+        bu = None
+        if base_u is not None:
+            bu = np.ascontiguousarray(np.asarray(base_u, dtype=np.float64).reshape(self.T, 2))
+        if noise is not None:
+            self._check_noise(noise)
+        N.check(self._lib.mppi_rollout_traj(self._ctx, _dptr(bu) if bu is not None else None,
+                                            C.c_void_p(noise.data_ptr()) if noise is not None else None,
+                                            K, C.c_void_p(out.data_ptr())),
+                "mppi_rollout_traj")
+        self._keep_traj = bu
+        return out
+
+    def philox_noise(self, seed: int, step: int = 0, out: torch.Tensor | None = None) -> torch.Tensor:
+        self._sync_stream()
+        out = self.new_noise() if out is None else out
+        self._check_noise(out)
+        N.check(self._lib.mppi_noise_philox(self._ctx, int(seed) & (2 ** 64 - 1), int(step) & (2 ** 64 - 1),
+                                            C.c_void_p(out.data_ptr())), "mppi_noise_philox")
+        return out
+
+    def synchronize(self) -> None:
+        N.check(self._lib.mppi_sync(self._ctx), "mppi_sync")
+
+    def _check_noise(self, noise: torch.Tensor) -> None:
+        if (noise.dtype != torch.float32 or not noise.is_contiguous() or noise.device != self.device
+                or tuple(noise.shape) != (self.T, self.K_local, 2)):
+            raise ValueError(f"noise must be a contiguous fp32 {(self.T, self.K_local, 2)} tensor on {self.device}")
+
+
+def exploit_count(param_exploration: float, K: int) -> int:
+    """Number of samples with ``k < (1 - expl) * K`` (control.py:98)."""
+    thr = (1.0 - param_exploration) * K
+    return 0 if thr <= 0 else min(K, int(math.ceil(thr)))

@@ -1,0 +1,287 @@
+"""GPU parity: the HIP path (through the C ABI) against the golden fixtures
+captured from the reference and against the fp64 oracles.
+
+Tolerances (fp32 device arithmetic vs the fp64 reference, BASELINE.json
+north_star: "control output within 1e-4 rel-err of the NumPy reference"):
+  * u (updated control sequence): max |du| / max(|u|, 1) <= 1e-4
+  * S (per-sample cost): relative error <= 5e-5, same argmin
+  * trajectories: |dx| <= 1e-4 (1 + |x|)
+"""
+import math
+
+import numpy as np
+import pytest
+
+torch = pytest.importorskip("torch")
+pytestmark = pytest.mark.gpu
+
+import coracle  # noqa: E402
+import mppi_oracle as O  # noqa: E402
+from conftest import LOOP_FIXTURES, STEP_FIXTURES, ctor_kwargs, load_loop, load_step  # noqa: E402
+
+U_TOL = 1e-4
+S_TOL = 5e-5
+
+RUNPY = dict(param_exploration=0.0, param_lambda=100.0, param_alpha=0.98, sigma=np.eye(2) * 20.0,
+             stage_cost_weight=np.array([0.5, 0.5, 5.0, 5.0]),
+             terminal_cost_weight=np.array([5.0, 5.0, 50.0, 50.0]))
+X0 = np.array([1.152198236517471885e00, -1.266101672070702344e00, 0.0, 0.0])
+
+
+@pytest.fixture(scope="module", autouse=True)
+def _gpu():
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    torch.cuda.set_device(0)
+
+
+def _ctrl(g, paths, **kw):
+    from mppi_robotarm_amd.controller import MPPIControllerForPathTracking
+    c = MPPIControllerForPathTracking(ref_path=paths[str(g["path"])], verbose=False, **ctor_kwargs(g), **kw)
+    c.prev_waypoints_idx = int(g["prev_idx"])
+    c.u_prev = g["u_prev"].copy()
+    return c
+
+
+def _urel(a, b):
+    return float(np.max(np.abs(a - b)) / max(1.0, float(np.max(np.abs(b)))))
+
+
+def _engine(K, T, lps=0, K_total=None, k_offset=0, **over):
+    from mppi_robotarm_amd.engine import RolloutEngine
+    from mppi_robotarm_amd.params import ArmParams
+    kw = dict(RUNPY)
+    kw.update(over)
+    return RolloutEngine(K, T, 0.006, kw["param_lambda"], kw["param_alpha"], kw["sigma"],
+                         kw["stage_cost_weight"], kw["terminal_cost_weight"], kw["param_exploration"],
+                         ArmParams(), K_total=K_total, k_offset=k_offset, device=0, lanes_per_sample=lps)
+
+
+@pytest.mark.parametrize("name", STEP_FIXTURES)
+def test_step_matches_reference(name, paths):
+    g = load_step(name)
+    c = _ctrl(g, paths)
+    c.keep_costs = True
+    eps = g["eps"].astype(np.float64)
+    c._calc_epsilon = lambda *a, **k: eps
+    u_prev = c.u_prev
+    u0, u_seq, opt, samp = c.calc_control_input(g["x0"])
+    S = c.last_S
+    assert int(np.argmin(S)) == int(np.argmin(g["S"]))
+    assert float(np.max(np.abs(S - g["S"]) / np.abs(g["S"]))) < S_TOL
+    assert _urel(u_seq, g["u_seq"]) < U_TOL
+    assert _urel(u0, g["u0"]) < U_TOL
+    assert u_seq is u_prev and np.shares_memory(u0, u_prev)       # control.py:70,148-152
+    assert c.prev_waypoints_idx == int(g["prev_idx_after"])
+    np.testing.assert_allclose(opt, g["optimal_traj"], rtol=1e-4, atol=1e-4)
+    if "sampled_traj" in g:
+        np.testing.assert_allclose(samp, g["sampled_traj"], rtol=1e-4, atol=1e-4)
+    else:
+        assert not np.any(samp)
+    c.close()
+
+
+@pytest.mark.parametrize("name", ["c1_circle_k128_t20", "runpy_k100_t30", "sigma_k128_t20"])
+def test_dropin_consumes_reference_rng_stream(name, paths):
+    """np.random.seed(s) + calc_control_input draws the same noise the reference drew."""
+    g = load_step(name)
+    c = _ctrl(g, paths)
+    np.random.seed(int(g["seed"]))
+    u0, u_seq, opt, _ = c.calc_control_input(g["x0"])
+    assert _urel(u_seq, g["u_seq"]) < U_TOL
+    c.close()
+
+
+@pytest.mark.parametrize("name", LOOP_FIXTURES)
+def test_closed_loop_ticks(name, paths):
+    """Each tick of run.py's loop from the reference's own state / u_prev / index."""
+    from mppi_robotarm_amd.controller import MPPIControllerForPathTracking
+    g = load_loop(name)
+    T, K = int(g["T"]), int(g["K"])
+    c = MPPIControllerForPathTracking(delta_t=0.006, ref_path=paths["xydq_circle"], horizon_step_T=T,
+                                      number_of_samples_K=K, verbose=False, visualize_optimal_traj=False,
+                                      **RUNPY)
+    u_prev = np.array([[10.0, -2.0]] * T)
+    prev = 0
+    for i in range(int(g["ticks"])):
+        c.u_prev = u_prev.copy()
+        c.prev_waypoints_idx = prev
+        eps = g["eps"][i].astype(np.float64)
+        c._calc_epsilon = lambda *a, e=eps, **k: e
+        u, u_seq, _, _ = c.calc_control_input(g["states"][i])
+        assert _urel(u_seq, g["u_seq"][i]) < U_TOL, i
+        assert c.prev_waypoints_idx == int(g["prev_idx"][i])
+        u_prev, prev = g["u_seq"][i].copy(), int(g["prev_idx"][i])
+    c.close()
+
+
+def _window(paths, prev=0):
+    return paths["xydq_circle"][prev:prev + 30]
+
+
+@pytest.mark.parametrize("K,T", [(65536, 64), (4096, 32), (3000, 7)])
+def test_large_rollout_against_c_oracle(K, T, paths):
+    """Full-size S on a sample subset, and the full weighted noise, vs the C fp64 oracle."""
+    eng = _engine(K, T)
+    win = _window(paths)
+    u = np.array([[10.0, -2.0]] * T) + np.random.default_rng(1).normal(0, 0.5, (T, 2))
+    eng.set_step_inputs(X0, win, u)
+    noise = eng.philox_noise(42, 3)
+    S_dev = torch.empty(K, dtype=torch.float64, device="cuda")
+    eng.rollout(noise, S_out=S_dev)
+    w_eps = eng.weighted_noise()
+    S = S_dev.cpu().numpy()
+    eps_tk = noise.cpu().numpy()
+    ref_S = coracle.rollout_costs(X0, u, eps_tk, win, 0.006, 100.0, 0.98, np.eye(2) * 20.0,
+                                  RUNPY["stage_cost_weight"], RUNPY["terminal_cost_weight"], O.ArmParams(),
+                                  layout="TK")
+    rel = np.abs(S - ref_S) / np.abs(ref_S)
+    assert float(np.max(rel)) < S_TOL
+    assert int(np.argmin(S)) == int(np.argmin(ref_S))
+    _, ref_weps = coracle.weighted_noise(ref_S, eps_tk, 100.0, layout="TK")
+    assert _urel(w_eps, ref_weps) < U_TOL
+    eng.close()
+
+
+def test_deterministic_and_lanes_per_sample_invariant(paths):
+    K, T = 20000, 48
+    outs = []
+    for lps in (1, 2, 4, 2):
+        eng = _engine(K, T, lps=lps)
+        eng.set_step_inputs(X0, _window(paths, 5), np.array([[10.0, -2.0]] * T))
+        noise = eng.philox_noise(7, 0)
+        S_dev = torch.empty(K, dtype=torch.float64, device="cuda")
+        eng.rollout(noise, S_out=S_dev)
+        outs.append((S_dev.cpu().numpy(), eng.weighted_noise()))
+        eng.close()
+    for S, w in outs[1:]:
+        assert np.array_equal(S, outs[0][0])     # the split search is exact: same bits
+        assert np.array_equal(w, outs[0][1])
+
+
+def test_shard_invariance_and_merge(paths):
+    """G virtual shards on one device + device merge == unsharded."""
+    K, T, G = 12288, 32, 4
+    u = np.array([[10.0, -2.0]] * T)
+    kw = dict(param_lambda=3.0e6, param_alpha=0.95)          # non-degenerate weights
+    full = _engine(K, T, **kw)
+    full.set_step_inputs(X0, _window(paths), u)
+    noise = full.philox_noise(99, 1)
+    full.rollout(noise)
+    w_full = full.weighted_noise()
+    parts = torch.empty(G * full.partial_len, dtype=torch.float64, device="cuda")
+    Kl = K // G
+    engs = []
+    for g in range(G):
+        e = _engine(Kl, T, K_total=K, k_offset=g * Kl, **kw)
+        e.set_step_inputs(X0, _window(paths), u)
+        nz = e.philox_noise(99, 1)
+        assert torch.equal(nz, noise[:, g * Kl:(g + 1) * Kl])   # Philox slice == unsharded draw
+        e.rollout(nz, partial_out=parts[g * e.partial_len:(g + 1) * e.partial_len])
+        engs.append(e)
+    engs[0].merge(parts, G)
+    w_sh = engs[0].weighted_noise()
+    np.testing.assert_allclose(w_sh, w_full, rtol=1e-10, atol=1e-12)
+    ess = None  # weights must really be spread for this test to mean something
+    S_dev = torch.empty(K, dtype=torch.float64, device="cuda")
+    full.rollout(noise, S_out=S_dev)
+    S = S_dev.cpu().numpy()
+    w = np.exp(-(S - S.min()) / 3.0e6)
+    ess = w.sum() ** 2 / (w ** 2).sum()
+    assert ess > 10
+    for e in engs + [full]:
+        e.close()
+
+
+def test_fused_device_update_matches_host_update(paths):
+    from scipy.ndimage import median_filter
+    K, T = 8192, 40
+    eng = _engine(K, T)
+    u = np.array([[10.0, -2.0]] * T) + np.random.default_rng(3).normal(0, 0.3, (T, 2))
+    eng.set_step_inputs(X0, _window(paths), u)
+    for step in range(3):
+        noise = eng.philox_noise(5, step)
+        eng.rollout(noise, fused_update=True)
+        w = eng.weighted_noise()
+        filt = np.stack([median_filter(w[:, d], size=10, mode="reflect") for d in range(2)], 1)
+        un = u + filt
+        expect = np.concatenate([un[1:], un[-1:]], 0)
+        got = eng.nominal()
+        np.testing.assert_allclose(got, expect, rtol=1e-13, atol=1e-13)
+        u = got
+    eng.close()
+
+
+def test_exploration_split_across_shards(paths):
+    K, T = 1000, 16
+    kw = dict(param_exploration=0.37)
+    full = _engine(K, T, **kw)
+    full.set_step_inputs(X0, _window(paths), np.array([[10.0, -2.0]] * T))
+    noise = full.philox_noise(1, 0)
+    S_full = torch.empty(K, dtype=torch.float64, device="cuda")
+    full.rollout(noise, S_out=S_full)
+    ref = coracle.rollout_costs(X0, np.array([[10.0, -2.0]] * T), noise.cpu().numpy(), _window(paths), 0.006,
+                                100.0, 0.98, np.eye(2) * 20.0, RUNPY["stage_cost_weight"],
+                                RUNPY["terminal_cost_weight"], O.ArmParams(),
+                                k_exploit=math.ceil(0.63 * K), layout="TK")
+    assert float(np.max(np.abs(S_full.cpu().numpy() - ref) / np.abs(ref))) < S_TOL
+    sh = _engine(400, T, K_total=K, k_offset=600, **kw)
+    sh.set_step_inputs(X0, _window(paths), np.array([[10.0, -2.0]] * T))
+    nz = sh.philox_noise(1, 0)
+    S_sh = torch.empty(400, dtype=torch.float64, device="cuda")
+    sh.rollout(nz, S_out=S_sh)
+    assert np.array_equal(S_sh.cpu().numpy(), S_full.cpu().numpy()[600:])
+    full.close()
+    sh.close()
+
+
+def test_philox_noise_statistics():
+    K, T = 65536, 64
+    sig = np.array([[20.0, 6.0], [6.0, 12.0]])
+    eng = _engine(K, T, sigma=sig)
+    z = eng.philox_noise(11, 0).double().reshape(-1, 2).cpu().numpy()
+    cov = np.cov(z.T)
+    np.testing.assert_allclose(z.mean(0), 0.0, atol=0.02)
+    np.testing.assert_allclose(cov, sig, rtol=0.01, atol=0.03)
+    z2 = eng.philox_noise(11, 1).cpu().numpy()
+    assert not np.array_equal(z2.reshape(-1, 2), z.astype(np.float32))
+    eng.close()
+
+
+def test_window_truncated_at_path_end(paths):
+    g = load_step("end_k64_t16")
+    ref = paths["xydq_circle"]
+    prev = int(g["prev_idx_after"])
+    win = ref[prev:prev + 30]
+    assert win.shape[0] < 30
+    eng = _engine(int(g["K"]), int(g["T"]))
+    eng.set_step_inputs(g["x0"], win, g["u_prev"])
+    noise = eng.upload_noise(g["eps"])
+    S_dev = torch.empty(int(g["K"]), dtype=torch.float64, device="cuda")
+    eng.rollout(noise, S_out=S_dev)
+    S = S_dev.cpu().numpy()
+    assert float(np.max(np.abs(S - g["S"]) / g["S"])) < S_TOL
+    eng.close()
+
+
+def test_error_paths(paths):
+    from mppi_robotarm_amd.controller import MPPIControllerForPathTracking
+    with pytest.raises(np.linalg.LinAlgError):
+        _engine(64, 8, sigma=np.array([[10.0, 10.0], [100.0, 100.0]]))
+    with pytest.raises(ValueError):
+        _engine(64, 129)
+    eng = _engine(64, 8)
+    with pytest.raises(ValueError):
+        eng.rollout(torch.zeros((8, 63, 2), device="cuda"))
+    with pytest.raises(ValueError):
+        eng.set_step_inputs(X0, np.zeros((31, 4)))
+    eng.close()
+    # default (singular) sigma raises LinAlgError at the reference's point, after the draw
+    c = MPPIControllerForPathTracking(delta_t=0.006, ref_path=paths["xydq_circle"], horizon_step_T=8,
+                                      number_of_samples_K=4, verbose=False)
+    with pytest.raises(np.linalg.LinAlgError):
+        with np.errstate(all="ignore"):
+            import warnings
+            with warnings.catch_warnings():
+                warnings.simplefilter("ignore")
+                c.calc_control_input(X0)

@@ -1,0 +1,4 @@
+set -u
+cd "$GRAFT_REPO_ROOT"; mkdir -p gpurun_out
+timeout -k 10 120 ./tools/ubench_valu > gpurun_out/ubench.log 2>&1 || exit $?
+timeout -k 10 120 rocprofv3 -L > gpurun_out/counters.txt 2>&1 || true

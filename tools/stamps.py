@@ -1,0 +1,61 @@
+"""Diagnostic timeline of the rollout kernel (stamp build, not the product).
+
+Usage: python tools/stamps.py LIB.so [K T steps]
+Prints, per recorded step: kernel span, per-workgroup rollout / epilogue
+durations, the last workgroup's merge / update, and the sample / partial counts.
+"""
+import os
+import sys
+
+lib = os.path.abspath(sys.argv[1])
+os.environ["MPPI_LIB_PATH"] = lib
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+sys.path.insert(0, os.path.join(ROOT, "oracle"))
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+
+from mppi_robotarm_amd import _native as N  # noqa: E402
+from mppi_robotarm_amd.engine import RolloutEngine  # noqa: E402
+from mppi_robotarm_amd.params import ArmParams, X0_RUNPY  # noqa: E402
+
+K = int(sys.argv[2]) if len(sys.argv) > 2 else 65536
+T = int(sys.argv[3]) if len(sys.argv) > 3 else 64
+steps = int(sys.argv[4]) if len(sys.argv) > 4 else 12
+lam = float(os.environ.get("LAMBDA", "100"))
+torch.cuda.set_device(0)
+eng = RolloutEngine(K, T, 0.006, lam, 0.98, np.eye(2) * 20.0, [0.5, 0.5, 5, 5], [5, 5, 50, 50], 0.0, ArmParams(),
+                    device=0, lanes_per_sample=int(os.environ.get("LPS", "0")))
+path = np.load(os.path.join(ROOT, "tests", "golden", "paths.npz"))["xydq_circle"][:, :4]
+eng.set_step_inputs(X0_RUNPY, path[:30], np.array([[10.0, -2.0]] * T))
+noise = [eng.philox_noise(1234, i) for i in range(4)]
+dbg = torch.zeros(eng.blocks * 16, dtype=torch.int64, device="cuda")
+N.check(eng._lib.mppi_debug_set_buffer(eng._ctx, N.C.c_void_p(dbg.data_ptr())), "dbg")
+print(f"K={K} T={T} lps={eng.lanes_per_sample} blocks={eng.blocks} lambda={lam} lib={os.path.basename(lib)}")
+S_dev = torch.empty(K, dtype=torch.float64, device="cuda")
+for i in range(steps):
+    dbg.zero_()
+    s0, s1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    s0.record()
+    eng.rollout(noise[i % 4], fused_update=True)
+    s1.record()
+    torch.cuda.synchronize()
+    d = dbg.view(-1, 16).cpu().numpy().astype(np.int64)
+    t0 = d[:, 0].min()
+    roll = (d[:, 1] - d[:, 0]) / 100.0   # us (100 MHz)
+    epi = (d[:, 2] - d[:, 1]) / 100.0
+    last = int(np.argmax(d[:, 7]))
+    merge = (d[last, 4] - d[last, 2]) / 100.0
+    upd = (d[last, 7] - d[last, 4]) / 100.0
+    span = (d[last, 7] - t0) / 100.0
+    start_spread = (d[:, 0].max() - t0) / 100.0
+    hw = d[:, 8]
+    cu = (d[:, 9] & 0xF) * 1000 + ((hw >> 13) & 7) * 100 + ((hw >> 12) & 1) * 16 + ((hw >> 8) & 0xF)
+    _, per_cu = np.unique(cu, return_counts=True)
+    occ = f"CUs {len(per_cu)} blocks/CU {np.bincount(per_cu).tolist()}"
+    print(f"step {i:2d}: {occ} | event {s0.elapsed_time(s1)*1e3:7.1f} us | span {span:6.1f} | starts spread {start_spread:5.1f} | "
+          f"rollout med {np.median(roll):6.1f} max {roll.max():6.1f} | epilogue med {np.median(epi):5.1f} max {epi.max():6.1f} | "
+          f"last-arrive {(d[last,3]-t0)/100:6.1f} merge {merge:6.1f} update {upd:5.1f} | nl med {np.median(d[:,5]):.0f} max {d[:,5].max()} | "
+          f"relevant partials {d[last,6]}")
+u = eng.nominal()
+print("final nominal u range", u.min(0), u.max(0))
