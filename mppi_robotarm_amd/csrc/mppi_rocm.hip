@@ -34,6 +34,7 @@
 #include <string.h>
 
 #include <string>
+#include <type_traits>
 
 #include "mppi_rocm.h"
 
@@ -134,7 +135,6 @@ __device__ __forceinline__ void dyn_step(ArmState& x, float v1, float v2, const 
 // --------------------------------------------------- merge + update helpers
 
 constexpr int kMaxWaves = 16;       // up to 1024-thread workgroups
-constexpr int kMergeChunk = 1024;
 constexpr int kGroup = 16;          // workgroups per first-level merge group
 // A partial whose rescale factor s = exp((rho - rho_i) / lambda) is below 2^-64
 // changes eta and N by less than 2^-64 * 512 relative to the leading term
@@ -159,15 +159,16 @@ __device__ __forceinline__ void st_wt(__amdgpu_buffer_rsrc_t r, int idx, double 
     __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u32x2, v), r, idx * 8, 0, kSC1);
 }
 
+constexpr int kMergeRows = 32;   // rows per load round in a merge
+
 struct MergeScratch {
     double red[kMaxWaves];
-    int cnt[kMaxWaves];
-    int list_i[kMergeChunk];
-    double list_s[kMergeChunk];
+    double rho_i[kMergeRows];
+    double s_i[kMergeRows];
     double weps[2 * kMaxT];
     double unew[2 * kMaxT];
     double rho, eta;
-    int n, nrel;
+    int nrel;
 };
 
 template <int NT>
@@ -184,59 +185,62 @@ __device__ __forceinline__ double block_min_f64(double v, MergeScratch& sm) {
 }
 
 // Merge n rows {rho, eta, N[2T]} (row stride 2 + 2T, read write-through from
-// `rows`) with a log-sum-exp rescale: rho = min rho_i,
-// s_i = exp((rho - rho_i) / lambda), eta = sum s_i eta_i, N = sum s_i N_i over
-// the rows with s_i >= 2^-64, in ascending row order (deterministic).
-// The merged row goes to out_wt (write-through, next merge level) or out_row
+// `rows`) with a log-sum-exp rescale, rho = min rho_i, s_i = exp((rho - rho_i)
+// / lambda), eta = sum s_i eta_i, N = sum s_i N_i, in ascending row order
+// (deterministic).  Rows are consumed kMergeRows at a time, every load of a
+// round issued together (one memory round trip per round) with an online
+// rescale of the running sums when a round lowers rho; rows whose factor is
+// below 2^-64 of the running best are skipped (below fp64 resolution).
+// The merged row goes to out_wt (write-through, next level) and/or out_row
 // (plain, read after the launch); with `final`, w_eps = N / eta
 // (control.py:112-118) goes to sm.weps and w_eps_out.
 template <int NT>
 __device__ void merge_rows_block(__amdgpu_buffer_rsrc_t rows, int row0, int n, const KConst& c, MergeScratch& sm,
                                  const __amdgpu_buffer_rsrc_t* out_wt, int out_idx, double* out_row, bool final,
                                  double* w_eps_out) {
-    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int tid = threadIdx.x;
     const int stride = 2 + 2 * c.T;
-    const int ncol = 2 * c.T + 1;  // col 0 = eta, col 1 + j = N[j]
-    double m = INFINITY;
-    for (int i = tid; i < n; i += NT) m = fmin(m, ld_wt(rows, (row0 + i) * stride));
-    const double rho = block_min_f64<NT>(m, sm);
-    if (tid == 0) sm.nrel = 0;
-    double acc0 = 0.0, acc1 = 0.0;  // columns tid and tid + NT (2T + 1 <= 257)
-    for (int chunk = 0; chunk < n; chunk += kMergeChunk) {
-        const int cend = min(n, chunk + kMergeChunk);
-        if (tid == 0) sm.n = 0;
+    const int ncol = 2 * c.T + 1;            // col 0 = eta, col 1 + j = N[j]
+    const bool has0 = tid < ncol, has1 = tid + NT < ncol;
+    double acc0 = 0.0, acc1 = 0.0, rho = INFINITY;
+    int nrel = 0;
+    for (int r0 = 0; r0 < n; r0 += kMergeRows) {
+        const int nr = min(kMergeRows, n - r0);
+        double v[kMergeRows];
+#pragma unroll
+        for (int i = 0; i < kMergeRows; ++i)
+            v[i] = has0 ? ld_wt(rows, (row0 + r0 + min(i, nr - 1)) * stride + 1 + tid) : 0.0;
+        if (tid < nr) sm.rho_i[tid] = ld_wt(rows, (row0 + r0 + tid) * stride);
         __syncthreads();
-        for (int base = chunk; base < cend; base += NT) {
-            const int i = base + tid;
-            double s = 0.0;
-            if (i < cend) s = exp((rho - ld_wt(rows, (row0 + i) * stride)) * c.inv_lambda);
-            const bool keep = (i < cend) && (s >= kMergeFloor);
-            const unsigned long long bal = __ballot(keep);
-            if (lane == 0) sm.cnt[wave] = __popcll(bal);
-            __syncthreads();
-            int off = sm.n;
-            for (int w = 0; w < wave; ++w) off += sm.cnt[w];
-            if (keep) {
-                const int pos = off + lanes_below(bal);
-                sm.list_i[pos] = i;
-                sm.list_s[pos] = s;
-            }
-            __syncthreads();
-            if (tid == 0) {
-                int tot = sm.n;
-                for (int w = 0; w < NT / 64; ++w) tot += sm.cnt[w];
-                sm.n = tot;
-            }
-            __syncthreads();
+        double rnew = rho;
+        for (int i = 0; i < nr; ++i) rnew = fmin(rnew, sm.rho_i[i]);
+        if (tid < nr) {
+            const double s = exp((rnew - sm.rho_i[tid]) * c.inv_lambda);
+            sm.s_i[tid] = s >= kMergeFloor ? s : 0.0;
         }
-        const int nl = sm.n;
-        if (tid < ncol)
-            for (int l = 0; l < nl; ++l)
-                acc0 = fma(sm.list_s[l], ld_wt(rows, (row0 + sm.list_i[l]) * stride + 1 + tid), acc0);
-        if (tid + NT < ncol)
-            for (int l = 0; l < nl; ++l)
-                acc1 = fma(sm.list_s[l], ld_wt(rows, (row0 + sm.list_i[l]) * stride + 1 + tid + NT), acc1);
-        if (tid == 0) sm.nrel += nl;
+        __syncthreads();
+        if (rnew < rho) {  // uniform: rescale the running sums to the new minimum
+            const double f = exp((rnew - rho) * c.inv_lambda);
+            acc0 *= f;
+            acc1 *= f;
+        }
+        rho = rnew;
+#pragma unroll
+        for (int i = 0; i < kMergeRows; ++i) {
+            if (i < nr) {
+                const double s = sm.s_i[i];
+                if (s != 0.0) {
+                    acc0 = fma(s, v[i], acc0);
+                    nrel += (tid == 0);
+                }
+            }
+        }
+        if (ncol > NT) {  // second column pass (T = 128 only: 2T + 1 = 257 columns)
+            for (int i = 0; i < nr; ++i) {
+                const double s = sm.s_i[i];
+                if (s != 0.0 && has1) acc1 = fma(s, ld_wt(rows, (row0 + r0 + i) * stride + 1 + tid + NT), acc1);
+            }
+        }
         __syncthreads();
     }
     auto put = [&](int col, double v) {  // col 0 = rho, 1 = eta, 2 + j = N[j]
@@ -245,13 +249,14 @@ __device__ void merge_rows_block(__amdgpu_buffer_rsrc_t rows, int row0, int n, c
     };
     if (tid == 0) {
         sm.eta = acc0;
+        sm.nrel = nrel;
         put(0, rho);
         put(1, acc0);
-    } else if (tid < ncol) {
+    } else if (has0) {
         sm.weps[tid - 1] = acc0;
         put(1 + tid, acc0);
     }
-    if (tid + NT < ncol) {
+    if (has1) {
         sm.weps[tid + NT - 1] = acc1;
         put(1 + tid + NT, acc1);
     }
@@ -283,11 +288,22 @@ __device__ __forceinline__ bool arrive_last(unsigned* counter, unsigned expected
     return *s_flag != 0;
 }
 
+// Upper median of 10 (rank 5): a 29-comparator sorting network (verified on all
+// 2^10 0/1 inputs), the element scipy.ndimage.median_filter(size=10) returns.
+__device__ __forceinline__ double median10(double* v) {
+#define CX(i, j) { const double lo = fmin(v[i], v[j]), hi = fmax(v[i], v[j]); v[i] = lo; v[j] = hi; }
+    CX(4, 9) CX(3, 8) CX(2, 7) CX(1, 6) CX(0, 5) CX(1, 4) CX(6, 9) CX(0, 3) CX(5, 8) CX(0, 2)
+    CX(3, 6) CX(7, 9) CX(0, 1) CX(2, 4) CX(5, 7) CX(8, 9) CX(1, 2) CX(4, 6) CX(7, 8) CX(3, 5)
+    CX(2, 5) CX(6, 8) CX(1, 3) CX(4, 7) CX(2, 3) CX(6, 7) CX(3, 4) CX(5, 6) CX(4, 5)
+#undef CX
+    return v[5];
+}
+
 // Median filter (scipy.ndimage.median_filter(size=10, mode='reflect'),
-// control.py:319-327, valid for T >= 5), u += w_eps (control.py:126), shift
-// (control.py:148-149) and the fp32 per-step constants of the next launch.
-// u_cur: this thread's element cur->u[t][d] (t = tid / 2, d = tid % 2), read
-// at kernel entry.
+// control.py:319-327, window [t-5, t+4], valid for T >= 5), u += w_eps
+// (control.py:126), shift (control.py:148-149) and the fp32 per-step constants
+// of the next launch.  u_cur: this thread's cur->u[t][d] (t = tid/2, d = tid%2),
+// read at kernel entry.
 template <int NT>
 __device__ void nominal_update_block(const DevStep* cur, DevStep* nxt, const KConst& c, MergeScratch& sm,
                                      double u_cur) {
@@ -298,24 +314,12 @@ __device__ void nominal_update_block(const DevStep* cur, DevStep* nxt, const KCo
         double v[10];
 #pragma unroll
         for (int i = 0; i < 10; ++i) {
-            int m = t - 5 + i;
-            m %= 2 * T;
-            if (m < 0) m += 2 * T;
-            if (m >= T) m = 2 * T - 1 - m;
+            int m = t - 5 + i;              // one reflection suffices for T >= 5
+            m = m < 0 ? -m - 1 : m;
+            m = m >= T ? 2 * T - 1 - m : m;
             v[i] = sm.weps[2 * m + d];
         }
-        double med = v[0];
-#pragma unroll
-        for (int i = 0; i < 10; ++i) {  // element of rank 5 (upper median)
-            int less = 0, leq = 0;
-#pragma unroll
-            for (int j = 0; j < 10; ++j) {
-                less += v[j] < v[i];
-                leq += v[j] <= v[i];
-            }
-            if (less <= 5 && 5 < leq) med = v[i];
-        }
-        sm.unew[tid] = u_cur + med;
+        sm.unew[tid] = u_cur + median10(v);
     }
     __syncthreads();
     if (tid < T) {
@@ -328,14 +332,8 @@ __device__ void nominal_update_block(const DevStep* cur, DevStep* nxt, const KCo
         const double a1 = g0 * c.sig_inv[1] + g1 * c.sig_inv[3];
         nxt->ua[tid] = make_float4((float)u0, (float)u1, (float)a0, (float)a1);
     }
-    if (tid < kSlots) {
-        nxt->win[tid] = cur->win[tid];
-        nxt->key[tid] = cur->key[tid];
-    }
-    if (tid == 0) {
-        nxt->x0 = cur->x0;
-        nxt->ctr = cur->ctr;
-    }
+    // win / key / x0 / ctr are written to both ping-pong blocks by
+    // mppi_set_step_inputs, so only the nominal moves here.
 }
 
 // ------------------------------------------------------------ rollout kernel
@@ -360,28 +358,49 @@ __device__ __forceinline__ float2 noise_ld(const float2* p) { return *p; }
 typedef __attribute__((address_space(4))) const float cfloat;
 __device__ __forceinline__ float4 const_ld4(cfloat* p) { return make_float4(p[0], p[1], p[2], p[3]); }
 
+typedef float f32x2 __attribute__((ext_vector_type(2)));
+
+// v_min3_f32 / v_min_f32 issued directly: the operands are bit-packed keys, and
+// fminf() would make hipcc canonicalise every one of them (v_max x, x) first.
+__device__ __forceinline__ float min3_raw(float a, float b, float c) {
+    float r;
+    asm("v_min3_f32 %0, %1, %2, %3" : "=v"(r) : "v"(a), "v"(b), "v"(c));
+    return r;
+}
+__device__ __forceinline__ float min_raw(float a, float b) {
+    float r;
+    asm("v_min_f32 %0, %1, %2" : "=v"(r) : "v"(a), "v"(b));
+    return r;
+}
+
 template <int LPS>
 struct Search {
-    static constexpr int SL = (MPPI_SEARCH_LEN + LPS - 1) / LPS;  // window slots per lane
-    float krx[SL], kry[SL], kc[SL];
+    // window slots per lane, even so they pair up for packed math
+    static constexpr int SL = ((MPPI_SEARCH_LEN + LPS - 1) / LPS + 1) & ~1;
+    static constexpr int SP = SL / 2;
+    f32x2 krx[SP], kry[SP], kc[SP];
     int sub;
     float cx, cy;
 
     // Nearest waypoint of the shared window (control.py:208-215):
     //   argmin_j |p - r_j|^2 = argmin_j (|r'_j|^2 - 2 p'.r'_j) (window-centred),
-    // the slot index packed into the 5 low mantissa bits so one min per slot
-    // carries the argmin; the LPS lanes of a sample close it with DPP.
+    // two slots per v_pk_fma_f32; the slot index is packed into the 5 low
+    // mantissa bits so one v_min3 per two slots carries the argmin; the LPS
+    // lanes of a sample close it with DPP.
     __device__ __forceinline__ unsigned nearest(float px, float py) const {
         const float ax = -2.f * (px - cx), ay = -2.f * (py - cy);
+        const f32x2 ax2 = {ax, ax}, ay2 = {ay, ay};
         float best = 3.0e38f;
 #pragma unroll
-        for (int i = 0; i < SL; ++i) {
-            const float key = fmaf(ax, krx[i], fmaf(ay, kry[i], kc[i]));
-            const unsigned kb = (__float_as_uint(key) & ~31u) | (unsigned)(sub * SL + i);
-            best = fminf(best, __uint_as_float(kb));
+        for (int i = 0; i < SP; ++i) {
+            const f32x2 key = __builtin_elementwise_fma(ax2, krx[i], __builtin_elementwise_fma(ay2, kry[i], kc[i]));
+            const unsigned j = (unsigned)(sub * SL + 2 * i);
+            const float k0 = __uint_as_float((__float_as_uint(key.x) & ~31u) | j);
+            const float k1 = __uint_as_float((__float_as_uint(key.y) & ~31u) | (j + 1));
+            best = min3_raw(best, k0, k1);
         }
-        if (LPS >= 2) best = fminf(best, dpp_f32<0xB1>(best));  // quad_perm xor 1
-        if (LPS >= 4) best = fminf(best, dpp_f32<0x4E>(best));  // quad_perm xor 2
+        if (LPS >= 2) best = min_raw(best, dpp_f32<0xB1>(best));  // quad_perm xor 1
+        if (LPS >= 4) best = min_raw(best, dpp_f32<0x4E>(best));  // quad_perm xor 2
         return __float_as_uint(best) & 31u;
     }
 };
@@ -401,6 +420,7 @@ __device__ __forceinline__ float weighted_sq(float ex, float ey, float e1, float
 #endif
 
 constexpr int kPF = 4;  // noise rows in flight per lane
+constexpr int kSparseMax = 16;  // weighted samples per workgroup handled by the gather path
 
 template <int LPS, int NT>
 __global__ __launch_bounds__(NT) void rollout_kernel(
@@ -441,12 +461,14 @@ __global__ __launch_bounds__(NT) void rollout_kernel(
     } else {
         sr.sub = tid & (LPS - 1);
     }
+    static_assert(Search<LPS>::SL * LPS <= kSlots, "window slots");
 #pragma unroll
-    for (int i = 0; i < Search<LPS>::SL; ++i) {
-        const float4 kk = st->key[sr.sub * Search<LPS>::SL + i];
-        sr.krx[i] = kk.x;
-        sr.kry[i] = kk.y;
-        sr.kc[i] = kk.z;
+    for (int i = 0; i < Search<LPS>::SP; ++i) {
+        const float4 k0 = st->key[sr.sub * Search<LPS>::SL + 2 * i];
+        const float4 k1 = st->key[sr.sub * Search<LPS>::SL + 2 * i + 1];
+        sr.krx[i] = f32x2{k0.x, k1.x};
+        sr.kry[i] = f32x2{k0.y, k1.y};
+        sr.kc[i] = f32x2{k0.z, k1.z};
     }
     sr.cx = st->ctr.x;
     sr.cy = st->ctr.y;
@@ -473,9 +495,12 @@ __global__ __launch_bounds__(NT) void rollout_kernel(
     // Horizon loop (control.py:95-109): v = u + eps -> _F -> end effector ->
     // nearest waypoint -> stage cost + control cost, S in fp64.
     double S = 0.0;
+    float S4 = 0.f;  // fp32 partial over one 4-step block, folded into fp64 S
     float ex = 0.f, ey = 0.f, e1 = 0.f, e2 = 0.f;
-    auto step = [&](int t) {
-        const int slot = t % kPF;
+    // `slot` (= t % kPF) is a compile-time constant at every call, so the rings
+    // stay in registers (a runtime index sends them to scratch).
+    auto step = [&](int t, auto slot_c) {
+        constexpr int slot = decltype(slot_c)::value;
         const float2 e = ring[slot];
         const float4 ua = uring[slot];
         const int tl = t + kPF < T ? t + kPF : T - 1;
@@ -493,14 +518,26 @@ __global__ __launch_bounds__(NT) void rollout_kernel(
         e1 = x.dq1 - r.z;
         e2 = x.dq2 - r.w;
         const float g = fmaf(ua.z, v1, ua.w * v2);  // (gamma u^T Sigma^-1) v, control.py:106
-        S += (double)(weighted_sq(ex, ey, e1, e2, c.sw) + g);
+        S4 += weighted_sq(ex, ey, e1, e2, c.sw) + g;
     };
+    using I0 = std::integral_constant<int, 0>;
+    using I1 = std::integral_constant<int, 1>;
+    using I2 = std::integral_constant<int, 2>;
+    using I3 = std::integral_constant<int, 3>;
+    static_assert(kPF == 4, "unrolled for a 4-deep ring");
     int t = 0;
     for (; t + kPF <= T; t += kPF) {
-#pragma unroll
-        for (int j = 0; j < kPF; ++j) step(t + j);
+        step(t, I0{});
+        step(t + 1, I1{});
+        step(t + 2, I2{});
+        step(t + 3, I3{});
+        S += (double)S4;
+        S4 = 0.f;
     }
-    for (; t < T; ++t) step(t);
+    if (t < T) step(t, I0{});          // remainder: t % kPF == 0, 1, 2 in order
+    if (t + 1 < T) step(t + 1, I1{});
+    if (t + 2 < T) step(t + 2, I2{});
+    S += (double)S4;
     S += (double)weighted_sq(ex, ey, e1, e2, c.tw);  // terminal cost, control.py:109
 
     STAMP(1, NOW());
@@ -539,12 +576,48 @@ __global__ __launch_bounds__(NT) void rollout_kernel(
     const int ngroups = (nrows + kGroup - 1) / kGroup;
     const __amdgpu_buffer_rsrc_t slab_r = rows_rsrc(slab, nrows * stride * 8);
     const __amdgpu_buffer_rsrc_t gslab_r = rows_rsrc(gslab, ngroups * stride * 8);
-    const float* nf = reinterpret_cast<const float*>(noise);
-    for (int col = tid; col < 2 * T; col += NT) {
-        const float* base = nf + (size_t)(col >> 1) * K * 2 + (col & 1);
-        double acc = 0.0;
-        for (int l = 0; l < nl; ++l) acc = fma((double)s_e[l], (double)base[(size_t)s_k[l] * 2], acc);
-        st_wt(slab_r, blockIdx.x * stride + 2 + col, acc);
+    if (nl <= kSparseMax) {
+        // few weighted samples (the usual case: S spread >> lambda): column
+        // threads gather eps[t][k_l] for the listed samples
+        const float* nf = reinterpret_cast<const float*>(noise);
+        for (int col = tid; col < 2 * T; col += NT) {
+            const float* base = nf + (size_t)(col >> 1) * K * 2 + (col & 1);
+            double acc = 0.0;
+            for (int l = 0; l < nl; ++l) acc = fma((double)s_e[l], (double)base[(size_t)s_k[l] * 2], acc);
+            st_wt(slab_r, blockIdx.x * stride + 2 + col, acc);
+        }
+    } else {
+        // dense weights: each wave takes whole rows eps[t][k0 : k0 + NS] (coalesced),
+        // lane l owns samples l, l + 64, ..., then a wave reduction per row
+        constexpr int NS = NT / LPS;               // samples of this workgroup
+        constexpr int PER = (NS + 63) / 64;
+        const int k0 = blockIdx.x * NS;
+        if (tid < NS) s_e[tid] = 0.f;
+        __syncthreads();
+        if (nz) s_e[k - k0] = wgt;
+        __syncthreads();
+        double w[PER];
+#pragma unroll
+        for (int i = 0; i < PER; ++i) {
+            const int ks = lane + 64 * i;
+            w[i] = (ks < NS && k0 + ks < K) ? (double)s_e[ks] : 0.0;
+        }
+        for (int tr = wave; tr < T; tr += NT / 64) {
+            double ax = 0.0, ay = 0.0;
+#pragma unroll
+            for (int i = 0; i < PER; ++i) {
+                const int ks = lane + 64 * i;
+                const float2 e = (w[i] != 0.0) ? noise[(size_t)tr * K + k0 + ks] : make_float2(0.f, 0.f);
+                ax = fma(w[i], (double)e.x, ax);
+                ay = fma(w[i], (double)e.y, ay);
+            }
+            ax = wave_sum_f64(ax);
+            ay = wave_sum_f64(ay);
+            if (lane == 0) {
+                st_wt(slab_r, blockIdx.x * stride + 2 + 2 * tr, ax);
+                st_wt(slab_r, blockIdx.x * stride + 3 + 2 * tr, ay);
+            }
+        }
     }
     if (tid == 0) {
         st_wt(slab_r, blockIdx.x * stride, rho_b);
@@ -698,12 +771,14 @@ int launch_check(const char* what) {
 }
 
 int auto_lps(int K_local) {
-    // Measured on MI355X (tools/ubench_valu.hip): one wave issues a VALU op at
-    // most every ~8 cycles, 2 waves/SIMD reach ~4.4, 4 waves ~3.0.  Splitting
-    // the window search over 2 lanes per sample doubles the wave count at
-    // ~1.5x the instructions per sample: worth it below 2 waves per SIMD.
+    // Measured on MI355X (tools/ubench_valu.hip, tools/stamps.py): a lone wave
+    // issues a VALU op every ~6-8 cycles, 2 waves/SIMD ~4.4, 4 waves ~3.0.
+    // Splitting the window search over LPS lanes multiplies the instructions
+    // per sample by ~1.6 (LPS=2) / ~2.7 (LPS=4); at K = 65536 (one wave per
+    // SIMD) one lane per sample won (37 vs 45 us span), so split only when the
+    // grid would leave SIMDs empty.
     const long long waves1 = ((long long)K_local + 63) / 64;
-    if (waves1 >= 2048) return 1;
+    if (waves1 >= 1024) return 1;
     if (waves1 >= 256) return 2;
     return 4;
 }
@@ -878,6 +953,8 @@ int mppi_set_step_inputs(mppi_ctx* c, const double* x0, const double* window, in
         }
         bytes = sizeof(DevStep);
     }
+    // static part (window, keys, x0) into both ping-pong blocks, nominal into the current one
+    HIP_TRY(hipMemcpyAsync(c->d_step + (c->cur ^ 1), h, offsetof(DevStep, ua), hipMemcpyHostToDevice, c->stream));
     HIP_TRY(hipMemcpyAsync(c->d_step + c->cur, h, bytes, hipMemcpyHostToDevice, c->stream));
     HIP_TRY(hipEventRecord(c->staged, c->stream));
     return MPPI_OK;

@@ -119,10 +119,12 @@ def _window(paths, prev=0):
     return paths["xydq_circle"][prev:prev + 30]
 
 
-@pytest.mark.parametrize("K,T", [(65536, 64), (4096, 32), (3000, 7)])
-def test_large_rollout_against_c_oracle(K, T, paths):
-    """Full-size S on a sample subset, and the full weighted noise, vs the C fp64 oracle."""
-    eng = _engine(K, T)
+@pytest.mark.parametrize("K,T,lam,lps", [(65536, 64, 100.0, 0), (65536, 64, 3.0e6, 0), (65536, 64, 100.0, 2),
+                                         (4096, 32, 100.0, 0), (3000, 7, 100.0, 1), (20000, 128, 1.0e6, 0)])
+def test_large_rollout_against_c_oracle(K, T, lam, lps, paths):
+    """Full-size S and the full weighted noise vs the C fp64 oracle (one-hot and
+    dense weights, every lanes-per-sample variant, T up to the 128 limit)."""
+    eng = _engine(K, T, lps=lps, param_lambda=lam)
     win = _window(paths)
     u = np.array([[10.0, -2.0]] * T) + np.random.default_rng(1).normal(0, 0.5, (T, 2))
     eng.set_step_inputs(X0, win, u)
@@ -132,13 +134,13 @@ def test_large_rollout_against_c_oracle(K, T, paths):
     w_eps = eng.weighted_noise()
     S = S_dev.cpu().numpy()
     eps_tk = noise.cpu().numpy()
-    ref_S = coracle.rollout_costs(X0, u, eps_tk, win, 0.006, 100.0, 0.98, np.eye(2) * 20.0,
+    ref_S = coracle.rollout_costs(X0, u, eps_tk, win, 0.006, lam, 0.98, np.eye(2) * 20.0,
                                   RUNPY["stage_cost_weight"], RUNPY["terminal_cost_weight"], O.ArmParams(),
                                   layout="TK")
     rel = np.abs(S - ref_S) / np.abs(ref_S)
     assert float(np.max(rel)) < S_TOL
     assert int(np.argmin(S)) == int(np.argmin(ref_S))
-    _, ref_weps = coracle.weighted_noise(ref_S, eps_tk, 100.0, layout="TK")
+    _, ref_weps = coracle.weighted_noise(ref_S, eps_tk, lam, layout="TK")
     assert _urel(w_eps, ref_weps) < U_TOL
     eng.close()
 

@@ -1,0 +1,8 @@
+set -u
+cd "$GRAFT_REPO_ROOT"; mkdir -p gpurun_out
+timeout -k 10 300 python -m pytest tests -m gpu -q > gpurun_out/t8.log 2>&1; rc=$?; tail -3 gpurun_out/t8.log; [ $rc -le 1 ] || exit $rc
+timeout -k 10 200 python tools/stamps.py mppi_robotarm_amd/_lib/libmppi_rocm_stamps.so 65536 64 5 > gpurun_out/st8.log 2>&1 || exit $?
+LPS=1 timeout -k 10 200 python tools/stamps.py mppi_robotarm_amd/_lib/libmppi_rocm_stamps.so 65536 64 3 >> gpurun_out/st8.log 2>&1 || exit $?
+LPS=4 timeout -k 10 200 python tools/stamps.py mppi_robotarm_amd/_lib/libmppi_rocm_stamps.so 65536 64 3 >> gpurun_out/st8.log 2>&1 || exit $?
+LAMBDA=3e6 timeout -k 10 200 python tools/stamps.py mppi_robotarm_amd/_lib/libmppi_rocm_stamps.so 65536 64 3 >> gpurun_out/st8.log 2>&1 || exit $?
+timeout -k 10 300 python bench.py --steps 200 --warmup 20 --cpu-seconds 0 > gpurun_out/b8.log 2>&1 || exit $?
