@@ -33,6 +33,7 @@ import torch
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
+from mppi_robotarm_amd.distributed import exchange_partials  # noqa: E402
 from mppi_robotarm_amd.engine import RolloutEngine  # noqa: E402
 from mppi_robotarm_amd.params import ArmParams, X0_RUNPY  # noqa: E402
 
@@ -51,6 +52,7 @@ def parse():
     p.add_argument("--lps", type=int, default=0, help="lanes per sample (0 = auto)")
     p.add_argument("--cpu-seconds", type=float, default=10.0, help="CPU baseline budget (0 = skip)")
     p.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "traffic.json"))
+    p.add_argument("--no-graph", action="store_true", help="N = 1: launch eagerly instead of replaying a HIP graph")
     return p.parse_args()
 
 
@@ -103,41 +105,63 @@ def main():
     gathered = torch.empty(world * eng.partial_len, dtype=torch.float64, device=eng.device)
     stream = torch.cuda.current_stream()
 
-    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(args.steps)]
+    # N = 1: the device-resident loop has no host synchronisation, so a chunk of
+    # steps (one per noise buffer, an even count so the ping-pong parameter
+    # block returns to the same parity) is captured once into a HIP graph and
+    # replayed; launch overhead is then one graph launch per chunk.
+    use_graph = world == 1 and not args.no_graph and args.nbuf % 2 == 0
+    chunk = args.nbuf if use_graph else 1
+    steps = (args.steps + chunk - 1) // chunk * chunk
 
-    def step(i, timed=False):
-        if timed:
-            ev[i][0].record(stream)
+    def step(i):
         if world == 1:
             eng.rollout(noise[i % args.nbuf], fused_update=True)
-            if timed:
-                ev[i][1].record(stream)
         else:
             eng.rollout(noise[i % args.nbuf], partial_out=partial)
-            if timed:
-                ev[i][1].record(stream)
-            dist.all_gather_into_tensor(gathered, partial)
+            exchange_partials(partial, gathered)
             eng.merge(gathered, world, fused_update=True)
 
     for i in range(args.warmup):
         step(i)
     torch.cuda.synchronize()
+    graph = None
+    if use_graph:
+        s_cap = torch.cuda.Stream()
+        s_cap.wait_stream(torch.cuda.current_stream())
+        with torch.cuda.stream(s_cap):
+            graph = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(graph, stream=s_cap):
+                for i in range(chunk):
+                    step(i)
+        torch.cuda.current_stream().wait_stream(s_cap)
+        graph.replay()      # one untimed replay
+        torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
+    nev = steps // chunk
+    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(nev)]
     t0 = time.perf_counter()
-    for i in range(args.steps):
-        step(i, timed=True)
+    for c in range(nev):
+        ev[c][0].record(stream)
+        if graph is not None:
+            graph.replay()
+        else:
+            step(c)
+        ev[c][1].record(stream)
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
     elapsed = time.perf_counter() - t0
-    kern_ms = sum(a.elapsed_time(b) for a, b in ev) / args.steps
+    # average duration per launch of the step (events on the launch stream);
+    # with a graph this includes the ~1.5 us dependent-kernel boundaries
+    kern_ms = sum(a.elapsed_time(b) for a, b in ev) / steps
     if world > 1:
         tt = torch.tensor([elapsed, kern_ms], dtype=torch.float64, device=eng.device)
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
         elapsed, kern_ms = float(tt[0]), float(tt[1])
+    args.steps = steps
     u_final = eng.nominal()
     assert np.all(np.isfinite(u_final)), "non-finite nominal control"
 
@@ -174,7 +198,7 @@ def main():
                                    f"xydq_circle.txt window, Philox N(0,20I) noise x{args.nbuf} buffers",
                        "K_total": K_total, "K_per_gpu": K, "T": T, "lanes_per_sample": eng.lanes_per_sample,
                        "parallelism": f"samples sharded x{world}, RCCL all_gather of partials" if world > 1
-                       else "single device, fused update"},
+                       else "single device, fused update" + (f", HIP graph of {chunk} steps" if use_graph else "")},
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": achieved / HBM_PEAK_GBS, "traffic": traffic},
         }

@@ -30,6 +30,7 @@ import numpy as np
 import torch
 from scipy.ndimage import median_filter
 
+from .distributed import exchange_partials, shard_geometry
 from .engine import RolloutEngine
 from .params import ArmParams
 
@@ -104,11 +105,7 @@ class MPPIControllerForPathTracking:
     def _get_engine(self) -> RolloutEngine:
         if self._engine is None:
             world, rank = self._shard()
-            if self.K < world:
-                raise ValueError("number_of_samples_K must be >= the number of ranks")
-            base, rem = divmod(self.K, world)
-            K_local = base + (1 if rank < rem else 0)
-            k_offset = rank * base + min(rank, rem)
+            K_local, k_offset = shard_geometry(self.K, world, rank)
             device = self._device if self._device is not None else torch.cuda.current_device()
             self._engine = RolloutEngine(
                 K_local, self.T, self.delta_t, self.param_lambda, self.param_alpha, self.Sigma,
@@ -154,9 +151,8 @@ class MPPIControllerForPathTracking:
         if world == 1:
             eng.rollout(self._noise_dev, S_out=self._S_dev if self.keep_costs else None)
         else:
-            import torch.distributed as dist
             eng.rollout(self._noise_dev, S_out=self._S_dev if self.keep_costs else None, partial_out=self._partial)
-            dist.all_gather_into_tensor(self._gathered, self._partial, group=self.process_group)
+            exchange_partials(self._partial, self._gathered, self.process_group)
             eng.merge(self._gathered, world)
         w_epsilon = eng.weighted_noise()
         if self.keep_costs:

@@ -139,11 +139,13 @@ class RolloutEngine:
 
     def weighted_noise(self) -> np.ndarray:
         """w_eps (T, 2) fp64 of the last rollout / merge (synchronising)."""
+        self._sync_stream()
         out = np.zeros((self.T, 2))
         N.check(self._lib.mppi_get_weighted_noise(self._ctx, _dptr(out)), "mppi_get_weighted_noise")
         return out
 
     def nominal(self) -> np.ndarray:
+        self._sync_stream()
         out = np.zeros((self.T, 2))
         N.check(self._lib.mppi_get_nominal(self._ctx, _dptr(out)), "mppi_get_nominal")
         return out

@@ -1,0 +1,79 @@
+"""CPU: the C-ABI library loads and exports every entry point include/mppi_rocm.h
+declares, and the ctypes mirror of the config structs matches the C layout
+(checked against a gcc-compiled probe of the header).  No compute calls."""
+import ctypes as C
+import os
+import re
+import subprocess
+
+import pytest
+
+from conftest import ROOT
+
+HEADER = os.path.join(ROOT, "include", "mppi_rocm.h")
+
+
+def declared_functions():
+    text = open(HEADER).read()
+    text = re.sub(r"/\*.*?\*/", "", text, flags=re.S)
+    return sorted(set(re.findall(r"\b(mppi_[a-z_]+)\s*\(", text)))
+
+
+def test_header_declares_the_python_export_list():
+    from mppi_robotarm_amd import _native
+    assert declared_functions() == sorted(_native.EXPORTS)
+
+
+def test_library_loads_and_exports_every_symbol():
+    from mppi_robotarm_amd import _native
+    if not os.path.exists(_native.LIB_PATH):
+        from mppi_robotarm_amd.build import build_native
+        build_native()
+    lib = _native.load()
+    for name in declared_functions():
+        assert hasattr(lib, name), name
+    nm = subprocess.run(["nm", "-D", "--defined-only", _native.LIB_PATH], capture_output=True, text=True).stdout
+    exported = set(re.findall(r"\bT (mppi_\w+)", nm))
+    assert set(declared_functions()) <= exported
+
+
+def test_struct_layout_matches_header(tmp_path):
+    from mppi_robotarm_amd import _native as N
+    probe = tmp_path / "probe.c"
+    probe.write_text(r'''
+#include <stddef.h>
+#include <stdio.h>
+#include "mppi_rocm.h"
+int main(void) {
+  printf("%zu %zu %zu %zu %zu %zu %zu %zu\n", sizeof(mppi_config), sizeof(mppi_arm_params),
+         offsetof(mppi_config, delta_t), offsetof(mppi_config, sigma), offsetof(mppi_config, stage_cost_weight),
+         offsetof(mppi_config, terminal_cost_weight), offsetof(mppi_config, arm),
+         offsetof(mppi_config, lanes_per_sample));
+  return 0;
+}
+''')
+    exe = tmp_path / "probe"
+    subprocess.run(["gcc", "-I", os.path.dirname(HEADER), str(probe), "-o", str(exe)], check=True)
+    vals = [int(v) for v in subprocess.run([str(exe)], capture_output=True, text=True, check=True).stdout.split()]
+    Cc = N.ConfigC
+    assert vals == [C.sizeof(Cc), C.sizeof(N.ArmParamsC), Cc.delta_t.offset, Cc.sigma.offset,
+                    Cc.stage_cost_weight.offset, Cc.terminal_cost_weight.offset, Cc.arm.offset,
+                    Cc.lanes_per_sample.offset]
+
+
+def test_constants_match_header():
+    from mppi_robotarm_amd import _native as N
+    text = open(HEADER).read()
+    for name in ("MPPI_MAX_T", "MPPI_SEARCH_LEN", "MPPI_OK", "MPPI_E_ARG", "MPPI_E_HIP", "MPPI_E_SINGULAR"):
+        m = re.search(rf"#define {name}\s+(-?\d+)", text)
+        assert m and int(m.group(1)) == getattr(N, name), name
+    assert re.search(r"#define MPPI_FLAG_FUSED_UPDATE\s+1u", text) and N.MPPI_FLAG_FUSED_UPDATE == 1
+
+
+def test_missing_library_fails_loudly(monkeypatch, tmp_path):
+    """No silent fallback: a missing .so raises at load time."""
+    from mppi_robotarm_amd import _native as N
+    monkeypatch.setattr(N, "_lib", None)
+    monkeypatch.setattr(N, "LIB_PATH", str(tmp_path / "nope.so"))
+    with pytest.raises(OSError):
+        N.load()

@@ -1,0 +1,133 @@
+"""CPU: the host-side half of the drop-in controller (control.py:67-78, 122-164)
+against the golden fixtures and the reference's semantics — everything that
+runs before / after the device call, without a GPU."""
+import contextlib
+import io
+import math
+
+import numpy as np
+import pytest
+
+import mppi_oracle as O
+from conftest import STEP_FIXTURES, ctor_kwargs, load_step
+from mppi_robotarm_amd.controller import MPPIControllerForPathTracking
+from mppi_robotarm_amd.distributed import shard_geometry
+from mppi_robotarm_amd.engine import exploit_count
+from mppi_robotarm_amd.params import SYS_PARAMS, ArmParams, runpy_config
+
+RUNPY = dict(param_exploration=0.0, param_lambda=100.0, param_alpha=0.98, sigma=np.eye(2) * 20.0,
+             stage_cost_weight=np.array([0.5, 0.5, 5.0, 5.0]),
+             terminal_cost_weight=np.array([5.0, 5.0, 50.0, 50.0]))
+
+
+def test_constructor_state_matches_reference(paths):
+    c = MPPIControllerForPathTracking(ref_path=paths["xydq_circle"], **runpy_config())
+    assert (c.dim_x, c.dim_u, c.T, c.K) == (4, 2, 30, 100)
+    assert c.param_gamma == pytest.approx(100.0 * (1 - 0.98))           # control.py:45
+    assert np.array_equal(c.u_prev, np.array([[10.0, -2.0]] * 30))      # control.py:59
+    assert c.prev_waypoints_idx == 0 and c.l1 == 1 and c.l2 == 1
+    assert c.visualze_sampled_trajs is True and c.visualize_optimal_traj is True
+    assert c.ref_path is paths["xydq_circle"]                           # held by reference
+
+
+def test_sys_params_and_arm():
+    assert SYS_PARAMS() == {"Ts": 0.0025, "m1": 1, "m2": 1, "l1": 1, "l2": 1, "lc1": 0.5, "lc2": 0.5, "g": 9.81}
+    assert ArmParams.from_sys_params() == ArmParams()
+
+
+@pytest.mark.parametrize("name", STEP_FIXTURES)
+def test_nearest_waypoint_update_matches_fixture(name, paths):
+    g = load_step(name)
+    c = MPPIControllerForPathTracking(ref_path=paths[str(g["path"])], verbose=False, **ctor_kwargs(g))
+    c.prev_waypoints_idx = int(g["prev_idx"])
+    idx, rx, ry, rdq1, rdq2 = c._get_nearest_waypoint(g["x0"][0], g["x0"][1], update_prev_idx=True)
+    assert idx == int(g["prev_idx_after"]) == c.prev_waypoints_idx
+    oi, *ref = O.nearest_waypoint(g["x0"][0], g["x0"][1], paths[str(g["path"])], int(g["prev_idx"]), O.ArmParams())
+    assert int(oi) == idx and np.allclose(ref, [rx, ry, rdq1, rdq2], rtol=0, atol=0)
+
+
+def test_progress_prints_like_reference(paths):
+    c = MPPIControllerForPathTracking(ref_path=paths["xydq_circle"], **runpy_config())
+    buf = io.StringIO()
+    with contextlib.redirect_stdout(buf):
+        c._get_nearest_waypoint(1.152198236517471885, -1.266101672070702344, update_prev_idx=True)
+    assert buf.getvalue().splitlines() == ["0     prev_idx = 0", "0     nearest_idx = 0",
+                                          "======================updated======================="]
+
+
+@pytest.mark.parametrize("name", STEP_FIXTURES)
+def test_median_filter_and_update_match_fixture(name, paths):
+    g = load_step(name)
+    c = MPPIControllerForPathTracking(ref_path=paths[str(g["path"])], verbose=False, **ctor_kwargs(g))
+    filt = c._moving_median_filter(g["w_eps_raw"], 10)
+    assert np.array_equal(filt, g["w_eps_filt"])
+    assert np.array_equal(g["u_prev"] + filt, g["u_new"])
+
+
+@pytest.mark.parametrize("name", ["c1_circle_k128_t20", "sigma_k128_t20", "runpy_k100_t30"])
+def test_noise_draw_is_the_reference_stream(name, paths):
+    """_calc_epsilon consumes np.random exactly as control.py:163 does."""
+    g = load_step(name)
+    c = MPPIControllerForPathTracking(ref_path=paths[str(g["path"])], verbose=False, **ctor_kwargs(g))
+    np.random.seed(int(g["seed"]))
+    eps = c._calc_epsilon(c.Sigma, c.K, c.T, c.dim_u)
+    assert np.array_equal(eps.astype(np.float32), g["eps"])
+
+
+def test_error_paths_before_the_device(paths):
+    # end of path (control.py:76-78): IndexError, after the print
+    c = MPPIControllerForPathTracking(ref_path=paths["xydq_circle"], verbose=False, **runpy_config())
+    c.prev_waypoints_idx = paths["xydq_circle"].shape[0] - 1
+    buf = io.StringIO()
+    with contextlib.redirect_stdout(buf), pytest.raises(IndexError):
+        c.calc_control_input(np.array([0.0, 0.0, 0.0, 0.0]))
+    assert "[ERROR] Reached the end of the reference path." in buf.getvalue()
+    # sigma shape (control.py:157-159): ValueError
+    c = MPPIControllerForPathTracking(delta_t=0.006, ref_path=paths["xydq_circle"], horizon_step_T=8,
+                                      number_of_samples_K=4, verbose=False, **{**RUNPY, "sigma": np.eye(3)})
+    with contextlib.redirect_stdout(io.StringIO()), pytest.raises(ValueError):
+        c.calc_control_input(np.array([1.15, -1.27, 0.0, 0.0]))
+    # default sigma is singular (control.py:30, :106): LinAlgError after the noise draw
+    c = MPPIControllerForPathTracking(delta_t=0.006, ref_path=paths["xydq_circle"], horizon_step_T=8,
+                                      number_of_samples_K=4, verbose=False)
+    np.random.seed(0)
+    import warnings
+    with warnings.catch_warnings(), pytest.raises(np.linalg.LinAlgError):
+        warnings.simplefilter("ignore")
+        c.calc_control_input(np.array([1.15, -1.27, 0.0, 0.0]))
+
+
+@pytest.mark.parametrize("expl,K", [(0.0, 100), (0.25, 128), (0.37, 1000), (1.0, 64), (0.999, 7), (-0.5, 10),
+                                    (0.3, 10), (0.1, 10)])
+def test_exploit_count_is_the_reference_split(expl, K):
+    """k < (1 - expl) * K evaluated in fp64 exactly as control.py:98."""
+    assert exploit_count(expl, K) == sum(1 for k in range(K) if k < (1.0 - expl) * K)
+
+
+@pytest.mark.parametrize("K,world", [(65536, 8), (100, 3), (7, 7), (524288, 8), (1000, 6)])
+def test_shard_geometry_partitions_samples(K, world):
+    seen = []
+    for r in range(world):
+        n, off = shard_geometry(K, world, r)
+        seen.extend(range(off, off + n))
+    assert seen == list(range(K))
+    with pytest.raises(ValueError):
+        shard_geometry(2, 3, 0)
+
+
+def test_exploration_split_is_shard_invariant():
+    """The device rule (k_offset + k) < k_exploit reproduces control.py:98 per shard."""
+    K, expl, world = 1000, 0.37, 3
+    kx = exploit_count(expl, K)
+    ref = [k < (1.0 - expl) * K for k in range(K)]
+    got = []
+    for r in range(world):
+        n, off = shard_geometry(K, world, r)
+        got.extend((off + k) < kx for k in range(n))
+    assert got == ref
+
+
+def test_oracle_reproduces_exploration_fixture(paths):
+    g = load_step("expl_k128_t20")
+    K = int(g["K"])
+    assert exploit_count(float(g["param_exploration"]), K) == math.ceil(0.75 * K)
