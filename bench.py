@@ -53,6 +53,7 @@ def parse():
     p.add_argument("--cpu-seconds", type=float, default=10.0, help="CPU baseline budget (0 = skip)")
     p.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "traffic.json"))
     p.add_argument("--no-graph", action="store_true", help="N = 1: launch eagerly instead of replaying a HIP graph")
+    p.add_argument("--backend", default="nccl", help="torch.distributed backend for N > 1 (nccl = RCCL)")
     return p.parse_args()
 
 
@@ -86,10 +87,14 @@ def main():
     rank = int(os.environ.get("RANK", "0"))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    local_rank = local_rank % max(1, torch.cuda.device_count())  # rehearsal: several ranks on one GPU
     torch.cuda.set_device(local_rank)
     if world > 1:
         import torch.distributed as dist
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
+        if args.backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
+        else:
+            dist.init_process_group(args.backend)
     K, T = args.K, args.T
     K_total, k_offset = K * world, K * rank
     eng = RolloutEngine(K, T, 0.006, 100.0, 0.98, np.eye(2) * 20.0, [0.5, 0.5, 5.0, 5.0],
@@ -113,11 +118,16 @@ def main():
     chunk = args.nbuf if use_graph else 1
     steps = (args.steps + chunk - 1) // chunk * chunk
 
-    def step(i):
+    def step(i, ev_pair=None):
+        if ev_pair is not None:
+            ev_pair[0].record(stream)
         if world == 1:
             eng.rollout(noise[i % args.nbuf], fused_update=True)
         else:
             eng.rollout(noise[i % args.nbuf], partial_out=partial)
+        if ev_pair is not None:
+            ev_pair[1].record(stream)
+        if world > 1:
             exchange_partials(partial, gathered)
             eng.merge(gathered, world, fused_update=True)
 
@@ -143,12 +153,12 @@ def main():
     ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(nev)]
     t0 = time.perf_counter()
     for c in range(nev):
-        ev[c][0].record(stream)
         if graph is not None:
+            ev[c][0].record(stream)
             graph.replay()
+            ev[c][1].record(stream)
         else:
-            step(c)
-        ev[c][1].record(stream)
+            step(c, ev[c])   # events bracket the rollout launch only
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()

@@ -38,5 +38,11 @@ def exchange_partials(partial: torch.Tensor, gathered: torch.Tensor, group=None)
     world = dist.get_world_size(group)
     if gathered.numel() != world * partial.numel():
         raise ValueError("gathered must hold world_size partial rows")
+    if partial.is_cuda and dist.get_backend(group) == "gloo":
+        # gloo has no device all-gather: stage the 1 KB rows through the host
+        host = torch.empty(gathered.numel(), dtype=torch.float64)
+        dist.all_gather_into_tensor(host, partial.cpu(), group=group)
+        gathered.copy_(host)
+        return gathered
     dist.all_gather_into_tensor(gathered, partial, group=group)
     return gathered
