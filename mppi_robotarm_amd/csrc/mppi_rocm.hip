@@ -631,10 +631,12 @@ __global__ __launch_bounds__(NT) void rollout_kernel(
     if (!arrive_last<NT>(counters + g, (unsigned)gsz, &s_flag)) return;
     STAMP(3, NOW());
     merge_rows_block<NT>(slab_r, g * kGroup, gsz, c, sm, &gslab_r, g, nullptr, false, nullptr);
+    STAMP(10, NOW());
     // ---- level 2: the last group merges the group rows and finishes the step
     if (!arrive_last<NT>(counters + ngroups, (unsigned)ngroups, &s_flag)) return;
     STAMP(4, NOW());
     merge_rows_block<NT>(gslab_r, 0, ngroups, c, sm, nullptr, 0, partial_out, true, w_eps_out);
+    STAMP(11, NOW());
     STAMP(6, (unsigned long long)sm.nrel);
     if (flags & MPPI_FLAG_FUSED_UPDATE) nominal_update_block<NT>(st, nxt, c, sm, u_cur);
     STAMP(7, NOW());

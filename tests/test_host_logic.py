@@ -131,3 +131,19 @@ def test_oracle_reproduces_exploration_fixture(paths):
     g = load_step("expl_k128_t20")
     K = int(g["K"])
     assert exploit_count(float(g["param_exploration"]), K) == math.ceil(0.75 * K)
+
+
+def test_harness_plant_matches_reference_loop():
+    """utils.py:14-38 plant + run.py:53-59 integration, replayed on the fixture's controls."""
+    from conftest import load_loop
+    from mppi_robotarm_amd.harness import arm_dynamic, forward_kinematics
+    g = load_loop("runpy_k100_t30")
+    q = g["states"][0][:2].copy()
+    dq = g["states"][0][2:].copy()
+    for i in range(int(g["ticks"])):
+        dq += 0.003 * arm_dynamic(q, dq, g["u"][i])
+        q += 0.003 * dq
+        nxt = g["states"][i + 1] if i + 1 < int(g["ticks"]) else g["final_state"]
+        assert np.array_equal(np.concatenate([q, dq]), nxt)
+    x1, y1, x2, y2 = forward_kinematics(np.array([0.3, -0.4]))
+    assert np.allclose([x2, y2], [np.cos(0.3) + np.cos(-0.1), np.sin(0.3) + np.sin(-0.1)])

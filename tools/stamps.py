@@ -42,20 +42,18 @@ for i in range(steps):
     torch.cuda.synchronize()
     d = dbg.view(-1, 16).cpu().numpy().astype(np.int64)
     t0 = d[:, 0].min()
+    us = lambda v: (v - t0) / 100.0
     roll = (d[:, 1] - d[:, 0]) / 100.0   # us (100 MHz)
     epi = (d[:, 2] - d[:, 1]) / 100.0
     last = int(np.argmax(d[:, 7]))
-    merge = (d[last, 4] - d[last, 2]) / 100.0
-    upd = (d[last, 7] - d[last, 4]) / 100.0
-    span = (d[last, 7] - t0) / 100.0
-    start_spread = (d[:, 0].max() - t0) / 100.0
     hw = d[:, 8]
     cu = (d[:, 9] & 0xF) * 1000 + ((hw >> 13) & 7) * 100 + ((hw >> 12) & 1) * 16 + ((hw >> 8) & 0xF)
     _, per_cu = np.unique(cu, return_counts=True)
-    occ = f"CUs {len(per_cu)} blocks/CU {np.bincount(per_cu).tolist()}"
-    print(f"step {i:2d}: {occ} | event {s0.elapsed_time(s1)*1e3:7.1f} us | span {span:6.1f} | starts spread {start_spread:5.1f} | "
-          f"rollout med {np.median(roll):6.1f} max {roll.max():6.1f} | epilogue med {np.median(epi):5.1f} max {epi.max():6.1f} | "
-          f"last-arrive {(d[last,3]-t0)/100:6.1f} merge {merge:6.1f} update {upd:5.1f} | nl med {np.median(d[:,5]):.0f} max {d[:,5].max()} | "
-          f"relevant partials {d[last,6]}")
+    occ = f"blocks/CU {np.bincount(per_cu).tolist()}"
+    print(f"step {i:2d}: {occ} | event {s0.elapsed_time(s1)*1e3:6.1f} | rollout med {np.median(roll):5.1f} max {roll.max():5.1f} "
+          f"| epi med {np.median(epi):4.1f} max {epi.max():4.1f} | last epi end {us(d[:, 2].max()):5.1f} | final wg: "
+          f"grp-arrive {us(d[last, 3]):5.1f} grp-merge {us(d[last, 10]):5.1f} fin-arrive {us(d[last, 4]):5.1f} "
+          f"fin-merge {us(d[last, 11]):5.1f} update {us(d[last, 7]):5.1f} | nl med {np.median(d[:, 5]):.0f} max {d[:, 5].max()} "
+          f"| rows {d[last, 6]}")
 u = eng.nominal()
 print("final nominal u range", u.min(0), u.max(0))
