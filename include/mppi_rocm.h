@@ -73,6 +73,13 @@ const char *mppi_last_error(void);
 int mppi_set_stream(mppi_ctx *ctx, void *stream);
 int mppi_ctx_info(const mppi_ctx *ctx, int *lanes_per_sample, int *blocks, int *threads_per_block);
 
+/* In-launch hand-off of the workgroup partial rows chosen at creation: *poll = 1
+ * for tagged-granule polling (grid co-resident, at most one workgroup per CU),
+ * 0 for arrival counters (larger grids, or MPPI_HANDOFF=counter in the
+ * environment).  No reference equivalent (the reference reduces in NumPy,
+ * control.py:112-118). */
+int mppi_ctx_handoff(const mppi_ctx *ctx, int *poll);
+
 /* Per control step inputs (control.py:70-75): observed state x0[4], the search
  * window ref_path[prev:prev+W, 0:4] (W = min(30, N - prev), row-major W x 4),
  * and the nominal control sequence u[T][2] (self.u_prev).  Async H2D on the
@@ -119,10 +126,13 @@ int mppi_rollout_traj(mppi_ctx *ctx, const double *base_u, const float *noise_de
 int mppi_noise_philox(mppi_ctx *ctx, unsigned long long seed, unsigned long long step,
                       float *out_dev);
 
+/* Wait for the context stream.  MPPI_E_HIP if a bounded in-launch spin of the
+ * granule hand-off gave up since the last check (that launch's results are
+ * invalid; it cannot happen while the grid is co-resident). */
 int mppi_sync(mppi_ctx *ctx);
 
 /* Diagnostics: in a -DMPPI_STAMPS build the rollout kernel writes a per-workgroup
- * timeline (8 uint64 per workgroup) to dbg_dev; product builds ignore it. */
+ * timeline (16 uint64 per workgroup) to dbg_dev; product builds ignore it. */
 int mppi_debug_set_buffer(mppi_ctx *ctx, void *dbg_dev);
 
 #ifdef __cplusplus

@@ -22,7 +22,7 @@ MPPI_FLAG_FUSED_UPDATE = 1
 
 # every symbol the header declares (tests check the library exports all of them)
 EXPORTS = (
-    "mppi_ctx_create", "mppi_ctx_destroy", "mppi_last_error", "mppi_set_stream", "mppi_ctx_info",
+    "mppi_ctx_create", "mppi_ctx_destroy", "mppi_last_error", "mppi_set_stream", "mppi_ctx_info", "mppi_ctx_handoff",
     "mppi_set_step_inputs", "mppi_rollout", "mppi_merge_partials", "mppi_get_weighted_noise",
     "mppi_get_nominal", "mppi_rollout_traj", "mppi_noise_philox", "mppi_sync", "mppi_debug_set_buffer",
 )
@@ -64,6 +64,7 @@ def load():
         "mppi_last_error": ([], C.c_char_p),
         "mppi_set_stream": ([vp, vp], C.c_int),
         "mppi_ctx_info": ([vp, ip, ip, ip], C.c_int),
+        "mppi_ctx_handoff": ([vp, ip], C.c_int),
         "mppi_set_step_inputs": ([vp, dp, dp, C.c_int, dp], C.c_int),
         "mppi_rollout": ([vp, fp, vp, vp, C.c_uint], C.c_int),
         "mppi_merge_partials": ([vp, vp, C.c_int, C.c_uint], C.c_int),

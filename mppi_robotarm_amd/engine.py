@@ -63,6 +63,10 @@ class RolloutEngine:
         lps, blocks, threads = C.c_int(), C.c_int(), C.c_int()
         N.check(self._lib.mppi_ctx_info(ctx, C.byref(lps), C.byref(blocks), C.byref(threads)), "mppi_ctx_info")
         self.lanes_per_sample, self.blocks, self.threads = lps.value, blocks.value, threads.value
+        poll = C.c_int()
+        N.check(self._lib.mppi_ctx_handoff(ctx, C.byref(poll)), "mppi_ctx_handoff")
+        # in-launch hand-off of the workgroup partials: "poll" (tagged granules) or "counter"
+        self.handoff = "poll" if poll.value else "counter"
         self.partial_len = 2 + 2 * self.T
         self._weps = np.zeros((self.T, 2))
 
