@@ -52,7 +52,8 @@ def parse():
     p.add_argument("--lps", type=int, default=0, help="lanes per sample (0 = auto)")
     p.add_argument("--cpu-seconds", type=float, default=10.0, help="CPU baseline budget (0 = skip)")
     p.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "traffic.json"))
-    p.add_argument("--no-graph", action="store_true", help="N = 1: launch eagerly instead of replaying a HIP graph")
+    p.add_argument("--launch", choices=("eager", "graph"), default="eager",
+                   help="N = 1: back-to-back launches from the host loop (default) or replay of a captured HIP graph")
     p.add_argument("--backend", default="nccl", help="torch.distributed backend for N > 1 (nccl = RCCL)")
     return p.parse_args()
 
@@ -110,11 +111,14 @@ def main():
     gathered = torch.empty(world * eng.partial_len, dtype=torch.float64, device=eng.device)
     stream = torch.cuda.current_stream()
 
-    # N = 1: the device-resident loop has no host synchronisation, so a chunk of
-    # steps (one per noise buffer, an even count so the ping-pong parameter
-    # block returns to the same parity) is captured once into a HIP graph and
-    # replayed; launch overhead is then one graph launch per chunk.
-    use_graph = world == 1 and not args.no_graph and args.nbuf % 2 == 0
+    # N = 1: the device-resident loop has no host synchronisation.  Default:
+    # the host loop launches step after step (a launch costs less host time than
+    # a step takes on the GPU, so the queue never drains; measured 31 us/step
+    # against 36 with graph replay, whose per-node cost is higher on ROCm 7.2).
+    # --launch graph captures a chunk of steps (one per noise buffer, an even
+    # count so the ping-pong parameter block returns to the same parity) once
+    # and replays it.
+    use_graph = world == 1 and args.launch == "graph" and args.nbuf % 2 == 0
     chunk = args.nbuf if use_graph else 1
     steps = (args.steps + chunk - 1) // chunk * chunk
 
@@ -151,22 +155,31 @@ def main():
     torch.cuda.synchronize()
     nev = steps // chunk
     ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(nev)]
+    whole = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
     t0 = time.perf_counter()
-    for c in range(nev):
-        if graph is not None:
-            ev[c][0].record(stream)
-            graph.replay()
-            ev[c][1].record(stream)
-        else:
-            step(c, ev[c])   # events bracket the rollout launch only
+    if world == 1:
+        # one event pair around the whole timed region on the launch stream
+        whole[0].record(stream)
+        for c in range(nev):
+            if graph is not None:
+                graph.replay()
+            else:
+                step(c)
+        whole[1].record(stream)
+    else:
+        for c in range(nev):
+            step(c, ev[c])   # events bracket the rollout launch only (the exchange is timed by the wall clock)
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
     elapsed = time.perf_counter() - t0
-    # average duration per launch of the step (events on the launch stream);
-    # with a graph this includes the ~1.5 us dependent-kernel boundaries
-    kern_ms = sum(a.elapsed_time(b) for a, b in ev) / steps
+    # average duration per launch of the rollout kernel (events on the launch
+    # stream); at N = 1 the back-to-back launches' average, boundaries included
+    if world == 1:
+        kern_ms = whole[0].elapsed_time(whole[1]) / steps
+    else:
+        kern_ms = sum(a.elapsed_time(b) for a, b in ev) / steps
     if world > 1:
         tt = torch.tensor([elapsed, kern_ms], dtype=torch.float64, device=eng.device)
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
@@ -208,7 +221,8 @@ def main():
                                    f"xydq_circle.txt window, Philox N(0,20I) noise x{args.nbuf} buffers",
                        "K_total": K_total, "K_per_gpu": K, "T": T, "lanes_per_sample": eng.lanes_per_sample,
                        "parallelism": f"samples sharded x{world}, RCCL all_gather of partials" if world > 1
-                       else "single device, fused update" + (f", HIP graph of {chunk} steps" if use_graph else "")},
+                       else "single device, fused update" + (f", HIP graph of {chunk} steps" if use_graph
+                                                               else ", back-to-back launches")},
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": achieved / HBM_PEAK_GBS, "traffic": traffic},
         }

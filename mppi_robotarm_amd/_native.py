@@ -49,14 +49,12 @@ class MPPIError(RuntimeError):
 _lib = None
 
 
-def load():
-    """Load libmppi_rocm.so (raises OSError if it is missing — no fallback)."""
-    global _lib
-    if _lib is not None:
-        return _lib
-    if not os.path.exists(LIB_PATH):
-        raise OSError(f"{LIB_PATH} is missing: build it with `python -c 'import __graft_entry__ as g; g.build()'`")
-    L = C.CDLL(LIB_PATH)
+def open_library(path: str):
+    """dlopen one build of the C ABI with every entry point's signature set
+    (``load`` uses it for the product library; tools open variants with it)."""
+    if not os.path.exists(path):
+        raise OSError(f"{path} is missing: build it with `python -c 'import __graft_entry__ as g; g.build()'`")
+    L = C.CDLL(path)
     vp, dp, fp, ip = C.c_void_p, C.POINTER(C.c_double), C.c_void_p, C.POINTER(C.c_int)
     sig = {
         "mppi_ctx_create": ([C.POINTER(ConfigC), C.c_int, vp, C.POINTER(vp)], C.c_int),
@@ -79,8 +77,15 @@ def load():
         fn = getattr(L, name)
         fn.argtypes = args
         fn.restype = res
-    _lib = L
     return L
+
+
+def load():
+    """Load libmppi_rocm.so (raises OSError if it is missing — no fallback)."""
+    global _lib
+    if _lib is None:
+        _lib = open_library(LIB_PATH)
+    return _lib
 
 
 def check(rc: int, what: str) -> None:

@@ -1,5 +1,5 @@
 #!/bin/bash
-# PMC counter passes + stochastic PC sampling of the rollout kernel for one
+# PMC counter passes (one counter set per pass) of the rollout kernel for one
 # library variant.  Usage: tools/pmc.sh VARIANT   (libmppi_rocm_VARIANT.so; "" = product)
 set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
@@ -14,4 +14,3 @@ run p1 --pmc SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_A
 run p2 --pmc GRBM_GUI_ACTIVE SQ_INSTS_SALU SQ_INSTS_SMEM SQ_INSTS_LDS SQ_ACTIVE_INST_SCA SQ_ACTIVE_INST_LDS SQ_WAVES SQ_INSTS_VMEM_RD
 run p3 --pmc FETCH_SIZE
 run p4 --pmc WRITE_SIZE
-run pcs --pc-sampling-beta-enabled --pc-sampling-method stochastic --pc-sampling-unit cycles --pc-sampling-interval 65536

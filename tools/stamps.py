@@ -42,7 +42,7 @@ for i in range(steps):
     torch.cuda.synchronize()
     d = dbg.view(-1, 16).cpu().numpy().astype(np.int64)
     t0 = d[:, 0].min()
-    us = lambda v: (v - t0) / 100.0
+    us = lambda v: (v - t0) / 100.0 if v else float("nan")   # slot never written (direct merge: no group level)
     roll = (d[:, 1] - d[:, 0]) / 100.0   # us (100 MHz)
     epi = (d[:, 2] - d[:, 1]) / 100.0
     last = int(np.argmax(d[:, 7]))

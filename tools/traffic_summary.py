@@ -1,0 +1,97 @@
+"""Summarise one tools/profile_round.sh run into the committed profile files.
+
+    python tools/traffic_summary.py gpurun_out/prof_TAG profiles/TAG [K T]
+
+Reads the kernel-trace stats and the PMC passes (each counter in its own
+rocprofv3 run, as the MI355X guide prescribes), applies the measured gfx950
+calibration (tools/calib_fetch.hip: the same 8 B/lane [T][K][2] row pattern
+with a known byte count; FETCH_SIZE reports that pattern at ~0.5x its true
+bytes, WRITE_SIZE at 1.0x) and writes:
+
+  profiles/TAG/kernel_stats.csv      rocprofv3 --kernel-trace --stats summary
+  profiles/TAG/pmc_*.csv             the counter CSVs (one per pass)
+  profiles/TAG/sq_counters.json      SQ issue / wait summary
+  profiles/traffic.json              HBM bytes per rollout launch (read by bench.py)
+"""
+import csv
+import json
+import os
+import re
+import shutil
+import sys
+
+import numpy as np
+
+
+def counters(path, name_filter):
+    vals = {}
+    with open(path) as f:
+        for row in csv.DictReader(f):
+            if name_filter not in row["Kernel_Name"]:
+                continue
+            vals.setdefault(row["Counter_Name"], []).append(float(row["Counter_Value"]))
+    return vals
+
+
+def main():
+    src, dst = sys.argv[1], sys.argv[2]
+    K = int(sys.argv[3]) if len(sys.argv) > 3 else 65536
+    T = int(sys.argv[4]) if len(sys.argv) > 4 else 64
+    os.makedirs(dst, exist_ok=True)
+    shutil.copy(os.path.join(src, "stats", "run_kernel_stats.csv"), os.path.join(dst, "kernel_stats.csv"))
+    for p in ("fetch", "write", "cfetch", "cwrite", "sq", "grbm"):
+        f = os.path.join(src, p, "p_counter_collection.csv")
+        if os.path.exists(f):
+            shutil.copy(f, os.path.join(dst, f"pmc_{p}.csv"))
+    avg_ns = None
+    with open(os.path.join(src, "stats", "run_kernel_stats.csv")) as f:
+        for row in csv.DictReader(f):
+            if "rollout_kernel" in row["Name"]:
+                avg_ns = float(row["AverageNs"])
+                m = re.search(r"rollout_kernel<[^>]*>", row["Name"])
+                kname = m.group(0) if m else row["Name"][:60]
+    fetch = np.median(counters(os.path.join(src, "fetch", "p_counter_collection.csv"), "rollout")["FETCH_SIZE"])
+    write = np.median(counters(os.path.join(src, "write", "p_counter_collection.csv"), "rollout")["WRITE_SIZE"])
+    cf = counters(os.path.join(src, "cfetch", "p_counter_collection.csv"), "calib")["FETCH_SIZE"]
+    cw = counters(os.path.join(src, "cwrite", "p_counter_collection.csv"), "calib")["WRITE_SIZE"]
+    known_read, known_write = 33554432, 262144     # tools/calib_fetch.hip
+    f_ratio = np.median(cf) * 1024 / known_read
+    w_ratio = np.median(cw) * 1024 / known_write
+    read_b = fetch * 1024 / f_ratio
+    write_b = write * 1024 / w_ratio
+    alg = 8 * K * T
+    out = {
+        "K": K, "T": T, "kernel": kname + " (fused update)",
+        "hbm_bytes_per_launch": int(round(read_b + write_b)),
+        "read_bytes_per_launch": int(round(read_b)),
+        "write_bytes_per_launch": int(round(write_b)),
+        "algorithmic_bytes_per_launch": alg,
+        "traffic_over_algorithmic": (read_b + write_b) / alg,
+        "FETCH_SIZE_KB_median": fetch, "WRITE_SIZE_KB_median": write,
+        "calibration": {"kernel": "tools/calib_fetch.hip (same 8 B/lane [T][K][2] row pattern)",
+                        "known_read_bytes": known_read, "FETCH_SIZE_KB": float(np.median(cf)),
+                        "fetch_reported_over_true": f_ratio, "known_write_bytes": known_write,
+                        "WRITE_SIZE_KB": float(np.median(cw)), "write_reported_over_true": w_ratio},
+        "rocprof_avg_kernel_ns": avg_ns,
+        "source": f"rocprofv3 --pmc FETCH_SIZE / --pmc WRITE_SIZE (separate passes), bench.py; {os.path.basename(dst)}",
+    }
+    json.dump(out, open(os.path.join(os.path.dirname(dst.rstrip('/')), "traffic.json"), "w"), indent=1)
+    sqf = os.path.join(src, "sq", "p_counter_collection.csv")
+    if os.path.exists(sqf):
+        sq = {k: float(np.median(v)) for k, v in counters(sqf, "rollout").items()}
+        gr = {}
+        grf = os.path.join(src, "grbm", "p_counter_collection.csv")
+        if os.path.exists(grf):
+            gr = {k: float(np.median(v)) for k, v in counters(grf, "rollout").items()}
+        summ = {"SQ": sq, "GRBM": gr}
+        if "SQ_WAVE_CYCLES" in sq:
+            summ["wait_any_frac"] = sq.get("SQ_WAIT_ANY", 0) / sq["SQ_WAVE_CYCLES"]
+            summ["active_inst_frac"] = sq.get("SQ_ACTIVE_INST_ANY", 0) / sq["SQ_WAVE_CYCLES"]
+        if "SQ_WAVES" in sq and "SQ_INSTS_VALU" in sq:
+            summ["valu_insts_per_wave"] = sq["SQ_INSTS_VALU"] / sq["SQ_WAVES"]
+        json.dump(summ, open(os.path.join(dst, "sq_counters.json"), "w"), indent=1)
+    print(json.dumps({k: out[k] for k in ("hbm_bytes_per_launch", "traffic_over_algorithmic", "rocprof_avg_kernel_ns")}))
+
+
+if __name__ == "__main__":
+    main()
