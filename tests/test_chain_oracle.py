@@ -1,0 +1,86 @@
+"""CPU: the n-link chain oracle (BASELINE config 5).
+
+The 7-DoF model is build-defined (the reference has none), so its parity is
+unpinned by the reference at n = 7.  These tests pin what can be pinned:
+at n = 2 with the reference constants and inertia := length
+(control.py:241-245) the chain IS the reference model — dynamics, the whole
+K x T cost, and the full controller update — checked against the 2-DoF oracle
+and the reference's own golden steps; and the two chain restatements (NumPy,
+C) agree at n = 7.
+"""
+import numpy as np
+import pytest
+
+import chain_oracle as CO
+import coracle
+import mppi_oracle as O
+from conftest import STEP_FIXTURES, load_step
+
+P7 = CO.ChainParams()
+P2 = CO.ChainParams.from_arm2()
+
+
+def test_chain_dynamics_reduce_to_reference_F_at_n2():
+    rng = np.random.default_rng(0)
+    q, dq, v = rng.normal(0, 1, (500, 2)), rng.normal(0, 2, (500, 2)), rng.normal(0, 20, (500, 2))
+    ref = np.stack(O.forward_dynamics(q[:, 0], q[:, 1], dq[:, 0], dq[:, 1], v[:, 0], v[:, 1], 0.006, O.ArmParams()), 1)
+    qn, dqn = CO.chain_forward_dynamics(q, dq, v, 0.006, P2)
+    np.testing.assert_allclose(np.concatenate([qn, dqn], 1), ref, rtol=1e-12, atol=1e-14)
+
+
+@pytest.mark.parametrize("name", STEP_FIXTURES)
+def test_chain_step_at_n2_matches_reference_golden(name, paths):
+    """S and the updated control of the reference's golden steps, through the chain model."""
+    g = load_step(name)
+    ref_path = paths[str(g["path"])]
+    c = CO.ChainOracleController(float(g["delta_t"]), ref_path, int(g["T"]), int(g["K"]),
+                                 float(g["param_exploration"]), float(g["param_lambda"]), float(g["param_alpha"]),
+                                 g["sigma"], g["stage_cost_weight"], g["terminal_cost_weight"], chain=P2,
+                                 visualize_optimal_traj=False)
+    c.u_prev = g["u_prev"].copy()
+    c.prev_waypoints_idx = int(g["prev_idx"])
+    _, u_seq, _, _ = c.calc_control_input(g["x0"], epsilon=g["eps"].astype(np.float64))
+    S = c.last["S"]
+    assert int(np.argmin(S)) == int(np.argmin(g["S"]))
+    assert float(np.max(np.abs(S - g["S"]) / np.abs(g["S"]))) < 1e-13
+    assert float(np.max(np.abs(u_seq - g["u_seq"]))) < 1e-10 * max(1.0, float(np.max(np.abs(g["u_seq"]))))
+    assert c.prev_waypoints_idx == int(g["prev_idx_after"])
+
+
+def _c5_inputs(K, T, seed=3):
+    rng = np.random.default_rng(seed)
+    x0 = np.concatenate([[1.481492] + [-0.320757] * 6, [0.0] * 7])
+    u = np.tile(CO.gravity_torque(x0[:7], P7), (T, 1)) + rng.normal(0, 0.5, (T, 7))
+    sig = np.diag([20.0, 16.0, 12.0, 8.0, 4.0, 2.0, 1.0])
+    eps = (rng.normal(0, 1, (K, T, 7)) * np.sqrt(np.diag(sig))).astype(np.float32)
+    return x0, u, sig, eps
+
+
+def test_c_chain_oracle_matches_numpy_at_n7(paths):
+    K, T = 96, 24
+    x0, u, sig, eps = _c5_inputs(K, T)
+    win = paths["xydq_circle"][:30]
+    S = CO.chain_rollout_costs(x0, u, eps.astype(np.float64), paths["xydq_circle"], 0, 0.006, 100.0, 0.98, sig,
+                               [0.5, 0.5, 5, 5], [5, 5, 50, 50], 0.25, P7)
+    Sc = coracle.chain_rollout_costs(x0, u, eps, win, 0.006, 100.0, 0.98, sig, [0.5, 0.5, 5, 5], [5, 5, 50, 50], P7,
+                                     k_exploit=int(np.ceil(0.75 * K)))
+    np.testing.assert_allclose(Sc, S, rtol=1e-11)
+    Sd = coracle.chain_rollout_costs(x0, u, np.ascontiguousarray(eps.transpose(1, 2, 0)), win, 0.006, 100.0, 0.98,
+                                     sig, [0.5, 0.5, 5, 5], [5, 5, 50, 50], P7, k_exploit=int(np.ceil(0.75 * K)),
+                                     layout="TNK")
+    assert np.array_equal(Sc, Sd)                      # device [T][n][K] layout reads the same values
+    w, we = coracle.chain_weighted_noise(Sc, eps, 1.0e7)
+    np.testing.assert_allclose(we, O.weighted_noise(O.compute_weights(Sc, 1.0e7), eps), rtol=1e-12, atol=1e-15)
+    traj = coracle.chain_traj(x0, np.repeat(u[None], 3, 0), 0.006, P7)
+    np.testing.assert_allclose(traj[0], CO.chain_rollout_trajectory(x0, u, 0.006, P7), rtol=1e-12, atol=1e-12)
+
+
+def test_gravity_torque_holds_the_chain():
+    q = np.array([1.481492] + [-0.320757] * 6)
+    qn, dqn = CO.chain_forward_dynamics(q[None], np.zeros((1, 7)), CO.gravity_torque(q, P7)[None], 0.006, P7)
+    assert np.max(np.abs(dqn)) < 1e-12 and np.max(np.abs(qn - q)) < 1e-14
+
+
+def test_c5_start_pose_is_on_the_path(paths):
+    x, y = CO.chain_fk(np.array([1.481492] + [-0.320757] * 6), P7)
+    assert np.hypot(x - paths["xydq_circle"][0, 0], y - paths["xydq_circle"][0, 1]) < 1e-5
