@@ -135,6 +135,63 @@ int mppi_sync(mppi_ctx *ctx);
  * timeline (16 uint64 per workgroup) to dbg_dev; product builds ignore it. */
 int mppi_debug_set_buffer(mppi_ctx *ctx, void *dbg_dev);
 
+/* ------------------------------------------------------------------------
+ * n-link planar chain (BASELINE config 5: "7-DoF arm dynamics (extended
+ * sys_params.py), K=131072 T=128, xydq_circle.txt reference").  The reference
+ * has no such model; it is BUILD-DEFINED (oracle/chain_oracle.py: mass matrix
+ * D_ab = mu_ab cos(th_a - th_b) + delta_ab I_a in absolute angles, Coriolis,
+ * gravity, Cholesky solve, semi-implicit Euler as control.py:256-259) and
+ * reduces to the reference _F (control.py:234-263) at n = 2 with I = l.  The
+ * cost is control.py:174-232 on (end-effector x, y, dq_1, dq_2).  Same
+ * conventions as above; noise is [T][n][K_local] fp32, u and w_eps are T x n
+ * row-major, x0 = [q(n), dq(n)].
+ * ------------------------------------------------------------------------ */
+#define MPPI_CHAIN_MAX_DOF 8   /* array capacity; n in [2, 7] is supported */
+
+typedef struct {
+    int n;                                  /* links, 2..7                                */
+    double m[MPPI_CHAIN_MAX_DOF];           /* masses                                     */
+    double l[MPPI_CHAIN_MAX_DOF];           /* lengths (dynamics)                         */
+    double lc[MPPI_CHAIN_MAX_DOF];          /* joint-to-centre-of-mass distances          */
+    double I[MPPI_CHAIN_MAX_DOF];           /* inertias about the centre of mass          */
+    double fk[MPPI_CHAIN_MAX_DOF];          /* lengths used by the cost's kinematics      */
+    double g;
+} mppi_chain_params;
+
+typedef struct {
+    int K_local, T, K_total, k_offset;      /* as mppi_config                             */
+    double delta_t, param_lambda, param_alpha, param_exploration;
+    double sigma[MPPI_CHAIN_MAX_DOF * MPPI_CHAIN_MAX_DOF]; /* n x n row-major, SPD        */
+    double stage_cost_weight[4];            /* on (x, y, dq_1, dq_2), control.py:185      */
+    double terminal_cost_weight[4];         /* control.py:198                             */
+    mppi_chain_params chain;
+} mppi_chain_config;
+
+typedef struct mppi_chain_ctx mppi_chain_ctx;
+
+/* control.py:21-65 with the chain model; MPPI_E_SINGULAR if Sigma is not SPD. */
+int mppi_chain_ctx_create(const mppi_chain_config *cfg, int device, void *stream, mppi_chain_ctx **out);
+void mppi_chain_ctx_destroy(mppi_chain_ctx *ctx);
+int mppi_chain_set_stream(mppi_chain_ctx *ctx, void *stream);
+int mppi_chain_ctx_info(const mppi_chain_ctx *ctx, int *blocks, int *threads_per_block, int *poll);
+/* inputs of control.py:70-75: x0[2n], the window (W x 4), u[T*n] (NULL: keep the device nominal) */
+int mppi_chain_set_step_inputs(mppi_chain_ctx *ctx, const double *x0, const double *window, int W,
+                               const double *u);
+/* control.py:81-118 (+ :122-149 with MPPI_FLAG_FUSED_UPDATE) for the chain */
+int mppi_chain_rollout(mppi_chain_ctx *ctx, const float *noise_dev, double *S_dev, double *partial_dev,
+                       unsigned flags);
+int mppi_chain_merge_partials(mppi_chain_ctx *ctx, const double *partials_dev, int n, unsigned flags);
+int mppi_chain_get_weighted_noise(mppi_chain_ctx *ctx, double *w_eps_host);
+int mppi_chain_get_nominal(mppi_chain_ctx *ctx, double *u_host);
+/* control.py:129-145 analogue: out_dev[K][T][2n] fp32 (q, dq) */
+int mppi_chain_rollout_traj(mppi_chain_ctx *ctx, const double *base_u, const float *noise_dev, int K,
+                            float *out_dev);
+/* N(0, Sigma) noise [T][n][K_local] from Philox4x32-10 (global sample index: shard-invariant) */
+int mppi_chain_noise_philox(mppi_chain_ctx *ctx, unsigned long long seed, unsigned long long step,
+                            float *out_dev);
+int mppi_chain_sync(mppi_chain_ctx *ctx);
+int mppi_chain_debug_set_buffer(mppi_chain_ctx *ctx, void *dbg_dev);
+
 #ifdef __cplusplus
 }
 #endif

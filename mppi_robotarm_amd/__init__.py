@@ -7,7 +7,8 @@ HIP kernel for gfx950 behind the C ABI in ``include/mppi_rocm.h``.
 """
 from .params import ArmParams, SYS_PARAMS, runpy_config  # noqa: F401
 
-__all__ = ["ArmParams", "SYS_PARAMS", "runpy_config", "MPPIControllerForPathTracking", "RolloutEngine"]
+__all__ = ["ArmParams", "SYS_PARAMS", "runpy_config", "MPPIControllerForPathTracking", "RolloutEngine",
+           "ChainMPPIController", "ChainEngine", "ChainParams"]
 
 
 def __getattr__(name):  # lazy: importing the package does not touch the GPU library
@@ -17,4 +18,7 @@ def __getattr__(name):  # lazy: importing the package does not touch the GPU lib
     if name == "RolloutEngine":
         from .engine import RolloutEngine
         return RolloutEngine
+    if name in ("ChainMPPIController", "ChainEngine", "ChainParams"):
+        from . import chain
+        return getattr(chain, name)
     raise AttributeError(name)

@@ -25,6 +25,10 @@ EXPORTS = (
     "mppi_ctx_create", "mppi_ctx_destroy", "mppi_last_error", "mppi_set_stream", "mppi_ctx_info", "mppi_ctx_handoff",
     "mppi_set_step_inputs", "mppi_rollout", "mppi_merge_partials", "mppi_get_weighted_noise",
     "mppi_get_nominal", "mppi_rollout_traj", "mppi_noise_philox", "mppi_sync", "mppi_debug_set_buffer",
+    "mppi_chain_ctx_create", "mppi_chain_ctx_destroy", "mppi_chain_set_stream", "mppi_chain_ctx_info",
+    "mppi_chain_set_step_inputs", "mppi_chain_rollout", "mppi_chain_merge_partials",
+    "mppi_chain_get_weighted_noise", "mppi_chain_get_nominal", "mppi_chain_rollout_traj",
+    "mppi_chain_noise_philox", "mppi_chain_sync", "mppi_chain_debug_set_buffer",
 )
 
 
@@ -39,6 +43,24 @@ class ConfigC(C.Structure):
         ("param_exploration", C.c_double), ("sigma", C.c_double * 4),
         ("stage_cost_weight", C.c_double * 4), ("terminal_cost_weight", C.c_double * 4),
         ("arm", ArmParamsC), ("lanes_per_sample", C.c_int),
+    ]
+
+
+CHAIN_MAX_DOF = 8
+
+
+class ChainParamsC(C.Structure):
+    _fields_ = [("n", C.c_int)] + [(f, C.c_double * CHAIN_MAX_DOF) for f in ("m", "l", "lc", "I", "fk")] + \
+               [("g", C.c_double)]
+
+
+class ChainConfigC(C.Structure):
+    _fields_ = [
+        ("K_local", C.c_int), ("T", C.c_int), ("K_total", C.c_int), ("k_offset", C.c_int),
+        ("delta_t", C.c_double), ("param_lambda", C.c_double), ("param_alpha", C.c_double),
+        ("param_exploration", C.c_double), ("sigma", C.c_double * (CHAIN_MAX_DOF * CHAIN_MAX_DOF)),
+        ("stage_cost_weight", C.c_double * 4), ("terminal_cost_weight", C.c_double * 4),
+        ("chain", ChainParamsC),
     ]
 
 
@@ -72,6 +94,19 @@ def open_library(path: str):
         "mppi_noise_philox": ([vp, C.c_ulonglong, C.c_ulonglong, fp], C.c_int),
         "mppi_sync": ([vp], C.c_int),
         "mppi_debug_set_buffer": ([vp, vp], C.c_int),
+        "mppi_chain_ctx_create": ([C.POINTER(ChainConfigC), C.c_int, vp, C.POINTER(vp)], C.c_int),
+        "mppi_chain_ctx_destroy": ([vp], None),
+        "mppi_chain_set_stream": ([vp, vp], C.c_int),
+        "mppi_chain_ctx_info": ([vp, ip, ip, ip], C.c_int),
+        "mppi_chain_set_step_inputs": ([vp, dp, dp, C.c_int, dp], C.c_int),
+        "mppi_chain_rollout": ([vp, fp, vp, vp, C.c_uint], C.c_int),
+        "mppi_chain_merge_partials": ([vp, vp, C.c_int, C.c_uint], C.c_int),
+        "mppi_chain_get_weighted_noise": ([vp, dp], C.c_int),
+        "mppi_chain_get_nominal": ([vp, dp], C.c_int),
+        "mppi_chain_rollout_traj": ([vp, dp, fp, C.c_int, fp], C.c_int),
+        "mppi_chain_noise_philox": ([vp, C.c_ulonglong, C.c_ulonglong, fp], C.c_int),
+        "mppi_chain_sync": ([vp], C.c_int),
+        "mppi_chain_debug_set_buffer": ([vp, vp], C.c_int),
     }
     for name, (args, res) in sig.items():
         fn = getattr(L, name)

@@ -1,12 +1,19 @@
-"""In-tree build of the HIP library for gfx950 (``hipcc`` cross-compiles without a GPU)."""
+"""In-tree build of the HIP library for gfx950 (``hipcc`` cross-compiles without a GPU).
+
+Two translation units — ``csrc/mppi_rocm.hip`` (the reference's 2-link arm)
+and ``csrc/mppi_chain.hip`` (the n-link chain of config 5) — are compiled in
+parallel and linked into ``_lib/libmppi_rocm.so``.
+"""
 from __future__ import annotations
 
+import glob
 import os
 import subprocess
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 ROOT = os.path.dirname(HERE)
-SRC = os.path.join(HERE, "csrc", "mppi_rocm.hip")
+CSRC = os.path.join(HERE, "csrc")
+SRCS = [os.path.join(CSRC, "mppi_rocm.hip"), os.path.join(CSRC, "mppi_chain.hip")]
 OUT = os.path.join(HERE, "_lib", "libmppi_rocm.so")
 ARCH = os.environ.get("MPPI_OFFLOAD_ARCH", "gfx950")
 
@@ -19,15 +26,24 @@ def hipcc() -> str:
 
 
 def build_native(force: bool = False, extra_flags: list[str] | None = None, out: str = OUT) -> str:
-    """Compile csrc/mppi_rocm.hip -> _lib/libmppi_rocm.so (skipped when up to date)."""
-    deps = [SRC, os.path.join(ROOT, "include", "mppi_rocm.h")]
+    """Compile csrc/*.hip -> _lib/libmppi_rocm.so (skipped when up to date)."""
+    deps = SRCS + glob.glob(os.path.join(CSRC, "*.h")) + [os.path.join(ROOT, "include", "mppi_rocm.h")]
     if not force and os.path.exists(out) and not extra_flags and \
             all(os.path.getmtime(out) >= os.path.getmtime(d) for d in deps):
         return out
     os.makedirs(os.path.dirname(out), exist_ok=True)
-    cmd = [hipcc(), f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-shared",
-           "-I", os.path.join(ROOT, "include"), "-o", out, SRC] + list(extra_flags or [])
-    subprocess.run(cmd, check=True)
+    flags = [f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-I", os.path.join(ROOT, "include")]
+    flags += list(extra_flags or [])
+    objs, procs = [], []
+    for src in SRCS:
+        obj = out + "." + os.path.splitext(os.path.basename(src))[0] + ".o"
+        objs.append(obj)
+        procs.append(subprocess.Popen([hipcc()] + flags + ["-c", "-o", obj, src]))
+    if any(p.wait() != 0 for p in procs):
+        raise subprocess.CalledProcessError(1, "hipcc")
+    subprocess.run([hipcc(), f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", out] + objs, check=True)
+    for obj in objs:
+        os.remove(obj)
     return out
 
 

@@ -1,0 +1,378 @@
+"""n-link planar chain MPPI (BASELINE config 5: 7-DoF, K=131072 T=128).
+
+The reference has no 7-DoF model; this model is build-defined (equations in
+``oracle/chain_oracle.py`` and ``include/mppi_rocm.h``) and reduces to the
+reference ``_F`` (control.py:234-263) at n = 2 with inertia := link length.
+``ChainMPPIController`` keeps the reference controller's interface
+(control.py:21-152) with ``dim_u = n``, ``dim_x = 2n``:
+``calc_control_input(observed_x)`` -> (u0, u_seq, optimal_traj (T, 2n),
+sampled_traj_list (K, T, 2n)); the cost is control.py:174-232 on the end
+effector (x, y) and the first two joint rates (xydq_circle.txt's columns).
+
+Device work runs in ``csrc/mppi_chain.hip`` through ``mppi_chain_*``; the host
+keeps the O(T n) work in fp64 (nearest-waypoint update, noise draw, median
+filter, update, shift), as ``controller.py`` does for the 2-link arm.
+"""
+from __future__ import annotations
+
+import ctypes as C
+from dataclasses import dataclass, field
+
+import numpy as np
+import torch
+from scipy.ndimage import median_filter
+
+from . import _native as N
+from .distributed import exchange_partials, shard_geometry
+
+SEARCH_IDX_LEN = 30  # control.py:203
+
+
+def _tup(v):
+    return field(default_factory=lambda: tuple(v))
+
+
+@dataclass(frozen=True)
+class ChainParams:
+    """Link constants of the chain ("extended sys_params.py").  Defaults: the
+    config-5 arm — 7 uniform slender links of 1 kg, total reach 2 m (the 2-link
+    arm's l1 + l2), centre of mass at mid-link, I = m l^2 / 12."""
+    m: tuple = _tup([1.0] * 7)
+    l: tuple = _tup([2.0 / 7.0] * 7)
+    lc: tuple = _tup([1.0 / 7.0] * 7)
+    I: tuple = _tup([(2.0 / 7.0) ** 2 / 12.0] * 7)
+    fk: tuple = _tup([2.0 / 7.0] * 7)
+    g: float = 9.81
+
+    @property
+    def n(self) -> int:
+        return len(self.m)
+
+    @staticmethod
+    def from_arm2(arm=None) -> "ChainParams":
+        """The reference 2-link model (control.py:11-18, 241-245): inertia := link length."""
+        from .params import ArmParams
+        a = ArmParams() if arm is None else arm
+        return ChainParams(m=(a.m1, a.m2), l=(a.l1, a.l2), lc=(a.lc1, a.lc2), I=(a.l1, a.l2),
+                           fk=(a.fk_l1, a.fk_l2), g=a.g)
+
+
+# Config-5 start pose: the end effector on xydq_circle.txt's first waypoint
+# (least-squares IK with a smooth bend, computed once), at rest.
+CHAIN7_X0 = np.array([1.481492] + [-0.320757] * 6 + [0.0] * 7)
+# Noise covariance scaled with the gravity load each joint carries.
+CHAIN7_SIGMA = np.diag([20.0, 16.0, 12.0, 8.0, 4.0, 2.0, 1.0])
+
+
+def gravity_torque(q, P: ChainParams = ChainParams()) -> np.ndarray:
+    """Joint torques that hold the chain still at q (the nominal's natural start)."""
+    m, l, lc = map(np.asarray, (P.m, P.l, P.lc))
+    tail = np.array([m[k + 1:].sum() for k in range(P.n)])
+    g_th = P.g * (m * lc + l * tail) * np.cos(np.cumsum(q))
+    return np.cumsum(g_th[::-1])[::-1]
+
+
+def chain7_config() -> dict:
+    """Constructor kwargs of the config-5 controller: run.py's constants (run.py:25-37) with the 7-link Sigma."""
+    return dict(delta_t=0.006, horizon_step_T=128, number_of_samples_K=131072, param_exploration=0.0,
+                param_lambda=100.0, param_alpha=0.98, sigma=CHAIN7_SIGMA.copy(),
+                stage_cost_weight=np.array([0.5, 0.5, 5.0, 5.0]),
+                terminal_cost_weight=np.array([5.0, 5.0, 50.0, 50.0]))
+
+
+def _dptr(a: np.ndarray):
+    return a.ctypes.data_as(C.POINTER(C.c_double))
+
+
+class ChainEngine:
+    """Owns one ``mppi_chain_ctx`` (one device, one shard of samples); noise layout [T][n][K_local] fp32."""
+
+    def __init__(self, K_local: int, T: int, delta_t: float, param_lambda: float, param_alpha: float, sigma,
+                 stage_cost_weight, terminal_cost_weight, param_exploration: float = 0.0,
+                 chain: ChainParams = ChainParams(), K_total: int | None = None, k_offset: int = 0,
+                 device: int | torch.device | None = None):
+        self._lib = N.load()
+        if device is None:
+            device = torch.cuda.current_device()
+        self.device = torch.device("cuda", device if isinstance(device, int) else device.index)
+        self.n = chain.n
+        self.K_local, self.T = int(K_local), int(T)
+        self.K_total = int(K_total if K_total is not None else K_local)
+        self.k_offset = int(k_offset)
+        cfg = N.ChainConfigC()
+        cfg.K_local, cfg.T, cfg.K_total, cfg.k_offset = self.K_local, self.T, self.K_total, self.k_offset
+        cfg.delta_t, cfg.param_lambda = float(delta_t), float(param_lambda)
+        cfg.param_alpha, cfg.param_exploration = float(param_alpha), float(param_exploration)
+        sig = np.asarray(sigma, dtype=np.float64)
+        if sig.shape != (self.n, self.n):
+            raise ValueError(f"sigma must be {self.n} x {self.n}")
+        for i, v in enumerate(sig.ravel()):
+            cfg.sigma[i] = float(v)
+        for i in range(4):
+            cfg.stage_cost_weight[i] = float(stage_cost_weight[i])
+            cfg.terminal_cost_weight[i] = float(terminal_cost_weight[i])
+        cfg.chain.n = self.n
+        for f in ("m", "l", "lc", "I", "fk"):
+            arr = getattr(cfg.chain, f)
+            for i, v in enumerate(getattr(chain, f)):
+                arr[i] = float(v)
+        cfg.chain.g = float(chain.g)
+        with torch.cuda.device(self.device):
+            self.stream = torch.cuda.current_stream(self.device)
+            ctx = C.c_void_p()
+            N.check(self._lib.mppi_chain_ctx_create(C.byref(cfg), self.device.index,
+                                                    C.c_void_p(self.stream.cuda_stream), C.byref(ctx)),
+                    "mppi_chain_ctx_create")
+        self._ctx = ctx
+        blocks, threads, poll = C.c_int(), C.c_int(), C.c_int()
+        N.check(self._lib.mppi_chain_ctx_info(ctx, C.byref(blocks), C.byref(threads), C.byref(poll)),
+                "mppi_chain_ctx_info")
+        self.blocks, self.threads = blocks.value, threads.value
+        self.handoff = "poll" if poll.value else "counter"
+        self.partial_len = 2 + self.n * self.T
+
+    def close(self) -> None:
+        if getattr(self, "_ctx", None):
+            self._lib.mppi_chain_ctx_destroy(self._ctx)
+            self._ctx = None
+
+    def __del__(self):  # pragma: no cover - best effort
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def _sync_stream(self):
+        s = torch.cuda.current_stream(self.device)
+        if s.cuda_stream != self.stream.cuda_stream:
+            self.stream = s
+            N.check(self._lib.mppi_chain_set_stream(self._ctx, C.c_void_p(s.cuda_stream)), "mppi_chain_set_stream")
+
+    def new_noise(self) -> torch.Tensor:
+        return torch.empty((self.T, self.n, self.K_local), dtype=torch.float32, device=self.device)
+
+    def new_partial(self) -> torch.Tensor:
+        return torch.empty(self.partial_len, dtype=torch.float64, device=self.device)
+
+    def upload_noise(self, eps_ktn: np.ndarray, out: torch.Tensor | None = None) -> torch.Tensor:
+        """Reference-order noise (K_local, T, n) -> device [T][n][K_local] fp32."""
+        out = self.new_noise() if out is None else out
+        host = torch.from_numpy(np.ascontiguousarray(np.asarray(eps_ktn).transpose(1, 2, 0), dtype=np.float32))
+        out.copy_(host.pin_memory(), non_blocking=True)
+        return out
+
+    def set_step_inputs(self, x0, window, u=None) -> None:
+        self._sync_stream()
+        x0 = np.ascontiguousarray(np.asarray(x0, dtype=np.float64).ravel()[:2 * self.n])
+        win = np.ascontiguousarray(np.asarray(window, dtype=np.float64)[:, :4])
+        if win.ndim != 2 or win.shape[0] < 1 or win.shape[0] > N.MPPI_SEARCH_LEN:
+            raise ValueError("window must have 1..30 rows of [x, y, dq1, dq2]")
+        uu = None if u is None else np.ascontiguousarray(np.asarray(u, dtype=np.float64).reshape(self.T, self.n))
+        N.check(self._lib.mppi_chain_set_step_inputs(self._ctx, _dptr(x0), _dptr(win), win.shape[0],
+                                                     _dptr(uu) if uu is not None else None),
+                "mppi_chain_set_step_inputs")
+        self._keep = (x0, win, uu)
+
+    def rollout(self, noise: torch.Tensor, S_out: torch.Tensor | None = None,
+                partial_out: torch.Tensor | None = None, fused_update: bool = False) -> None:
+        self._sync_stream()
+        self._check_noise(noise)
+        if S_out is not None:
+            assert S_out.dtype == torch.float64 and S_out.numel() >= self.K_local and S_out.device == self.device
+        if partial_out is not None:
+            assert partial_out.dtype == torch.float64 and partial_out.numel() >= self.partial_len
+        N.check(self._lib.mppi_chain_rollout(self._ctx, C.c_void_p(noise.data_ptr()),
+                                             C.c_void_p(S_out.data_ptr()) if S_out is not None else None,
+                                             C.c_void_p(partial_out.data_ptr()) if partial_out is not None else None,
+                                             N.MPPI_FLAG_FUSED_UPDATE if fused_update else 0),
+                "mppi_chain_rollout")
+
+    def merge(self, partials: torch.Tensor, n: int, fused_update: bool = False) -> None:
+        self._sync_stream()
+        assert partials.dtype == torch.float64 and partials.is_contiguous()
+        assert partials.numel() >= n * self.partial_len
+        N.check(self._lib.mppi_chain_merge_partials(self._ctx, C.c_void_p(partials.data_ptr()), int(n),
+                                                    N.MPPI_FLAG_FUSED_UPDATE if fused_update else 0),
+                "mppi_chain_merge_partials")
+
+    def weighted_noise(self) -> np.ndarray:
+        self._sync_stream()
+        out = np.zeros((self.T, self.n))
+        N.check(self._lib.mppi_chain_get_weighted_noise(self._ctx, _dptr(out)), "mppi_chain_get_weighted_noise")
+        return out
+
+    def nominal(self) -> np.ndarray:
+        self._sync_stream()
+        out = np.zeros((self.T, self.n))
+        N.check(self._lib.mppi_chain_get_nominal(self._ctx, _dptr(out)), "mppi_chain_get_nominal")
+        return out
+
+    def trajectories(self, base_u=None, noise: torch.Tensor | None = None, K: int | None = None) -> torch.Tensor:
+        """(K, T, 2n) fp32 states of the off-by-one re-roll (control.py:129-145 analogue)."""
+        self._sync_stream()
+        K = self.K_local if K is None else int(K)
+        out = torch.empty((K, self.T, 2 * self.n), dtype=torch.float32, device=self.device)
+        bu = None if base_u is None else np.ascontiguousarray(np.asarray(base_u, dtype=np.float64).reshape(
+            self.T, self.n))
+        if noise is not None:
+            self._check_noise(noise)
+        N.check(self._lib.mppi_chain_rollout_traj(self._ctx, _dptr(bu) if bu is not None else None,
+                                                  C.c_void_p(noise.data_ptr()) if noise is not None else None,
+                                                  K, C.c_void_p(out.data_ptr())),
+                "mppi_chain_rollout_traj")
+        self._keep_traj = bu
+        return out
+
+    def philox_noise(self, seed: int, step: int = 0, out: torch.Tensor | None = None) -> torch.Tensor:
+        self._sync_stream()
+        out = self.new_noise() if out is None else out
+        self._check_noise(out)
+        N.check(self._lib.mppi_chain_noise_philox(self._ctx, int(seed) & (2 ** 64 - 1), int(step) & (2 ** 64 - 1),
+                                                  C.c_void_p(out.data_ptr())), "mppi_chain_noise_philox")
+        return out
+
+    def synchronize(self) -> None:
+        N.check(self._lib.mppi_chain_sync(self._ctx), "mppi_chain_sync")
+
+    def _check_noise(self, noise: torch.Tensor) -> None:
+        shape = (self.T, self.n, self.K_local)
+        if (noise.dtype != torch.float32 or not noise.is_contiguous() or noise.device != self.device
+                or tuple(noise.shape) != shape):
+            raise ValueError(f"noise must be a contiguous fp32 {shape} tensor on {self.device}")
+
+
+class ChainMPPIController:
+    """control.py:20-152 for the n-link chain (dim_u = n, dim_x = 2n)."""
+
+    def __init__(self, delta_t: float = 0.006, ref_path=0, horizon_step_T: int = 128,
+                 number_of_samples_K: int = 131072, param_exploration: float = 0.0, param_lambda: float = 100.0,
+                 param_alpha: float = 0.98, sigma: np.ndarray = CHAIN7_SIGMA,
+                 stage_cost_weight: np.ndarray = np.array([0.5, 0.5, 5.0, 5.0]),
+                 terminal_cost_weight: np.ndarray = np.array([5.0, 5.0, 50.0, 50.0]),
+                 visualize_optimal_traj=True, visualze_sampled_trajs=False, *, chain: ChainParams = ChainParams(),
+                 u_init=None, device: int | None = None, verbose: bool = False, noise: str = "numpy", seed: int = 0,
+                 process_group=None) -> None:
+        self.chain = chain
+        self.dim_u, self.dim_x = chain.n, 2 * chain.n
+        self.T, self.K = horizon_step_T, number_of_samples_K
+        self.param_exploration, self.param_lambda, self.param_alpha = param_exploration, param_lambda, param_alpha
+        self.param_gamma = self.param_lambda * (1.0 - self.param_alpha)
+        self.Sigma = np.asarray(sigma, dtype=np.float64)
+        self.stage_cost_weight, self.terminal_cost_weight = stage_cost_weight, terminal_cost_weight
+        self.visualize_optimal_traj, self.visualze_sampled_trajs = visualize_optimal_traj, visualze_sampled_trajs
+        self.delta_t, self.ref_path = delta_t, ref_path
+        u0 = np.zeros(self.dim_u) if u_init is None else np.asarray(u_init, dtype=np.float64)
+        self.u_prev = np.tile(u0, (self.T, 1)) if u0.ndim == 1 else u0.astype(np.float64).copy()
+        self.prev_waypoints_idx = 0
+        if noise not in ("numpy", "device"):
+            raise ValueError("noise must be 'numpy' or 'device'")
+        self.verbose, self.noise_source, self.seed = verbose, noise, int(seed)
+        self.process_group = process_group
+        self._device = device
+        self._engine = None
+        self._step_count = 0
+        self.keep_costs = False
+        self.last_S = None
+
+    def _shard(self):
+        if self.process_group is None:
+            return 1, 0
+        import torch.distributed as dist
+        return dist.get_world_size(self.process_group), dist.get_rank(self.process_group)
+
+    def _get_engine(self) -> ChainEngine:
+        if self._engine is None:
+            world, rank = self._shard()
+            K_local, k_offset = shard_geometry(self.K, world, rank)
+            device = self._device if self._device is not None else torch.cuda.current_device()
+            self._engine = ChainEngine(K_local, self.T, self.delta_t, self.param_lambda, self.param_alpha, self.Sigma,
+                                       self.stage_cost_weight, self.terminal_cost_weight, self.param_exploration,
+                                       self.chain, K_total=self.K, k_offset=k_offset, device=device)
+            self._noise_dev = self._engine.new_noise()
+            self._partial = self._engine.new_partial()
+            self._S_dev = torch.empty(K_local, dtype=torch.float64, device=self._engine.device)
+            if world > 1:
+                self._gathered = torch.empty(world * self._engine.partial_len, dtype=torch.float64,
+                                             device=self._engine.device)
+        return self._engine
+
+    def _effector(self, q):
+        th = np.cumsum(q)
+        fk = np.asarray(self.chain.fk)
+        return float((fk * np.cos(th)).sum()), float((fk * np.sin(th)).sum())
+
+    def _get_nearest_waypoint(self, x: float, y: float, update_prev_idx: bool = False):
+        """control.py:200-232 on the end-effector position, host fp64"""
+        prev_idx = self.prev_waypoints_idx
+        win = self.ref_path[prev_idx:(prev_idx + SEARCH_IDX_LEN)]
+        nearest_idx = int(np.argmin(((x - win[:, 0]) ** 2 + (y - win[:, 1]) ** 2) * 100)) + prev_idx
+        if update_prev_idx:
+            if self.verbose:
+                print(f"0     prev_idx = {prev_idx}")
+                print(f"0     nearest_idx = {nearest_idx}")
+                print("======================updated=======================")
+            self.prev_waypoints_idx = nearest_idx
+        return nearest_idx
+
+    def _calc_epsilon(self, sigma, size_sample, size_time_step, size_dim_u):
+        """control.py:154-164 — NumPy's legacy global RNG, n-dimensional"""
+        if sigma.shape[0] != sigma.shape[1] or sigma.shape[0] != size_dim_u or size_dim_u < 1:
+            print("[ERROR] sigma must be a square matrix with the size of size_dim_u.")
+            raise ValueError
+        return np.random.multivariate_normal(np.zeros(size_dim_u), sigma, (size_sample, size_time_step))
+
+    def calc_control_input(self, observed_x):
+        u = self.u_prev
+        x0 = np.asarray(observed_x, dtype=np.float64)
+        self._get_nearest_waypoint(*self._effector(x0[:self.dim_u]), update_prev_idx=True)
+        if self.prev_waypoints_idx >= self.ref_path.shape[0] - 1:
+            print("[ERROR] Reached the end of the reference path.")
+            raise IndexError
+        if self.noise_source == "numpy":
+            epsilon = self._calc_epsilon(self.Sigma, self.K, self.T, self.dim_u)
+        else:
+            epsilon = None
+        np.linalg.inv(self.Sigma)
+        eng = self._get_engine()
+        if epsilon is not None:
+            eng.upload_noise(epsilon[eng.k_offset:eng.k_offset + eng.K_local], out=self._noise_dev)
+        else:
+            eng.philox_noise(self.seed, self._step_count, out=self._noise_dev)
+        self._step_count += 1
+        window = self.ref_path[self.prev_waypoints_idx:(self.prev_waypoints_idx + SEARCH_IDX_LEN)]
+        eng.set_step_inputs(x0, window, u)
+        world, _ = self._shard()
+        if world == 1:
+            eng.rollout(self._noise_dev, S_out=self._S_dev if self.keep_costs else None)
+        else:
+            eng.rollout(self._noise_dev, S_out=self._S_dev if self.keep_costs else None, partial_out=self._partial)
+            exchange_partials(self._partial, self._gathered, self.process_group)
+            eng.merge(self._gathered, world)
+        w_epsilon = eng.weighted_noise()
+        if self.keep_costs:
+            self.last_S = self._S_dev.cpu().numpy()
+        w_epsilon = np.stack([median_filter(w_epsilon[:, d], size=10, mode="reflect")
+                              for d in range(self.dim_u)], axis=1)   # control.py:319-327
+        u += w_epsilon
+        optimal_traj = np.zeros((self.T, self.dim_x))
+        if self.visualize_optimal_traj:
+            optimal_traj = eng.trajectories(base_u=u, K=1)[0].double().cpu().numpy()
+        sampled = np.zeros((self.K, self.T, self.dim_x))
+        if self.visualze_sampled_trajs:
+            tr = eng.trajectories(base_u=None, noise=self._noise_dev)
+            if world > 1:
+                import torch.distributed as dist
+                parts = [None] * world
+                dist.all_gather_object(parts, (eng.k_offset, tr.cpu().numpy()), group=self.process_group)
+                for off, arr in parts:
+                    sampled[off:off + arr.shape[0]] = arr
+            else:
+                sampled[:] = tr.double().cpu().numpy()
+        self.u_prev[:-1] = u[1:]
+        self.u_prev[-1] = u[-1]
+        return u[0], u, optimal_traj, sampled
+
+    def close(self):
+        if self._engine is not None:
+            self._engine.close()
+            self._engine = None

@@ -1,0 +1,910 @@
+// mppi_chain.hip — MI355X (gfx950) MPPI engine for an n-link planar chain
+// (BASELINE config 5: "7-DoF arm dynamics (extended sys_params.py), K=131072
+// T=128, xydq_circle.txt reference").  The reference has no 7-DoF model; the
+// model is build-defined (oracle/chain_oracle.py, equations there) and reduces
+// to the reference's _F (control.py:234-263) at n = 2 with inertia := length.
+//
+//  * chain_rollout_kernel<N>: one lane per sample, the whole n-link step in
+//    fp32 registers (fully unrolled for N): prefix sums -> cos/sin of the
+//    absolute-angle differences from the cached sincos -> D = mu o cos(.) + I,
+//    Coriolis/centrifugal and gravity terms -> Cholesky of D (v_rsq) -> two
+//    triangular solves -> joint accelerations -> semi-implicit Euler -> new
+//    sincos (shared with the next step and the end-effector kinematics) ->
+//    the window search of the 2-link engine -> stage + control cost.  Noise is
+//    [T][N][K] fp32: N coalesced 4-B-per-lane rows per step.  Same epilogue,
+//    in-launch merges and fused update as the 2-link engine (mppi_device.h),
+//    with T*N columns per partial row (MAXCH = 4 column chunks).
+//  * chain_traj_kernel<N>, chain_philox_kernel: trajectory re-roll and
+//    counter-based Gaussian noise with an n x n Cholesky factor.
+//
+// C ABI: include/mppi_rocm.h (mppi_chain_*).
+#include <hip/hip_runtime.h>
+
+#include <math.h>
+#include <stdlib.h>
+#include <string.h>
+
+#include <string>
+
+#include "mppi_device.h"
+#include "mppi_host.h"
+#include "mppi_rocm.h"
+
+namespace {
+
+using namespace mppi;
+
+constexpr int kCMax = MPPI_CHAIN_MAX_DOF;   // links
+constexpr int kCT = 256;                    // threads per workgroup, one lane per sample
+constexpr int kCMaxCh = 4;                  // column chunks of a partial row: T N + 1 <= 4 x 256 ... (N <= 7)
+constexpr int kCMaxVals = kMaxT * kCMax;    // T N values per row, at most
+constexpr int kCPF = 2;                     // noise steps in flight per lane (N rows each)
+constexpr int kCPU = 2;                     // per-step constant rows in flight
+
+// Device-resident per-step parameter block (ping-pong pair in the context).
+struct alignas(16) ChainStep {
+    float4 win[kSlots];                    // rx, ry, rdq1, rdq2 of window slot j
+    float4 key[kSlots];                    // centred search keys (see Search)
+    float4 ctr;                            // window centre (cx, cy), W
+    float x0[2 * kCMax];                   // q[n], dq[n]
+    float ua[kMaxT + kCPU][2 * kCMax];     // u_t[n], a_t[n] (a = (gamma u_t)^T Sigma^-1), fp32; rows >= T zero
+    double u[kMaxT][kCMax];                // nominal control sequence, fp64
+};
+
+// Launch constants (kernel argument, by value).
+struct ChainConst {
+    int K_local, T, k_offset, k_exploit, nblocks, acquire, n, pad0;
+    float dt;
+    float mu[kCMax][kCMax];   // mu_ab (a != b), the constant part of D
+    float Dd[kCMax];          // D_aa = mu_aa + I_a (constant)
+    float gnu[kCMax];         // g nu_a
+    float fk[kCMax];          // cost kinematics lengths
+    float sw[4], tw[4];       // stage / terminal weights x 10000
+    double lambda, inv_lambda, gamma;
+    double sig_inv[kCMax * kCMax];
+};
+
+using CScratch = MergeScratch<kCMaxVals>;
+
+// Chain state of one sample: joint angles / rates and the cached sin / cos of
+// the absolute angles theta_a = q_1 + ... + q_a.
+template <int N>
+struct ChainState {
+    float q[N], dq[N], s[N], c[N];
+
+    __device__ __forceinline__ void angles() {
+        float th = 0.f;
+#pragma unroll
+        for (int a = 0; a < N; ++a) {
+            th += q[a];
+            sincos_f32(th, &s[a], &c[a]);
+        }
+    }
+
+    // One semi-implicit Euler step (oracle/chain_oracle.py chain_forward_dynamics):
+    //   D theta_ddot = tau - bias - g,  tau_a = v_a - v_{a+1},
+    //   D_ab = mu_ab cos(th_a - th_b) (+ I_a on the diagonal),
+    //   bias_a = sum_b mu_ab sin(th_a - th_b) thdot_b^2,  g_a = g nu_a cos th_a,
+    //   q_ddot_a = theta_ddot_a - theta_ddot_{a-1};  dq += q_ddot dt;  q += dq dt.
+    __device__ __forceinline__ void step(const float (&v)[N], const ChainConst& k) {
+        float w[N];
+        {
+            float acc = 0.f;
+#pragma unroll
+            for (int a = 0; a < N; ++a) {
+                acc += dq[a];
+                w[a] = acc * acc;   // thdot_a^2
+            }
+        }
+        float L[N][N];   // lower triangle: D, then its Cholesky factor in place
+        float r[N];
+#pragma unroll
+        for (int a = 0; a < N; ++a) {
+            L[a][a] = k.Dd[a];
+            r[a] = (a + 1 < N ? v[a] - v[a + 1] : v[a]) - k.gnu[a] * c[a];
+        }
+#pragma unroll
+        for (int a = 0; a < N; ++a) {
+#pragma unroll
+            for (int b = a + 1; b < N; ++b) {
+                const float cab = fmaf(c[a], c[b], s[a] * s[b]);   // cos(th_a - th_b)
+                const float sab = fmaf(s[a], c[b], -c[a] * s[b]);  // sin(th_a - th_b)
+                const float m = k.mu[a][b];
+                L[b][a] = m * cab;
+                const float ms = m * sab;
+                r[a] = fmaf(-ms, w[b], r[a]);   // - mu_ab sin(th_a - th_b) thdot_b^2
+                r[b] = fmaf(ms, w[a], r[b]);    // - mu_ba sin(th_b - th_a) thdot_a^2
+            }
+        }
+        float inv[N];
+#pragma unroll
+        for (int j = 0; j < N; ++j) {
+            float d = L[j][j];
+#pragma unroll
+            for (int q2 = 0; q2 < j; ++q2) d = fmaf(-L[j][q2], L[j][q2], d);
+            inv[j] = __builtin_amdgcn_rsqf(d);
+#pragma unroll
+            for (int i = j + 1; i < N; ++i) {
+                float e = L[i][j];
+#pragma unroll
+                for (int q2 = 0; q2 < j; ++q2) e = fmaf(-L[i][q2], L[j][q2], e);
+                L[i][j] = e * inv[j];
+            }
+        }
+#pragma unroll
+        for (int i = 0; i < N; ++i) {           // L y = r
+            float e = r[i];
+#pragma unroll
+            for (int q2 = 0; q2 < i; ++q2) e = fmaf(-L[i][q2], r[q2], e);
+            r[i] = e * inv[i];
+        }
+#pragma unroll
+        for (int i = N - 1; i >= 0; --i) {      // L^T z = y
+            float e = r[i];
+#pragma unroll
+            for (int q2 = i + 1; q2 < N; ++q2) e = fmaf(-L[q2][i], r[q2], e);
+            r[i] = e * inv[i];
+        }
+        float prev = 0.f;
+#pragma unroll
+        for (int a = 0; a < N; ++a) {
+            dq[a] = fmaf(r[a] - prev, k.dt, dq[a]);
+            prev = r[a];
+            q[a] = fmaf(dq[a], k.dt, q[a]);
+        }
+        angles();
+    }
+
+    __device__ __forceinline__ void effector(const ChainConst& k, float* px, float* py) const {
+        float x = 0.f, y = 0.f;
+#pragma unroll
+        for (int a = 0; a < N; ++a) {
+            x = fmaf(k.fk[a], c[a], x);
+            y = fmaf(k.fk[a], s[a], y);
+        }
+        *px = x;
+        *py = y;
+    }
+};
+
+// Median filter (control.py:319-327) of the T x N weighted noise, u += w_eps
+// (control.py:126), shift (control.py:148-149) and the next launch's fp32
+// per-step constants.  u_cur[ch]: this thread's cur->u value idx = tid + ch kCT,
+// read at kernel entry.
+template <int N>
+__device__ void chain_update_block(ChainStep* nxt, const ChainConst& c, CScratch& sm, const double (&u_cur)[kCMaxCh]) {
+    const int tid = threadIdx.x, T = c.T;
+#pragma unroll
+    for (int ch = 0; ch < kCMaxCh; ++ch) {
+        const int idx = tid + ch * kCT;
+        if (idx < T * N) sm.unew[idx] = u_cur[ch] + median_at(sm, idx / N, idx % N, T, N);
+    }
+    __syncthreads();
+    if (tid < T) {
+        const int src = tid + 1 < T ? tid + 1 : T - 1;
+        double u[N];
+#pragma unroll
+        for (int d = 0; d < N; ++d) {
+            u[d] = sm.unew[src * N + d];
+            nxt->u[tid][d] = u[d];
+            nxt->ua[tid][d] = (float)u[d];
+        }
+#pragma unroll
+        for (int d = 0; d < N; ++d) {
+            double a = 0.0;
+#pragma unroll
+            for (int e = 0; e < N; ++e) a += (c.gamma * u[e]) * c.sig_inv[e * N + d];
+            nxt->ua[tid][kCMax + d] = (float)a;
+        }
+    }
+}
+
+// POLL / counter hand-off and the merges as in rollout_kernel (mppi_rocm.hip).
+template <int N, bool POLL>
+__global__ __launch_bounds__(kCT) void chain_rollout_kernel(
+    const ChainConst c, const ChainStep* __restrict__ st, const float* __restrict__ noise,
+    double* __restrict__ S_out, double* __restrict__ slab, double* __restrict__ gslab,
+    unsigned* __restrict__ counters, double* __restrict__ partial_out, double* __restrict__ w_eps_out,
+    ChainStep* __restrict__ nxt, unsigned flags, unsigned* __restrict__ epoch, unsigned* __restrict__ tmo,
+    unsigned long long* __restrict__ dbg) {
+    static_assert(N <= kCMax && N >= 2, "links");
+    __shared__ float4 s_win[kSlots];
+    __shared__ float s_redf[kCT / 64];
+    __shared__ int s_cnt[kCT / 64];
+    __shared__ int s_k[kCT];
+    __shared__ float s_e[kCT];
+    __shared__ unsigned s_flag;
+    __shared__ CScratch sm;
+
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int k_raw = blockIdx.x * kCT + tid;
+    const bool valid = k_raw < c.K_local;
+    const int k = valid ? k_raw : c.K_local - 1;
+    const float exf = (c.k_offset + k) < c.k_exploit ? 1.f : 0.f;  // control.py:98-101
+    const int K = c.K_local, T = c.T;
+
+    STAMP(0, NOW());
+    const unsigned tag_v = POLL ? __hip_atomic_load(epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) + 1u : 0u;
+    double u_cur[kCMaxCh];
+#pragma unroll
+    for (int ch = 0; ch < kCMaxCh; ++ch) {
+        const int idx = tid + ch * kCT;
+        u_cur[ch] = ((flags & MPPI_FLAG_FUSED_UPDATE) && idx < T * N) ? st->u[idx / N][idx % N] : 0.0;
+    }
+    if (tid < kSlots) s_win[tid] = st->win[tid];
+    Search<1> sr;
+    sr.load(st->key, st->ctr, 0);
+    ChainState<N> x;
+#pragma unroll
+    for (int a = 0; a < N; ++a) {
+        x.q[a] = st->x0[a];
+        x.dq[a] = st->x0[N + a];
+    }
+    x.angles();
+    // noise row (t, d) of sample k: noise[(t N + d) K + k]; prefetches past the
+    // last step read row T - 1 again (never used)
+    const float* nk = noise + k;
+    auto nrow = [&](int t, int d) { return nk[((size_t)min(t, T - 1) * N + d) * K]; };
+    cfloat* cua = (cfloat*)(&st->ua[0][0]);
+    float ring[kCPF][N];
+    float uring[kCPU][2 * N];
+#pragma unroll
+    for (int j = 0; j < kCPF; ++j)
+#pragma unroll
+        for (int d = 0; d < N; ++d) ring[j][d] = nrow(j, d);
+#pragma unroll
+    for (int j = 0; j < kCPU; ++j)
+#pragma unroll
+        for (int d = 0; d < 2 * N; ++d) uring[j][d] = cua[j * 2 * kCMax + (d < N ? d : kCMax + d - N)];
+    __syncthreads();
+
+    // Horizon loop (control.py:95-109 with the chain model), S in fp64.
+    double S = 0.0;
+    float S4 = 0.f;
+    float ex = 0.f, ey = 0.f, e1 = 0.f, e2 = 0.f;
+    auto step = [&](int t, auto i_c) {
+        constexpr int i = decltype(i_c)::value;
+        float v[N];
+        float g = 0.f;
+#pragma unroll
+        for (int d = 0; d < N; ++d) {
+            v[d] = fmaf(exf, uring[i % kCPU][d], ring[i % kCPF][d]);   // u_t + eps or eps
+            g = fmaf(uring[i % kCPU][N + d], v[d], g);                 // (gamma u_t^T Sigma^-1) v, control.py:106
+        }
+#pragma unroll
+        for (int d = 0; d < N; ++d) ring[i % kCPF][d] = nrow(t + kCPF, d);
+#pragma unroll
+        for (int d = 0; d < 2 * N; ++d)
+            uring[i % kCPU][d] = cua[(t + kCPU) * 2 * kCMax + (d < N ? d : kCMax + d - N)];
+        PIN_LOADS();
+        x.step(v, c);
+        float px, py;
+        x.effector(c, &px, &py);
+        const float4 r = s_win[sr.nearest(px, py)];
+        ex = px - r.x;
+        ey = py - r.y;
+        e1 = x.dq[0] - r.z;
+        e2 = x.dq[1] - r.w;
+        S4 += weighted_sq(ex, ey, e1, e2, c.sw) + g;
+        if constexpr ((i & 3) == 3) {
+            S += (double)S4;
+            S4 = 0.f;
+        }
+    };
+    int t = 0;
+    for (; t + 4 <= T; t += 4)
+        unroll_seq([&](auto i_c) { step(t + decltype(i_c)::value, i_c); }, std::make_integer_sequence<int, 4>{});
+    unroll_seq([&](auto i_c) {
+        if (t + decltype(i_c)::value < T) step(t + decltype(i_c)::value, i_c);
+    }, std::make_integer_sequence<int, 3>{});
+    S += (double)S4;
+    S += (double)weighted_sq(ex, ey, e1, e2, c.tw);  // terminal cost, control.py:109
+
+    STAMP(1, NOW());
+    if (S_out && valid) S_out[k] = S;
+
+    // ---- workgroup partial: rho_b, eta_b, N_b (control.py:112-118 over this block)
+    const double rho_b = block_min_f64<kCT>(valid ? S : INFINITY, sm);
+    const float wgt = valid ? __expf((float)((rho_b - S) * c.inv_lambda)) : 0.f;
+    const bool nz = wgt >= 5.421010862e-20f;
+    const unsigned long long bal = __ballot(nz);
+    const float esum = wave_sum_f32(nz ? wgt : 0.f);
+    if (lane == 0) {
+        s_cnt[wave] = __popcll(bal);
+        s_redf[wave] = esum;
+    }
+    __syncthreads();
+    int off = 0, nl = 0;
+    double eta_b = 0.0;
+#pragma unroll
+    for (int w = 0; w < kCT / 64; ++w) {
+        off += (w < wave) ? s_cnt[w] : 0;
+        nl += s_cnt[w];
+        eta_b += (double)s_redf[w];
+    }
+    if (nz) {
+        const int pos = off + lanes_below(bal);
+        s_k[pos] = k;
+        s_e[pos] = wgt;
+    }
+    __syncthreads();
+    const int nval = T * N;
+    const RowGeo geo(nval);
+    const int stride = geo.stride;
+    const int nrows = c.nblocks;
+    const int ngroups = (nrows + kGroup - 1) / kGroup;
+    constexpr int kValBytes = POLL ? 16 : 8;
+    const __amdgpu_buffer_rsrc_t slab_r = rows_rsrc(slab, nrows * stride * kValBytes);
+    const __amdgpu_buffer_rsrc_t gslab_r = rows_rsrc(gslab, ngroups * stride * kValBytes);
+    const unsigned tag = __builtin_amdgcn_readfirstlane(tag_v);
+    auto publish = [&](int idx, double v) {
+        if constexpr (POLL) st_gran(slab_r, idx, v, tag);
+        else st_wt(slab_r, idx, v);
+    };
+    nl = __builtin_amdgcn_readfirstlane(nl);
+    if (nl <= kSparseMax) {
+        // column (t, d) = t N + d of the noise is the row noise[col K : col K + K]
+        for (int col = tid; col < nval; col += kCT) {
+            const float* base = noise + (size_t)col * K;
+            float e[kSparseMax];
+#pragma unroll
+            for (int l = 0; l < kSparseMax; ++l) e[l] = base[nl > 0 ? s_k[min(l, nl - 1)] : 0];
+            double acc = 0.0;
+#pragma unroll
+            for (int l = 0; l < kSparseMax; ++l)
+                if (l < nl) acc = fma((double)s_e[l], (double)e[l], acc);
+            publish(blockIdx.x * stride + 2 + col, acc);
+        }
+    } else {
+        constexpr int PER = kCT / 64;
+        constexpr int kRowBatch = 4;
+        const int k0 = blockIdx.x * kCT;
+        s_e[tid] = 0.f;
+        __syncthreads();
+        if (nz) s_e[k - k0] = wgt;
+        __syncthreads();
+        double w[PER];
+#pragma unroll
+        for (int i = 0; i < PER; ++i) w[i] = (k0 + lane + 64 * i < K) ? (double)s_e[lane + 64 * i] : 0.0;
+        for (int cb = wave * kRowBatch; cb < nval; cb += (kCT / 64) * kRowBatch) {
+            float e[kRowBatch][PER];
+#pragma unroll
+            for (int r = 0; r < kRowBatch; ++r) {
+                const int cr = min(cb + r, nval - 1);
+#pragma unroll
+                for (int i = 0; i < PER; ++i) e[r][i] = noise[(size_t)cr * K + min(k0 + lane + 64 * i, K - 1)];
+            }
+#pragma unroll
+            for (int r = 0; r < kRowBatch; ++r) {
+                double a = 0.0;
+#pragma unroll
+                for (int i = 0; i < PER; ++i) a = fma(w[i], (double)e[r][i], a);
+                a = wave_sum_f64(a);
+                if (lane == 0 && cb + r < nval) publish(blockIdx.x * stride + 2 + cb + r, a);
+            }
+        }
+    }
+    if (tid == 0) {
+        publish(blockIdx.x * stride, rho_b);
+        publish(blockIdx.x * stride + 1, eta_b);
+    }
+    STAMP(2, NOW());
+    STAMP(5, (unsigned long long)nl);
+    const int g = blockIdx.x / kGroup;
+    const int gsz = min(kGroup, nrows - g * kGroup);
+    if constexpr (POLL) {
+        if ((int)blockIdx.x != g * kGroup + gsz - 1) return;
+        STAMP(3, NOW());
+        if (ngroups == 1) {
+            merge_rows_block<kCT, kCMaxCh, true, true>(slab_r, 0, gsz, geo, c.inv_lambda, sm, nullptr, 0, partial_out,
+                                                       w_eps_out, tag, tmo);
+        } else if ((int)blockIdx.x == nrows - 1 && nrows <= kDirectRows &&
+                   direct_merge<kCT, kCMaxCh, true>(slab_r, nrows, geo, c.inv_lambda, sm, partial_out, w_eps_out, tag,
+                                                    tmo)) {
+        } else {
+            merge_rows_block<kCT, kCMaxCh, false, true>(slab_r, g * kGroup, gsz, geo, c.inv_lambda, sm, &gslab_r, g,
+                                                        nullptr, nullptr, tag, tmo);
+            STAMP(10, NOW());
+            if ((int)blockIdx.x != nrows - 1) return;
+            STAMP(4, NOW());
+            merge_rows_block<kCT, kCMaxCh, true, true>(gslab_r, 0, ngroups, geo, c.inv_lambda, sm, nullptr, 0,
+                                                       partial_out, w_eps_out, tag, tmo);
+        }
+        if (threadIdx.x == 0) __hip_atomic_store(epoch, tag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    } else {
+        if (!arrive_last(counters + g, (unsigned)gsz, &s_flag, c.acquire != 0)) return;
+        STAMP(3, NOW());
+        merge_rows_block<kCT, kCMaxCh, false, false>(slab_r, g * kGroup, gsz, geo, c.inv_lambda, sm, &gslab_r, g,
+                                                     nullptr, nullptr, 0u, nullptr);
+        STAMP(10, NOW());
+        if (!arrive_last(counters + ngroups, (unsigned)ngroups, &s_flag, c.acquire != 0)) return;
+        STAMP(4, NOW());
+        if (!(ngroups > 1 && nrows <= kDirectRows &&
+              direct_merge<kCT, kCMaxCh, false>(slab_r, nrows, geo, c.inv_lambda, sm, partial_out, w_eps_out, 0u,
+                                                nullptr)))
+            merge_rows_block<kCT, kCMaxCh, true, false>(gslab_r, 0, ngroups, geo, c.inv_lambda, sm, nullptr, 0,
+                                                        partial_out, w_eps_out, 0u, nullptr);
+    }
+    STAMP(11, NOW());
+    STAMP(6, (unsigned long long)sm.nrel);
+    if (flags & MPPI_FLAG_FUSED_UPDATE) chain_update_block<N>(nxt, c, sm, u_cur);
+    STAMP(7, NOW());
+}
+
+// Merge of the all-gathered per-device rows (multi-GPU), plus the fused update.
+template <int N>
+__global__ __launch_bounds__(kCT) void chain_merge_kernel(const ChainConst c, const ChainStep* cur, const double* parts,
+                                                          int n, double* w_eps_out, ChainStep* nxt, unsigned flags) {
+    __shared__ CScratch sm;
+    const int tid = threadIdx.x, T = c.T;
+    double u_cur[kCMaxCh];
+#pragma unroll
+    for (int ch = 0; ch < kCMaxCh; ++ch) {
+        const int idx = tid + ch * kCT;
+        u_cur[ch] = ((flags & MPPI_FLAG_FUSED_UPDATE) && idx < T * N) ? cur->u[idx / N][idx % N] : 0.0;
+    }
+    const RowGeo geo(T * N);
+    const __amdgpu_buffer_rsrc_t r = rows_rsrc(parts, n * geo.stride * 8);
+    merge_rows_block<kCT, kCMaxCh, true, false>(r, 0, n, geo, c.inv_lambda, sm, nullptr, 0, nullptr, w_eps_out, 0u,
+                                                nullptr);
+    if (flags & MPPI_FLAG_FUSED_UPDATE) chain_update_block<N>(nxt, c, sm, u_cur);
+}
+
+// Trajectory re-roll (control.py:129-145 with the chain): control(t) =
+// base[(t-1) mod T] (+ eps); out[k][t][2N] = (q, dq) after step t.
+template <int N>
+__global__ __launch_bounds__(kCT) void chain_traj_kernel(const ChainConst c, const ChainStep* __restrict__ st,
+                                                         const float* __restrict__ base,
+                                                         const float* __restrict__ noise, int Kn,
+                                                         float* __restrict__ out) {
+    const int k = blockIdx.x * kCT + threadIdx.x;
+    if (k >= Kn) return;
+    const int T = c.T;
+    const float exf = noise ? ((c.k_offset + k) < c.k_exploit ? 1.f : 0.f) : 1.f;
+    ChainState<N> x;
+#pragma unroll
+    for (int a = 0; a < N; ++a) {
+        x.q[a] = st->x0[a];
+        x.dq[a] = st->x0[N + a];
+    }
+    x.angles();
+    for (int t = 0; t < T; ++t) {
+        const int ti = t == 0 ? T - 1 : t - 1;
+        float v[N];
+#pragma unroll
+        for (int d = 0; d < N; ++d) {
+            v[d] = base[ti * N + d];
+            if (noise) v[d] = fmaf(exf, v[d], noise[((size_t)ti * N + d) * c.K_local + k]);
+        }
+        x.step(v, c);
+        float* o = out + ((size_t)k * T + t) * 2 * N;
+#pragma unroll
+        for (int a = 0; a < N; ++a) {
+            o[a] = x.q[a];
+            o[N + a] = x.dq[a];
+        }
+    }
+}
+
+// eps[t][d][k] = (L z)_d, z ~ N(0, I) from Philox4x32-10 counters (global k, t,
+// call) + Box-Muller: a shard generates exactly its slice of the unsharded draw.
+__global__ __launch_bounds__(kCT) void chain_philox_kernel(int K_local, int T, int n, long long k_offset,
+                                                           unsigned long long seed, unsigned long long step,
+                                                           const float* __restrict__ Lch, float* __restrict__ out) {
+    const long long idx = (long long)blockIdx.x * kCT + threadIdx.x;
+    if (idx >= (long long)K_local * T) return;
+    const int k = (int)(idx % K_local);
+    const int t = (int)(idx / K_local);
+    const unsigned long long kg = (unsigned long long)(k_offset + k);
+    const uint2 key = make_uint2((unsigned)seed, (unsigned)(seed >> 32) ^ (unsigned)(step >> 32));
+    float z[kCMax];
+#pragma unroll
+    for (int call = 0; call < kCMax / 4; ++call) {
+        const uint4 ctr = make_uint4((unsigned)kg, (unsigned)(kg >> 32), (unsigned)(t * 4 + call), (unsigned)step);
+        const uint4 r = philox4x32_10(ctr, key);
+        const float2 a = box_muller(r.x, r.y), b = box_muller(r.z, r.w);
+        z[4 * call] = a.x;
+        z[4 * call + 1] = a.y;
+        z[4 * call + 2] = b.x;
+        z[4 * call + 3] = b.y;
+    }
+    for (int d = 0; d < n; ++d) {
+        float e = 0.f;
+        for (int j = 0; j <= d; ++j) e = fmaf(Lch[d * kCMax + j], z[j], e);
+        out[((size_t)t * n + d) * K_local + k] = e;
+    }
+}
+
+}  // namespace
+
+// ================================================================ host side
+
+struct mppi_chain_ctx {
+    mppi_chain_config cfg;
+    int device = 0, n = 0;
+    hipStream_t stream = nullptr;
+    int nblocks = 0;
+    bool poll = false;
+    ChainConst kc;
+    ChainStep* d_step = nullptr;   // [2] ping-pong
+    int cur = 0;
+    ChainStep* h_step = nullptr;   // pinned staging
+    hipEvent_t staged = nullptr;
+    double* d_slab = nullptr;
+    double* d_gslab = nullptr;
+    unsigned* d_counter = nullptr;
+    unsigned* d_epoch = nullptr;
+    double* d_weps = nullptr;
+    double* h_buf = nullptr;
+    float* d_base = nullptr;
+    float* h_base = nullptr;
+    float* d_chol = nullptr;       // Cholesky factor of Sigma (kCMax x kCMax, fp32) for the Philox noise
+    unsigned* h_tmo = nullptr;
+    unsigned* d_tmo = nullptr;
+    unsigned long long* d_dbg = nullptr;
+};
+
+namespace {
+
+using mppi_host::fail;
+
+template <int N, bool P>
+void launch_rollout(mppi_chain_ctx* c, const ChainStep* cur, const float* noise, double* S, double* part, ChainStep* nxt,
+                    unsigned flags) {
+    hipLaunchKernelGGL((chain_rollout_kernel<N, P>), dim3(c->nblocks), dim3(kCT), 0, c->stream, c->kc, cur, noise, S,
+                       c->d_slab, c->d_gslab, c->d_counter, part, c->d_weps, nxt, flags, c->d_epoch, c->d_tmo,
+                       c->d_dbg);
+}
+
+// the link counts with an instantiated kernel
+#define MPPI_CHAIN_DISPATCH(n, F) \
+    switch (n) {                  \
+        case 2: F(2); break;      \
+        case 3: F(3); break;      \
+        case 4: F(4); break;      \
+        case 5: F(5); break;      \
+        case 6: F(6); break;      \
+        case 7: F(7); break;      \
+        default: break;           \
+    }
+
+int check_tmo(mppi_chain_ctx* c) {
+    if (c->h_tmo && __atomic_load_n(c->h_tmo, __ATOMIC_ACQUIRE)) {
+        *c->h_tmo = 0;
+        return fail(MPPI_E_HIP, "in-launch hand-off timed out (workgroups not co-resident?); results invalid");
+    }
+    return MPPI_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+int mppi_chain_ctx_create(const mppi_chain_config* cfg, int device, void* stream, mppi_chain_ctx** out) {
+    if (!cfg || !out) return fail(MPPI_E_ARG, "null argument");
+    *out = nullptr;
+    const int n = cfg->chain.n;
+    if (n < 2 || n > 7) return fail(MPPI_E_ARG, "chain.n must be in [2, 7]");
+    if (cfg->T < 1 || cfg->T > MPPI_MAX_T) return fail(MPPI_E_ARG, "T must be in [1, 128]");
+    if (cfg->T * n + 1 > kCMaxCh * kCT) return fail(MPPI_E_ARG, "T * n too large");
+    if (cfg->K_local < 1 || cfg->K_total < cfg->K_local || cfg->k_offset < 0 ||
+        cfg->k_offset + (long long)cfg->K_local > cfg->K_total)
+        return fail(MPPI_E_ARG, "bad sample geometry (K_local, K_total, k_offset)");
+    if ((long long)cfg->K_local * cfg->T * n >= (1LL << 31)) return fail(MPPI_E_ARG, "too many samples");
+    // Sigma: symmetric positive definite (Cholesky), inverse for the control cost
+    double Lc[kCMax][kCMax] = {}, Si[kCMax * kCMax] = {};
+    {
+        const double* S = cfg->sigma;
+        for (int j = 0; j < n; ++j) {
+            double d = S[j * n + j];
+            for (int q = 0; q < j; ++q) d -= Lc[j][q] * Lc[j][q];
+            if (!(d > 0.0) || !isfinite(d)) return fail(MPPI_E_SINGULAR, "Sigma is not positive definite");
+            Lc[j][j] = sqrt(d);
+            for (int i = j + 1; i < n; ++i) {
+                double e = 0.5 * (S[i * n + j] + S[j * n + i]);
+                for (int q = 0; q < j; ++q) e -= Lc[i][q] * Lc[j][q];
+                Lc[i][j] = e / Lc[j][j];
+            }
+        }
+        for (int col = 0; col < n; ++col) {   // Sigma^-1 = L^-T L^-1, column by column
+            double y[kCMax] = {};
+            for (int i = 0; i < n; ++i) {
+                double e = i == col ? 1.0 : 0.0;
+                for (int q = 0; q < i; ++q) e -= Lc[i][q] * y[q];
+                y[i] = e / Lc[i][i];
+            }
+            for (int i = n - 1; i >= 0; --i) {
+                double e = y[i];
+                for (int q = i + 1; q < n; ++q) e -= Lc[q][i] * y[q];
+                y[i] = e / Lc[i][i];
+            }
+            for (int i = 0; i < n; ++i) Si[i * n + col] = y[i];
+        }
+    }
+    mppi_chain_ctx* c = new mppi_chain_ctx();
+    c->cfg = *cfg;
+    c->device = device;
+    c->n = n;
+    c->stream = (hipStream_t)stream;
+    c->nblocks = (cfg->K_local + kCT - 1) / kCT;
+    ChainConst& k = c->kc;
+    memset(&k, 0, sizeof(k));
+    k.K_local = cfg->K_local;
+    k.T = cfg->T;
+    k.k_offset = cfg->k_offset;
+    {
+        const double thr = (1.0 - cfg->param_exploration) * (double)cfg->K_total;  // control.py:98
+        long long kx = thr <= 0.0 ? 0 : (long long)ceil(thr);
+        if (kx > cfg->K_total) kx = cfg->K_total;
+        k.k_exploit = (int)kx;
+    }
+    k.nblocks = c->nblocks;
+    k.n = n;
+    k.dt = (float)cfg->delta_t;
+    const mppi_chain_params& P = cfg->chain;
+    for (int a = 0; a < n; ++a) {
+        double tail = 0.0;
+        for (int q = a + 1; q < n; ++q) tail += P.m[q];
+        const double mu_aa = P.m[a] * P.lc[a] * P.lc[a] + P.l[a] * P.l[a] * tail;
+        k.Dd[a] = (float)(mu_aa + P.I[a]);
+        k.gnu[a] = (float)(P.g * (P.m[a] * P.lc[a] + P.l[a] * tail));
+        k.fk[a] = (float)P.fk[a];
+        for (int b = a + 1; b < n; ++b) {
+            double tb = 0.0;
+            for (int q = b + 1; q < n; ++q) tb += P.m[q];
+            k.mu[a][b] = k.mu[b][a] = (float)(P.l[a] * (P.m[b] * P.lc[b] + P.l[b] * tb));
+        }
+    }
+    for (int i = 0; i < 4; ++i) {
+        k.sw[i] = (float)(cfg->stage_cost_weight[i] * 10000.0);     // control.py:185
+        k.tw[i] = (float)(cfg->terminal_cost_weight[i] * 10000.0);  // control.py:198
+    }
+    k.lambda = cfg->param_lambda;
+    k.inv_lambda = 1.0 / cfg->param_lambda;
+    k.gamma = cfg->param_lambda * (1.0 - cfg->param_alpha);
+    for (int i = 0; i < n * n; ++i) k.sig_inv[i] = Si[i];
+
+    auto cleanup_fail = [&](int rc) {
+        mppi_chain_ctx_destroy(c);
+        return rc;
+    };
+    hipError_t e;
+    if ((e = hipSetDevice(device)) != hipSuccess)
+        return cleanup_fail(fail(MPPI_E_HIP, std::string("hipSetDevice: ") + hipGetErrorString(e)));
+    int ncu = 0, per_cu = 0;
+    if ((e = hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, device)) != hipSuccess)
+        return cleanup_fail(fail(MPPI_E_HIP, std::string("device attributes: ") + hipGetErrorString(e)));
+#define MPPI_OCC(N) (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, (const void*)chain_rollout_kernel<N, true>, kCT, 0)
+    MPPI_CHAIN_DISPATCH(n, MPPI_OCC)
+#undef MPPI_OCC
+    c->poll = per_cu >= 1 && c->nblocks <= ncu;
+    if (const char* ev = getenv("MPPI_HANDOFF")) {
+        if (!strcmp(ev, "counter")) c->poll = false;
+    }
+    k.acquire = (!c->poll && c->nblocks > ncu) ? 1 : 0;
+    const size_t val = c->poll ? 16 : sizeof(double);
+    const int stride = 2 + cfg->T * n;
+    const size_t slab = (size_t)c->nblocks * stride * val;
+    const int ngroups = (c->nblocks + kGroup - 1) / kGroup;
+    const size_t gslab = (size_t)ngroups * stride * val;
+    const size_t ctr_bytes = ((size_t)(ngroups + 2) * sizeof(unsigned) + 255) & ~(size_t)255;
+    float chol[kCMax * kCMax] = {};
+    for (int i = 0; i < n; ++i)
+        for (int j = 0; j <= i; ++j) chol[i * kCMax + j] = (float)Lc[i][j];
+    if ((e = hipMalloc(&c->d_step, 2 * sizeof(ChainStep))) != hipSuccess ||
+        (e = hipMalloc(&c->d_slab, slab)) != hipSuccess || (e = hipMalloc(&c->d_gslab, gslab)) != hipSuccess ||
+        (e = hipMalloc(&c->d_counter, ctr_bytes)) != hipSuccess ||
+        (e = hipMalloc(&c->d_weps, kCMaxVals * sizeof(double))) != hipSuccess ||
+        (e = hipMalloc(&c->d_base, kCMaxVals * sizeof(float))) != hipSuccess ||
+        (e = hipMalloc(&c->d_chol, sizeof(chol))) != hipSuccess ||
+        (e = hipHostMalloc(&c->h_step, sizeof(ChainStep), hipHostMallocDefault)) != hipSuccess ||
+        (e = hipHostMalloc(&c->h_buf, kCMaxVals * sizeof(double), hipHostMallocDefault)) != hipSuccess ||
+        (e = hipHostMalloc(&c->h_base, kCMaxVals * sizeof(float), hipHostMallocDefault)) != hipSuccess ||
+        (e = hipHostMalloc(&c->h_tmo, 256, hipHostMallocMapped)) != hipSuccess ||
+        (e = hipHostGetDevicePointer((void**)&c->d_tmo, c->h_tmo, 0)) != hipSuccess ||
+        (e = hipEventCreateWithFlags(&c->staged, hipEventDisableTiming)) != hipSuccess ||
+        (e = hipMemset(c->d_counter, 0, ctr_bytes)) != hipSuccess || (e = hipMemset(c->d_slab, 0, slab)) != hipSuccess ||
+        (e = hipMemset(c->d_gslab, 0, gslab)) != hipSuccess ||
+        (e = hipMemset(c->d_step, 0, 2 * sizeof(ChainStep))) != hipSuccess ||
+        (e = hipMemset(c->d_weps, 0, kCMaxVals * sizeof(double))) != hipSuccess ||
+        (e = hipMemcpy(c->d_chol, chol, sizeof(chol), hipMemcpyHostToDevice)) != hipSuccess ||
+        (e = hipDeviceSynchronize()) != hipSuccess)
+        return cleanup_fail(fail(MPPI_E_HIP, std::string("allocation: ") + hipGetErrorString(e)));
+    memset(c->h_step, 0, sizeof(ChainStep));
+    *c->h_tmo = 0;
+    c->d_epoch = c->d_counter + ngroups + 1;
+    *out = c;
+    return MPPI_OK;
+}
+
+void mppi_chain_ctx_destroy(mppi_chain_ctx* c) {
+    if (!c) return;
+    if (c->stream) (void)hipStreamSynchronize(c->stream);
+    (void)hipDeviceSynchronize();
+    (void)hipFree(c->d_step);
+    (void)hipFree(c->d_slab);
+    (void)hipFree(c->d_gslab);
+    (void)hipFree(c->d_counter);
+    (void)hipFree(c->d_weps);
+    (void)hipFree(c->d_base);
+    (void)hipFree(c->d_chol);
+    if (c->h_step) (void)hipHostFree(c->h_step);
+    if (c->h_buf) (void)hipHostFree(c->h_buf);
+    if (c->h_base) (void)hipHostFree(c->h_base);
+    if (c->h_tmo) (void)hipHostFree(c->h_tmo);
+    if (c->staged) (void)hipEventDestroy(c->staged);
+    delete c;
+}
+
+int mppi_chain_set_stream(mppi_chain_ctx* c, void* stream) {
+    if (!c) return fail(MPPI_E_ARG, "null context");
+    c->stream = (hipStream_t)stream;
+    return MPPI_OK;
+}
+
+int mppi_chain_ctx_info(const mppi_chain_ctx* c, int* blocks, int* threads, int* poll) {
+    if (!c) return fail(MPPI_E_ARG, "null context");
+    if (blocks) *blocks = c->nblocks;
+    if (threads) *threads = kCT;
+    if (poll) *poll = c->poll ? 1 : 0;
+    return MPPI_OK;
+}
+
+int mppi_chain_set_step_inputs(mppi_chain_ctx* c, const double* x0, const double* window, int W, const double* u) {
+    if (!c || !x0 || !window) return fail(MPPI_E_ARG, "null argument");
+    if (W < 1 || W > MPPI_SEARCH_LEN) return fail(MPPI_E_ARG, "window rows must be in [1, 30]");
+    const int n = c->n, T = c->cfg.T;
+    if (hipEventSynchronize(c->staged) != hipSuccess) return fail(MPPI_E_HIP, "staging event");
+    ChainStep* h = c->h_step;
+    double cx = 0.0, cy = 0.0;
+    for (int j = 0; j < W; ++j) {
+        cx += window[4 * j];
+        cy += window[4 * j + 1];
+    }
+    cx /= W;
+    cy /= W;
+    for (int j = 0; j < kSlots; ++j) {
+        if (j < W) {
+            const double* r = window + 4 * j;
+            h->win[j] = make_float4((float)r[0], (float)r[1], (float)r[2], (float)r[3]);
+            const double rx = r[0] - cx, ry = r[1] - cy;
+            h->key[j] = make_float4((float)rx, (float)ry, (float)(rx * rx + ry * ry), 0.f);
+        } else {
+            h->win[j] = make_float4(0.f, 0.f, 0.f, 0.f);
+            h->key[j] = make_float4(0.f, 0.f, kPadKey, 0.f);
+        }
+    }
+    h->ctr = make_float4((float)cx, (float)cy, (float)W, 0.f);
+    for (int a = 0; a < 2 * kCMax; ++a) h->x0[a] = a < 2 * n ? (float)x0[a] : 0.f;
+    size_t bytes = offsetof(ChainStep, ua);
+    if (u) {
+        const ChainConst& k = c->kc;
+        for (int t = 0; t < T; ++t) {
+            for (int d = 0; d < kCMax; ++d) {
+                h->ua[t][d] = d < n ? (float)u[t * n + d] : 0.f;
+                h->u[t][d] = d < n ? u[t * n + d] : 0.0;
+                double a = 0.0;
+                if (d < n)
+                    for (int e2 = 0; e2 < n; ++e2) a += (k.gamma * u[t * n + e2]) * k.sig_inv[e2 * n + d];
+                h->ua[t][kCMax + d] = (float)a;
+            }
+        }
+        bytes = sizeof(ChainStep);
+    }
+    if (hipMemcpyAsync(c->d_step + (c->cur ^ 1), h, offsetof(ChainStep, ua), hipMemcpyHostToDevice, c->stream) !=
+            hipSuccess ||
+        hipMemcpyAsync(c->d_step + c->cur, h, bytes, hipMemcpyHostToDevice, c->stream) != hipSuccess ||
+        hipEventRecord(c->staged, c->stream) != hipSuccess)
+        return fail(MPPI_E_HIP, "step input upload");
+    return MPPI_OK;
+}
+
+int mppi_chain_rollout(mppi_chain_ctx* c, const float* noise_dev, double* S_dev, double* partial_dev, unsigned flags) {
+    if (!c || !noise_dev) return fail(MPPI_E_ARG, "null argument");
+    if ((flags & MPPI_FLAG_FUSED_UPDATE) && c->cfg.T < 5)
+        return fail(MPPI_E_ARG, "device median filter needs T >= 5 (use the host update)");
+    const ChainStep* cur = c->d_step + c->cur;
+    ChainStep* nxt = c->d_step + (c->cur ^ 1);
+#define MPPI_L(N)                                                                       \
+    if (c->poll) launch_rollout<N, true>(c, cur, noise_dev, S_dev, partial_dev, nxt, flags); \
+    else launch_rollout<N, false>(c, cur, noise_dev, S_dev, partial_dev, nxt, flags)
+    MPPI_CHAIN_DISPATCH(c->n, MPPI_L)
+#undef MPPI_L
+    const hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return fail(MPPI_E_HIP, std::string("chain_rollout_kernel: ") + hipGetErrorString(e));
+    if (flags & MPPI_FLAG_FUSED_UPDATE) c->cur ^= 1;
+    return MPPI_OK;
+}
+
+int mppi_chain_merge_partials(mppi_chain_ctx* c, const double* partials_dev, int nparts, unsigned flags) {
+    if (!c || !partials_dev || nparts < 1) return fail(MPPI_E_ARG, "bad argument");
+    if ((flags & MPPI_FLAG_FUSED_UPDATE) && c->cfg.T < 5)
+        return fail(MPPI_E_ARG, "device median filter needs T >= 5 (use the host update)");
+    const ChainStep* cur = c->d_step + c->cur;
+    ChainStep* nxt = c->d_step + (c->cur ^ 1);
+#define MPPI_M(N)                                                                                              \
+    hipLaunchKernelGGL(chain_merge_kernel<N>, dim3(1), dim3(kCT), 0, c->stream, c->kc, cur, partials_dev, nparts, \
+                       c->d_weps, nxt, flags)
+    MPPI_CHAIN_DISPATCH(c->n, MPPI_M)
+#undef MPPI_M
+    const hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return fail(MPPI_E_HIP, std::string("chain_merge_kernel: ") + hipGetErrorString(e));
+    if (flags & MPPI_FLAG_FUSED_UPDATE) c->cur ^= 1;
+    return MPPI_OK;
+}
+
+int mppi_chain_get_weighted_noise(mppi_chain_ctx* c, double* w_eps_host) {
+    if (!c || !w_eps_host) return fail(MPPI_E_ARG, "null argument");
+    const size_t bytes = (size_t)c->cfg.T * c->n * sizeof(double);
+    if (hipMemcpyAsync(c->h_buf, c->d_weps, bytes, hipMemcpyDeviceToHost, c->stream) != hipSuccess ||
+        hipStreamSynchronize(c->stream) != hipSuccess)
+        return fail(MPPI_E_HIP, "weighted noise read-back");
+    memcpy(w_eps_host, c->h_buf, bytes);
+    return check_tmo(c);
+}
+
+int mppi_chain_get_nominal(mppi_chain_ctx* c, double* u_host) {
+    if (!c || !u_host) return fail(MPPI_E_ARG, "null argument");
+    const int n = c->n, T = c->cfg.T;
+    if (hipMemcpyAsync(c->h_buf, (const char*)(c->d_step + c->cur) + offsetof(ChainStep, u),
+                       (size_t)T * kCMax * sizeof(double), hipMemcpyDeviceToHost, c->stream) != hipSuccess ||
+        hipStreamSynchronize(c->stream) != hipSuccess)
+        return fail(MPPI_E_HIP, "nominal read-back");
+    for (int t = 0; t < T; ++t)
+        for (int d = 0; d < n; ++d) u_host[t * n + d] = c->h_buf[t * kCMax + d];
+    return check_tmo(c);
+}
+
+int mppi_chain_rollout_traj(mppi_chain_ctx* c, const double* base_u, const float* noise_dev, int K, float* out_dev) {
+    if (!c || !out_dev || K < 1 || K > c->cfg.K_local) return fail(MPPI_E_ARG, "bad argument");
+    const int n = c->n, T = c->cfg.T;
+    const ChainStep* cur = c->d_step + c->cur;
+    if (base_u) {
+        if (hipEventSynchronize(c->staged) != hipSuccess) return fail(MPPI_E_HIP, "staging event");
+        for (int i = 0; i < T * n; ++i) c->h_base[i] = (float)base_u[i];
+        if (hipMemcpyAsync(c->d_base, c->h_base, (size_t)T * n * sizeof(float), hipMemcpyHostToDevice, c->stream) !=
+                hipSuccess ||
+            hipEventRecord(c->staged, c->stream) != hipSuccess)
+            return fail(MPPI_E_HIP, "base upload");
+    } else {
+        // the nominal u of the current step block: ua[t][0:n], row stride 2 kCMax floats
+        if (hipMemcpy2DAsync(c->d_base, n * sizeof(float), (const char*)cur + offsetof(ChainStep, ua),
+                             2 * kCMax * sizeof(float), n * sizeof(float), T, hipMemcpyDeviceToDevice,
+                             c->stream) != hipSuccess)
+            return fail(MPPI_E_HIP, "base copy");
+    }
+    const int blocks = (K + kCT - 1) / kCT;
+#define MPPI_T(N)                                                                                                  \
+    hipLaunchKernelGGL(chain_traj_kernel<N>, dim3(blocks), dim3(kCT), 0, c->stream, c->kc, cur, c->d_base, noise_dev, \
+                       K, out_dev)
+    MPPI_CHAIN_DISPATCH(n, MPPI_T)
+#undef MPPI_T
+    const hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return fail(MPPI_E_HIP, std::string("chain_traj_kernel: ") + hipGetErrorString(e));
+    return MPPI_OK;
+}
+
+int mppi_chain_noise_philox(mppi_chain_ctx* c, unsigned long long seed, unsigned long long step, float* out_dev) {
+    if (!c || !out_dev) return fail(MPPI_E_ARG, "null argument");
+    const long long nth = (long long)c->cfg.K_local * c->cfg.T;
+    const int blocks = (int)((nth + kCT - 1) / kCT);
+    hipLaunchKernelGGL(chain_philox_kernel, dim3(blocks), dim3(kCT), 0, c->stream, c->cfg.K_local, c->cfg.T, c->n,
+                       (long long)c->cfg.k_offset, seed, step, c->d_chol, out_dev);
+    const hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return fail(MPPI_E_HIP, std::string("chain_philox_kernel: ") + hipGetErrorString(e));
+    return MPPI_OK;
+}
+
+int mppi_chain_sync(mppi_chain_ctx* c) {
+    if (!c) return fail(MPPI_E_ARG, "null context");
+    if (hipStreamSynchronize(c->stream) != hipSuccess) return fail(MPPI_E_HIP, "stream synchronize");
+    return check_tmo(c);
+}
+
+int mppi_chain_debug_set_buffer(mppi_chain_ctx* c, void* dbg_dev) {
+    if (!c) return fail(MPPI_E_ARG, "null context");
+    c->d_dbg = (unsigned long long*)dbg_dev;
+    return MPPI_OK;
+}
+
+}  // extern "C"

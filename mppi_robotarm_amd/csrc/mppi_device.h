@@ -1,0 +1,683 @@
+// mppi_device.h — device building blocks shared by the MPPI kernels for gfx950
+// (mppi_rocm.hip: the reference's 2-link arm; mppi_chain.hip: the n-link chain
+// of BASELINE config 5): DPP wave reductions, the window search, write-through
+// row buffers and tagged granules, the in-launch log-sum-exp merges of the
+// workgroup partial rows, the median-of-10 network, Philox.
+//
+// A partial row is {rho, eta, N[nval]} (control.py:112-118 over some set of
+// samples in log-sum-exp form: rho = min S, eta = sum e^{-(S - rho)/lambda},
+// N = sum e^{-(S - rho)/lambda} eps), nval = T * du values.  The merges read
+// rows handed over by other workgroups of the same launch (MI355X guide,
+// Guideline 16): 8-B sc1 words behind an arrival counter, or 16-B tagged
+// granules polled without any counter.
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+#include <math.h>
+#include <stdint.h>
+
+#include <type_traits>
+#include <utility>
+
+#include "mppi_rocm.h"  // MPPI_SEARCH_LEN, MPPI_MAX_T
+
+namespace mppi {
+
+constexpr int kMaxT = MPPI_MAX_T;
+
+constexpr int kSlots = 32;             // window slots (>= MPPI_SEARCH_LEN), index fits 5 bits
+constexpr float kPadKey = 1.0e30f;
+constexpr int kMaxWaves = 16;          // up to 1024-thread workgroups
+constexpr int kGroup = 16;             // workgroups per first-level merge group
+// A partial whose rescale factor s = exp((rho - rho_i) / lambda) is below 2^-64
+// changes eta and N by less than 2^-64 * 512 relative to the leading term
+// (which has s = 1 and eta >= 1): far below the fp64 resolution of the result.
+constexpr double kMergeFloor = 5.421010862427522e-20;  // 2^-64
+constexpr int kDirectRows = 256;       // workgroup rows the direct merge scans (4 per lane)
+constexpr int kDirectMax = 16;         // weighted rows it merges; more go through the group rows
+constexpr int kSparseMax = 16;         // weighted samples per workgroup handled by the epilogue gather
+
+// ------------------------------------------------------------------ helpers
+
+// Hardware v_sin_f32 / v_cos_f32 (argument pre-scaled by 1/(2 pi)): 30 % faster
+// rollouts than OCML's sincosf at K=65536 T=64, parity unchanged (S rel-err
+// budget 5e-5 in tests/test_gpu_parity.py).  -DMPPI_ACCURATE_TRIG selects sincosf.
+__device__ __forceinline__ void sincos_f32(float x, float* s, float* c) {
+#ifdef MPPI_ACCURATE_TRIG
+    sincosf(x, s, c);
+#else
+    __sincosf(x, s, c);
+#endif
+}
+
+template <int CTRL>
+__device__ __forceinline__ float dpp_f32(float v) {
+    return __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), CTRL, 0xF, 0xF, false));
+}
+
+__device__ __forceinline__ int lanes_below(unsigned long long mask) {
+    return __builtin_amdgcn_mbcnt_hi((unsigned)(mask >> 32), __builtin_amdgcn_mbcnt_lo((unsigned)mask, 0u));
+}
+
+template <int CTRL>
+__device__ __forceinline__ double dpp_f64(double v) {
+    const long long b = __double_as_longlong(v);
+    const int lo = __builtin_amdgcn_mov_dpp((int)b, CTRL, 0xF, 0xF, false);
+    const int hi = __builtin_amdgcn_mov_dpp((int)(b >> 32), CTRL, 0xF, 0xF, false);
+    return __longlong_as_double(((long long)hi << 32) | (unsigned)lo);
+}
+
+// v from lane l as a wave-uniform (scalar) value
+__device__ __forceinline__ double readlane_f64(double v, int l) {
+    const long long b = __double_as_longlong(v);
+    const int lo = __builtin_amdgcn_readlane((int)b, l);
+    const int hi = __builtin_amdgcn_readlane((int)(b >> 32), l);
+    return __longlong_as_double(((long long)hi << 32) | (unsigned)lo);
+}
+__device__ __forceinline__ float readlane_f32(float v, int l) {
+    return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), l));
+}
+
+// Whole-wave reductions (all 64 lanes active), result wave-uniform: DPP
+// quad_perm xor 1 / xor 2, row_half_mirror, row_mirror reduce each row of 16
+// in registers, then the four row results are combined from v_readlane — no
+// LDS round trips (a ds_bpermute butterfly costs six of them).  The combine
+// order is fixed, so sums are deterministic.
+template <class T, class Op>
+__device__ __forceinline__ T wave_reduce(T v, Op op) {
+    if constexpr (sizeof(T) == 8) {
+        v = op(v, dpp_f64<0xB1>(v));
+        v = op(v, dpp_f64<0x4E>(v));
+        v = op(v, dpp_f64<0x141>(v));
+        v = op(v, dpp_f64<0x140>(v));
+        return op(op(readlane_f64(v, 0), readlane_f64(v, 16)), op(readlane_f64(v, 32), readlane_f64(v, 48)));
+    } else {
+        v = op(v, dpp_f32<0xB1>(v));
+        v = op(v, dpp_f32<0x4E>(v));
+        v = op(v, dpp_f32<0x141>(v));
+        v = op(v, dpp_f32<0x140>(v));
+        return op(op(readlane_f32(v, 0), readlane_f32(v, 16)), op(readlane_f32(v, 32), readlane_f32(v, 48)));
+    }
+}
+struct OpMin {
+    __device__ double operator()(double a, double b) const { return fmin(a, b); }
+};
+struct OpAdd {
+    template <class T>
+    __device__ T operator()(T a, T b) const { return a + b; }
+};
+__device__ __forceinline__ double wave_min_f64(double v) { return wave_reduce(v, OpMin{}); }
+__device__ __forceinline__ double wave_sum_f64(double v) { return wave_reduce(v, OpAdd{}); }
+__device__ __forceinline__ float wave_sum_f32(float v) { return wave_reduce(v, OpAdd{}); }
+
+// The k-th (0-based) set bit of m; k < popcount(m).
+__device__ __forceinline__ int select_bit(unsigned long long m, int k) {
+    int pos = 0;
+#pragma unroll
+    for (int w = 32; w > 0; w >>= 1) {
+        const int cnt = __popcll(m & ((1ull << w) - 1));
+        if (k >= cnt) {
+            k -= cnt;
+            m >>= w;
+            pos += w;
+        }
+    }
+    return pos;
+}
+
+template <class F, int... I>
+__device__ __forceinline__ void unroll_seq(F&& f, std::integer_sequence<int, I...>) {
+    (f(std::integral_constant<int, I>{}), ...);
+}
+
+// Scheduling boundary after each prefetch: an empty asm statement with a
+// memory clobber keeps the load where it is written (otherwise the scheduler
+// sinks it next to its use and every step pays the full memory latency).
+#define PIN_LOADS() asm volatile("" ::: "memory")
+
+// The per-step constants are read through the constant address space: scalar
+// (SMEM) loads that stay scalar across the scheduling boundaries above.  Their
+// block is written only by host copies or by the PREVIOUS launch (ping-pong).
+typedef __attribute__((address_space(4))) const float cfloat;
+__device__ __forceinline__ float4 const_ld4(cfloat* p) { return make_float4(p[0], p[1], p[2], p[3]); }
+
+typedef float f32x2 __attribute__((ext_vector_type(2)));
+
+// v_min3_f32 / v_min_f32 issued directly: the operands are bit-packed keys, and
+// fminf() would make hipcc canonicalise every one of them (v_max x, x) first.
+__device__ __forceinline__ float min3_raw(float a, float b, float c) {
+    float r;
+    asm("v_min3_f32 %0, %1, %2, %3" : "=v"(r) : "v"(a), "v"(b), "v"(c));
+    return r;
+}
+__device__ __forceinline__ float min_raw(float a, float b) {
+    float r;
+    asm("v_min_f32 %0, %1, %2" : "=v"(r) : "v"(a), "v"(b));
+    return r;
+}
+
+// ------------------------------------------------------------ window search
+
+// Nearest waypoint of the shared window (control.py:200-232): the window is
+// uploaded as centred keys (rx', ry', rx'^2 + ry'^2; pads 1e30), and
+//   argmin_j |p - r_j|^2 = argmin_j (|r'_j|^2 - 2 p'.r'_j),
+// two slots per v_pk_fma_f32; the slot index is packed into the 5 low mantissa
+// bits so one v_min3 per two slots carries the argmin (first occurrence: equal
+// keys resolve to the lower slot); the LPS lanes of a sample split the window
+// and close the min with DPP.
+template <int LPS>
+struct Search {
+    static constexpr int SL = ((MPPI_SEARCH_LEN + LPS - 1) / LPS + 1) & ~1;  // slots per lane, even
+    static constexpr int SP = SL / 2;
+    f32x2 krx[SP], kry[SP], kc[SP];
+    int sub;
+    float cx, cy;
+
+    // key: the centred keys (kSlots float4), ctr: the window centre
+    __device__ __forceinline__ void load(const float4* key, float4 ctr, int lane_sub) {
+        static_assert(SL * LPS <= kSlots, "window slots");
+        if (LPS == 1) {
+            // lane-opaque zero: keeps the 30 window slots in VGPRs (as uniform
+            // values they would go to SGPRs and spill)
+            int z;
+            asm volatile("v_mov_b32 %0, 0" : "=v"(z));
+            sub = z;
+        } else {
+            sub = lane_sub;
+        }
+#pragma unroll
+        for (int i = 0; i < SP; ++i) {
+            const float4 k0 = key[sub * SL + 2 * i];
+            const float4 k1 = key[sub * SL + 2 * i + 1];
+            krx[i] = f32x2{k0.x, k1.x};
+            kry[i] = f32x2{k0.y, k1.y};
+            kc[i] = f32x2{k0.z, k1.z};
+        }
+        cx = ctr.x;
+        cy = ctr.y;
+    }
+
+    __device__ __forceinline__ unsigned nearest(float px, float py) const {
+        const float ax = -2.f * (px - cx), ay = -2.f * (py - cy);
+        const f32x2 ax2 = {ax, ax}, ay2 = {ay, ay};
+        float best = 3.0e38f;
+#pragma unroll
+        for (int i = 0; i < SP; ++i) {
+            const f32x2 key = __builtin_elementwise_fma(ax2, krx[i], __builtin_elementwise_fma(ay2, kry[i], kc[i]));
+            const unsigned j = (unsigned)(sub * SL + 2 * i);
+            const float k0 = __uint_as_float((__float_as_uint(key.x) & ~31u) | j);
+            const float k1 = __uint_as_float((__float_as_uint(key.y) & ~31u) | (j + 1));
+            best = min3_raw(best, k0, k1);
+        }
+        if (LPS >= 2) best = min_raw(best, dpp_f32<0xB1>(best));  // quad_perm xor 1
+        if (LPS >= 4) best = min_raw(best, dpp_f32<0x4E>(best));  // quad_perm xor 2
+        return __float_as_uint(best) & 31u;
+    }
+};
+
+// stage / terminal cost terms (control.py:185-198, weights x 10000 folded in)
+__device__ __forceinline__ float weighted_sq(float ex, float ey, float e1, float e2, const float* w) {
+    return fmaf(w[0], ex * ex, fmaf(w[1], ey * ey, fmaf(w[2], e1 * e1, w[3] * e2 * e2)));
+}
+
+// ------------------------------------------------ rows handed between workgroups
+
+// Rows {rho, eta, N} handed between workgroups of one launch travel
+// write-through: every store and every load of them is a `sc1` buffer access
+// (MI355X guide G16, "Valid forms" row 1), so neither side needs an agent-scope
+// fence (~1.7 us each).
+typedef unsigned int u32x2 __attribute__((__vector_size__(2 * sizeof(unsigned int))));
+typedef unsigned int u32x4 __attribute__((__vector_size__(4 * sizeof(unsigned int))));
+constexpr int kSC1 = 16;  // buffer aux bit: sc1
+
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t rows_rsrc(const void* p, int bytes) {
+    return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(p), 0, bytes, 0x00020000);
+}
+__device__ __forceinline__ double ld_wt(__amdgpu_buffer_rsrc_t r, int idx) {
+    return __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(r, idx * 8, 0, kSC1));
+}
+__device__ __forceinline__ void st_wt(__amdgpu_buffer_rsrc_t r, int idx, double v) {
+    __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u32x2, v), r, idx * 8, 0, kSC1);
+}
+// Element index past every rows buffer: a raw buffer load beyond num_records
+// returns 0 without a memory access, so a predicated-off load needs no branch
+// (a branch around each load makes the compiler wait for it at the join).
+constexpr int kOffRange = 1 << 26;  // x 16 B = 1 GiB > any rows buffer, no int overflow
+
+// Tagged granules (MI355X guide, Guideline 16 R2: "the data IS the flag").  One
+// fp64 value travels as {lo32, tag, hi32, tag} in ONE 16-B sc1 store; each 8-B
+// half is a naturally aligned {value, tag} granule, so a reader that sees both
+// tags equal to this launch's epoch holds the whole value — no drain, no flag,
+// no counter.  Tags come from a device-resident epoch (never a kernel argument:
+// graph replay freezes those), zeroed once at context creation.
+__device__ __forceinline__ void st_gran(__amdgpu_buffer_rsrc_t r, int idx, double v, unsigned tag) {
+    const unsigned long long b = (unsigned long long)__double_as_longlong(v);
+    const u32x4 x = {(unsigned)b, tag, (unsigned)(b >> 32), tag};
+    __builtin_amdgcn_raw_buffer_store_b128(x, r, idx * 16, 0, kSC1);
+}
+// Poll loads are plain sc1 loads; every spin loop opens with an empty asm
+// memory clobber so the loads are re-issued each pass (without it LLVM hoists
+// the read-only loads out of the loop — nothing else in it writes memory — and
+// polls registers).
+__device__ __forceinline__ u32x4 ld_gran(__amdgpu_buffer_rsrc_t r, int idx) {
+    return __builtin_amdgcn_raw_buffer_load_b128(r, idx * 16, 0, kSC1);
+}
+__device__ __forceinline__ bool gran_ok(u32x4 x, unsigned tag) { return x[1] == tag && x[3] == tag; }
+__device__ __forceinline__ double gran_val(u32x4 x) {
+    return __longlong_as_double((long long)(((unsigned long long)x[2] << 32) | x[0]));
+}
+// Bounded spins: ~1 s of polling, then the hand-off reports a timeout (host
+// error word) instead of hanging the GPU; results of that launch are invalid.
+constexpr unsigned kSpinMax = 1u << 20;
+__device__ __forceinline__ void report_timeout(unsigned* tmo) {
+    if (tmo) __hip_atomic_store(tmo, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+#define MPPI_SPIN_OR_GIVE_UP(spins, tmo, lane)        \
+    if (spins >= kSpinMax) {                          \
+        if ((lane) == 0) report_timeout(tmo);         \
+        break;                                        \
+    }                                                 \
+    __builtin_amdgcn_s_sleep(1)
+
+// ------------------------------------------------------------ merge scratch
+
+template <int MAXV>
+struct MergeScratch {
+    double red[kMaxWaves];
+    double weps[MAXV];
+    double unew[MAXV];
+    int nrel;
+};
+
+// Workgroup minimum.  One use per kernel: the caller's next barrier protects
+// sm.red before any reuse.
+template <int NT, class SM>
+__device__ __forceinline__ double block_min_f64(double v, SM& sm) {
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    v = wave_min_f64(v);
+    if (lane == 0) sm.red[wave] = v;
+    __syncthreads();
+    double r = sm.red[0];
+#pragma unroll
+    for (int w = 1; w < NT / 64; ++w) r = fmin(r, sm.red[w]);
+    return r;
+}
+
+// Geometry of a partial row {rho, eta, N[nval]}: stride values, merged columns
+// (col 0 = eta, 1 + j = N[j]).  Thread tid owns columns tid + ch * NT, ch < MAXCH.
+struct RowGeo {
+    int stride, ncol;
+    __device__ explicit RowGeo(int nval) : stride(2 + nval), ncol(1 + nval) {}
+};
+
+// Final merged row: {rho, eta, N} to out_row (plain, read after the launch) and
+// w_eps = N / eta (control.py:112-118) to sm.weps and w_eps_out.
+template <int NT, int MAXCH, class SM>
+__device__ __forceinline__ void put_final(double rho, const double (&acc)[MAXCH], double eta, int nrel,
+                                          const RowGeo& geo, SM& sm, double* out_row, double* w_eps_out) {
+    const int tid = threadIdx.x;
+#pragma unroll
+    for (int ch = 0; ch < MAXCH; ++ch) {
+        const int col = tid + ch * NT;
+        if (col >= geo.ncol) continue;
+        if (col == 0) {
+            sm.nrel = nrel;
+            if (out_row) {
+                out_row[0] = rho;
+                out_row[1] = acc[ch];
+            }
+        } else {
+            if (out_row) out_row[1 + col] = acc[ch];
+            const double w = acc[ch] / eta;
+            sm.weps[col - 1] = w;
+            if (w_eps_out) w_eps_out[col - 1] = w;
+        }
+    }
+    __syncthreads();
+}
+
+// Merge n rows (read write-through from `rows`, rows row0 .. row0 + n - 1) with
+// a log-sum-exp rescale: rho = min rho_i, s_i = exp((rho - rho_i) / lambda),
+// eta = sum s_i eta_i, N = sum s_i N_i, in ascending row order (deterministic);
+// rows whose factor is below 2^-64 of the running best are skipped.  Rows go in
+// rounds with an online rescale of the running sums when a round lowers rho.
+// Wave-local: every wave reads the round's rho_i into its lanes, reduces them
+// with DPP and evaluates the s_i itself; the s_i reach the column FMAs as
+// scalars (v_readlane) — no LDS traffic and no barrier per round.
+//
+// !GRAN: 8-B sc1 words behind an arrival counter; every load of a round —
+//   rho, eta and all (row, column chunk) entries — is issued together (one
+//   memory round trip per round of 32 / MAXCH rows).
+// GRAN: 16-B tagged granules polled until every tag matches `tag`: rho first,
+//   one lane per row (16 rows per round), then eta and the entries of only the
+//   rows that carry weight, 16 / MAXCH rows per load batch.
+// The merged row goes to out_wt (same format, next level) or, with `final`,
+// to put_final.
+template <int NT, int MAXCH, bool final, bool GRAN, class SM>
+__device__ __forceinline__ void merge_rows_block(__amdgpu_buffer_rsrc_t rows, int row0, int n, const RowGeo& geo,
+                                                 double inv_lambda, SM& sm, const __amdgpu_buffer_rsrc_t* out_wt,
+                                                 int out_idx, double* out_row, double* w_eps_out, unsigned tag,
+                                                 unsigned* tmo) {
+    constexpr int LB = GRAN ? 16 : 32;          // loads per batch per thread
+    constexpr int RB = LB / MAXCH;              // rows per load batch
+    constexpr int R1 = GRAN ? 16 : RB;          // rows per round
+    static_assert(RB >= 1 && R1 <= 64, "one row per lane");
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int stride = geo.stride, ncol = geo.ncol;
+    double acc[MAXCH], eta = 0.0, rho = INFINITY;
+#pragma unroll
+    for (int ch = 0; ch < MAXCH; ++ch) acc[ch] = 0.0;
+    int nrel = 0;
+    for (int r0 = 0; r0 < n; r0 += R1) {
+        const int nr = min(R1, n - r0);   // uniform
+        const int rb = row0 + r0;
+        const int lrow = lane < nr ? (rb + lane) * stride : kOffRange;
+        double rho_r, eta_l = 0.0, v[GRAN ? 1 : LB];
+        if constexpr (GRAN) {
+            u32x4 gr;
+            for (unsigned spins = 0;; ++spins) {
+                asm volatile("" ::: "memory");
+                gr = ld_gran(rows, lrow);
+                if (__all(lane >= nr || gran_ok(gr, tag))) break;
+                MPPI_SPIN_OR_GIVE_UP(spins, tmo, lane);
+            }
+            rho_r = gran_val(gr);
+        } else {
+            rho_r = ld_wt(rows, lrow);
+            eta_l = ld_wt(rows, lrow + 1);
+#pragma unroll
+            for (int j = 0; j < LB; ++j) {
+                const int i = j / MAXCH, col = tid + (j % MAXCH) * NT;
+                v[j] = ld_wt(rows, (i < nr && col < ncol) ? (rb + i) * stride + 1 + col : kOffRange);
+            }
+        }
+        const double rho_l = lane < nr ? rho_r : INFINITY;
+        const double rnew = fmin(rho, wave_min_f64(rho_l));
+        double s_l = 0.0;
+        if (lane < nr) {
+            const double s = exp((rnew - rho_l) * inv_lambda);
+            s_l = s >= kMergeFloor ? s : 0.0;
+        }
+        const unsigned long long rel = __ballot(s_l != 0.0);   // rows that carry weight (uniform)
+        const int nrr = __popcll(rel);
+        nrel += nrr;
+        if (rnew < rho && rho != INFINITY) {  // uniform: rescale the running sums to the new minimum
+            const double f = exp((rnew - rho) * inv_lambda);
+#pragma unroll
+            for (int ch = 0; ch < MAXCH; ++ch) acc[ch] *= f;
+            eta *= f;
+        }
+        rho = rnew;
+        if constexpr (!GRAN) {
+#pragma unroll
+            for (int j = 0; j < LB; ++j) {
+                const int i = j / MAXCH, ch = j % MAXCH;
+                if (i < nr) {
+                    const double s = readlane_f64(s_l, i);
+                    if (s != 0.0) {
+                        acc[ch] = fma(s, v[j], acc[ch]);
+                        if (ch == 0) eta = fma(s, readlane_f64(eta_l, i), eta);
+                    }
+                }
+            }
+        } else {
+            // lane k < nrr: the round's k-th weighted row (ascending)
+            const int krow = lane < nrr ? select_bit(rel, lane) : 0;
+            for (int b0 = 0; b0 < nrr; b0 += RB) {
+                u32x4 ge, gv[LB];
+                for (unsigned spins = 0;; ++spins) {
+                    asm volatile("" ::: "memory");
+                    ge = ld_gran(rows, (b0 == 0 && lane < nrr) ? (rb + krow) * stride + 1 : kOffRange);
+                    bool ok = !(b0 == 0 && lane < nrr) || gran_ok(ge, tag);
+#pragma unroll
+                    for (int j = 0; j < LB; ++j) {
+                        const int i = b0 + j / MAXCH, col = tid + (j % MAXCH) * NT;
+                        const bool on = i < nrr && col < ncol;
+                        gv[j] = ld_gran(rows, on ? (rb + __builtin_amdgcn_readlane(krow, i)) * stride + 1 + col
+                                                 : kOffRange);
+                        ok = ok && (!on || gran_ok(gv[j], tag));
+                    }
+                    if (__all(ok)) break;
+                    MPPI_SPIN_OR_GIVE_UP(spins, tmo, lane);
+                }
+                if (b0 == 0) eta_l = gran_val(ge);
+#pragma unroll
+                for (int j = 0; j < LB; ++j) {
+                    const int i = b0 + j / MAXCH, ch = j % MAXCH;
+                    if (i < nrr) {
+                        const double s = readlane_f64(s_l, __builtin_amdgcn_readlane(krow, i));
+                        acc[ch] = fma(s, gran_val(gv[j]), acc[ch]);
+                        if (ch == 0) eta = fma(s, readlane_f64(eta_l, i), eta);
+                    }
+                }
+            }
+        }
+    }
+    if constexpr (final) {
+        put_final<NT, MAXCH>(rho, acc, eta, nrel, geo, sm, out_row, w_eps_out);
+    } else {
+        auto put = [&](int col, double x) {  // col 0 = rho, 1 = eta, 2 + j = N[j]
+            if constexpr (GRAN) st_gran(*out_wt, out_idx * stride + col, x, tag);
+            else st_wt(*out_wt, out_idx * stride + col, x);
+        };
+#pragma unroll
+        for (int ch = 0; ch < MAXCH; ++ch) {
+            const int col = tid + ch * NT;
+            if (col >= ncol) continue;
+            if (col == 0) put(0, rho);
+            put(1 + col, acc[ch]);
+        }
+    }
+}
+
+// Single-level finish for the usual regime (few weighted rows, S spread >> lambda):
+// read rho of EVERY workgroup row (n <= kDirectRows), and when at most
+// kDirectMax rows carry weight relative to the global minimum, merge exactly
+// those rows in ascending order straight from the workgroup slab — one hand-off
+// on the critical path instead of two.  Returns false (uniformly) when more rows
+// carry weight; the caller then merges through the group rows.  Wave-local
+// like merge_rows_block; the result goes out as in a final merge.
+template <int NT, int MAXCH, bool GRAN, class SM>
+__device__ __forceinline__ bool direct_merge(__amdgpu_buffer_rsrc_t rows, int n, const RowGeo& geo,
+                                             double inv_lambda, SM& sm, double* out_row, double* w_eps_out,
+                                             unsigned tag, unsigned* tmo) {
+    constexpr int P = kDirectRows / 64;
+    constexpr int LB = 16;                      // loads per batch per thread
+    constexpr int RB = LB / MAXCH;              // rows per load batch
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int stride = geo.stride, ncol = geo.ncol;
+    // phase 1: rho of row lane + 64 j in slot j
+    double rho_l[P];
+    if constexpr (GRAN) {
+        u32x4 gr[P];
+        for (unsigned spins = 0;; ++spins) {
+            asm volatile("" ::: "memory");
+            bool ok = true;
+#pragma unroll
+            for (int j = 0; j < P; ++j) {
+                const int r = lane + 64 * j;
+                gr[j] = ld_gran(rows, r < n ? r * stride : kOffRange);
+                ok = ok && (r >= n || gran_ok(gr[j], tag));
+            }
+            if (__all(ok)) break;
+            MPPI_SPIN_OR_GIVE_UP(spins, tmo, lane);
+        }
+#pragma unroll
+        for (int j = 0; j < P; ++j) rho_l[j] = lane + 64 * j < n ? gran_val(gr[j]) : INFINITY;
+    } else {
+#pragma unroll
+        for (int j = 0; j < P; ++j) {
+            const int r = lane + 64 * j;
+            const double x = ld_wt(rows, r < n ? r * stride : kOffRange);
+            rho_l[j] = r < n ? x : INFINITY;
+        }
+    }
+    double m = rho_l[0];
+#pragma unroll
+    for (int j = 1; j < P; ++j) m = fmin(m, rho_l[j]);
+    const double rho = wave_min_f64(m);
+    double s_l[P];
+    unsigned long long rel[P];
+    int nrel = 0;
+#pragma unroll
+    for (int j = 0; j < P; ++j) {
+        const double s = exp((rho - rho_l[j]) * inv_lambda);
+        s_l[j] = (lane + 64 * j < n && s >= kMergeFloor) ? s : 0.0;
+        rel[j] = __ballot(s_l[j] != 0.0);
+        nrel += __popcll(rel[j]);
+    }
+    if (nrel > kDirectMax) return false;
+    // lane k < nrel: the k-th weighted row (ascending) and its factor
+    int k = lane, row = 0;
+    bool found = false;
+#pragma unroll
+    for (int j = 0; j < P; ++j) {
+        const int cnt = __popcll(rel[j]);
+        if (!found && k < cnt) {
+            row = 64 * j + select_bit(rel[j], k);
+            found = true;
+        } else if (!found) {
+            k -= cnt;
+        }
+    }
+    double sk = 0.0;
+#pragma unroll
+    for (int j = 0; j < P; ++j) {
+        const double sj = __shfl(s_l[j], row & 63);
+        if ((row >> 6) == j) sk = sj;
+    }
+    const bool mine = lane < nrel;
+    // phase 2: eta and the (row, column chunk) entries of the weighted rows
+    double acc[MAXCH], eta = 0.0, eta_k = 0.0;
+#pragma unroll
+    for (int ch = 0; ch < MAXCH; ++ch) acc[ch] = 0.0;
+    for (int b0 = 0; b0 < nrel; b0 += RB) {
+        double v[LB];
+        if constexpr (GRAN) {
+            u32x4 ge, gv[LB];
+            for (unsigned spins = 0;; ++spins) {
+                asm volatile("" ::: "memory");
+                ge = ld_gran(rows, (b0 == 0 && mine) ? row * stride + 1 : kOffRange);
+                bool ok = !(b0 == 0 && mine) || gran_ok(ge, tag);
+#pragma unroll
+                for (int j = 0; j < LB; ++j) {
+                    const int i = b0 + j / MAXCH, col = tid + (j % MAXCH) * NT;
+                    const bool on = i < nrel && col < ncol;
+                    gv[j] = ld_gran(rows, on ? __builtin_amdgcn_readlane(row, i) * stride + 1 + col : kOffRange);
+                    ok = ok && (!on || gran_ok(gv[j], tag));
+                }
+                if (__all(ok)) break;
+                MPPI_SPIN_OR_GIVE_UP(spins, tmo, lane);
+            }
+            if (b0 == 0) eta_k = gran_val(ge);
+#pragma unroll
+            for (int j = 0; j < LB; ++j) v[j] = gran_val(gv[j]);
+        } else {
+            if (b0 == 0) eta_k = ld_wt(rows, mine ? row * stride + 1 : kOffRange);
+#pragma unroll
+            for (int j = 0; j < LB; ++j) {
+                const int i = b0 + j / MAXCH, col = tid + (j % MAXCH) * NT;
+                v[j] = ld_wt(rows, (i < nrel && col < ncol) ? __builtin_amdgcn_readlane(row, i) * stride + 1 + col
+                                                             : kOffRange);
+            }
+        }
+#pragma unroll
+        for (int j = 0; j < LB; ++j) {
+            const int i = b0 + j / MAXCH, ch = j % MAXCH;
+            if (i < nrel) {
+                const double s = readlane_f64(sk, i);
+                acc[ch] = fma(s, v[j], acc[ch]);
+                if (ch == 0) eta = fma(s, readlane_f64(eta_k, i), eta);
+            }
+        }
+    }
+    put_final<NT, MAXCH>(rho, acc, eta, nrel, geo, sm, out_row, w_eps_out);
+    return true;
+}
+
+// Arrive on `counter` after this workgroup's write-through stores; true in
+// every thread of the workgroup that arrived last (which re-arms the counter).
+// sc1 loads alone stand in for the acquire only at one workgroup per CU (the
+// measured form, MI355X guide "Valid forms"); with `acquire` (larger grids)
+// the last arriver also runs an agent-scope acquire before the barrier.
+__device__ __forceinline__ bool arrive_last(unsigned* counter, unsigned expected, unsigned* s_flag, bool acquire) {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every storing wave drains its sc1 stores
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        const unsigned prev = __hip_atomic_fetch_add(counter, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        const bool last = prev == expected - 1;
+        if (last) __hip_atomic_store(counter, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (last && acquire) {
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        }
+        *s_flag = last ? 1u : 0u;
+    }
+    __syncthreads();
+    return *s_flag != 0;
+}
+
+// Upper median of 10 (rank 5): a 29-comparator sorting network (verified on all
+// 2^10 0/1 inputs), the element scipy.ndimage.median_filter(size=10) returns.
+__device__ __forceinline__ double median10(double* v) {
+#define CX(i, j) { const double lo = fmin(v[i], v[j]), hi = fmax(v[i], v[j]); v[i] = lo; v[j] = hi; }
+    CX(4, 9) CX(3, 8) CX(2, 7) CX(1, 6) CX(0, 5) CX(1, 4) CX(6, 9) CX(0, 3) CX(5, 8) CX(0, 2)
+    CX(3, 6) CX(7, 9) CX(0, 1) CX(2, 4) CX(5, 7) CX(8, 9) CX(1, 2) CX(4, 6) CX(7, 8) CX(3, 5)
+    CX(2, 5) CX(6, 8) CX(1, 3) CX(4, 7) CX(2, 3) CX(6, 7) CX(3, 4) CX(5, 6) CX(4, 5)
+#undef CX
+    return v[5];
+}
+
+// scipy.ndimage.median_filter(size=10, mode='reflect') of column d of the
+// T x du array sm.weps at row t (control.py:319-327, window [t-5, t+4]; one
+// reflection suffices for T >= 5).
+template <class SM>
+__device__ __forceinline__ double median_at(const SM& sm, int t, int d, int T, int du) {
+    double v[10];
+#pragma unroll
+    for (int i = 0; i < 10; ++i) {
+        int m = t - 5 + i;
+        m = m < 0 ? -m - 1 : m;
+        m = m >= T ? 2 * T - 1 - m : m;
+        v[i] = sm.weps[m * du + d];
+    }
+    return median10(v);
+}
+
+// ------------------------------------------------------------------ Philox
+
+// Philox4x32-10 (Salmon et al., SC'11).
+__device__ __forceinline__ uint4 philox4x32_10(uint4 ctr, uint2 key) {
+#pragma unroll
+    for (int r = 0; r < 10; ++r) {
+        const unsigned lo0 = 0xD2511F53u * ctr.x, hi0 = __umulhi(0xD2511F53u, ctr.x);
+        const unsigned lo1 = 0xCD9E8D57u * ctr.z, hi1 = __umulhi(0xCD9E8D57u, ctr.z);
+        ctr = make_uint4(hi1 ^ ctr.y ^ key.x, lo1, hi0 ^ ctr.w ^ key.y, lo0);
+        key.x += 0x9E3779B9u;
+        key.y += 0xBB67AE85u;
+    }
+    return ctr;
+}
+
+// Two standard normals from two 32-bit uniforms (Box-Muller).
+__device__ __forceinline__ float2 box_muller(unsigned a, unsigned b) {
+    const float inv = 2.3283064365386963e-10f;  // 2^-32
+    const float u0 = ((float)a + 1.0f) * inv, u1 = (float)b * inv;
+    float s, c;
+    const float r = sqrtf(-2.0f * logf(fminf(u0, 1.0f)));
+    sincospif(2.0f * u1, &s, &c);
+    return make_float2(r * c, r * s);
+}
+
+}  // namespace mppi
+
+// Diagnostic builds only (-DMPPI_STAMPS, a separate .so): per-workgroup
+// timeline in s_memrealtime ticks (100 MHz) + counters.  Never in the product.
+#ifdef MPPI_STAMPS
+#define STAMP(slot, val) do { if (dbg && threadIdx.x == 0) dbg[(size_t)blockIdx.x * 16 + (slot)] = (val); } while (0)
+#define NOW() __builtin_amdgcn_s_memrealtime()
+#else
+#define STAMP(slot, val) do { (void)dbg; } while (0)
+#define NOW() 0ull
+#endif

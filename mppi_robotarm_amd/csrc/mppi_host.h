@@ -1,0 +1,12 @@
+// mppi_host.h — host-side helpers shared by the translation units of
+// libmppi_rocm.so (one error channel behind mppi_last_error()).
+#pragma once
+
+#include <string>
+
+namespace mppi_host {
+
+// Records msg as this thread's last error (mppi_last_error) and returns code.
+int fail(int code, const std::string& msg);
+
+}  // namespace mppi_host

@@ -36,14 +36,15 @@
 #include <string>
 #include <type_traits>
 
+#include "mppi_device.h"
+#include "mppi_host.h"
 #include "mppi_rocm.h"
 
 namespace {
 
+using namespace mppi;
+
 constexpr int kThreads = 256;
-constexpr int kMaxT = MPPI_MAX_T;
-constexpr int kSlots = 32;  // window slots (>= MPPI_SEARCH_LEN), index fits 5 bits
-constexpr float kPadKey = 1.0e30f;
 
 // Device-resident per-step parameter block (ping-pong pair in the context).
 struct alignas(16) DevStep {
@@ -64,77 +65,6 @@ struct KConst {
     double lambda, inv_lambda, gamma;
     double sig_inv[4];
 };
-
-// ------------------------------------------------------------------ helpers
-
-// Hardware v_sin_f32 / v_cos_f32 (argument pre-scaled by 1/(2 pi)): 30 % faster
-// rollouts than OCML's sincosf at K=65536 T=64, parity unchanged (S rel-err
-// budget 5e-5 in tests/test_gpu_parity.py).  -DMPPI_ACCURATE_TRIG selects sincosf.
-__device__ __forceinline__ void sincos_f32(float x, float* s, float* c) {
-#ifdef MPPI_ACCURATE_TRIG
-    sincosf(x, s, c);
-#else
-    __sincosf(x, s, c);
-#endif
-}
-
-template <int CTRL>
-__device__ __forceinline__ float dpp_f32(float v) {
-    return __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), CTRL, 0xF, 0xF, false));
-}
-
-__device__ __forceinline__ int lanes_below(unsigned long long mask) {
-    return __builtin_amdgcn_mbcnt_hi((unsigned)(mask >> 32),
-                                     __builtin_amdgcn_mbcnt_lo((unsigned)mask, 0u));
-}
-
-template <int CTRL>
-__device__ __forceinline__ double dpp_f64(double v) {
-    const long long b = __double_as_longlong(v);
-    const int lo = __builtin_amdgcn_mov_dpp((int)b, CTRL, 0xF, 0xF, false);
-    const int hi = __builtin_amdgcn_mov_dpp((int)(b >> 32), CTRL, 0xF, 0xF, false);
-    return __longlong_as_double(((long long)hi << 32) | (unsigned)lo);
-}
-
-// v from lane l as a wave-uniform (scalar) value
-__device__ __forceinline__ double readlane_f64(double v, int l) {
-    const long long b = __double_as_longlong(v);
-    const int lo = __builtin_amdgcn_readlane((int)b, l);
-    const int hi = __builtin_amdgcn_readlane((int)(b >> 32), l);
-    return __longlong_as_double(((long long)hi << 32) | (unsigned)lo);
-}
-__device__ __forceinline__ float readlane_f32(float v, int l) {
-    return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), l));
-}
-
-// Whole-wave reductions (all 64 lanes active), result wave-uniform: DPP
-// quad_perm xor 1 / xor 2, row_half_mirror, row_mirror reduce each row of 16
-// in registers, then the four row results are combined from v_readlane — no
-// LDS round trips (a ds_bpermute butterfly costs six of them).  The combine
-// order is fixed, so sums are deterministic.
-template <class T, class Op>
-__device__ __forceinline__ T wave_reduce(T v, Op op) {
-    if constexpr (sizeof(T) == 8) {
-        v = op(v, dpp_f64<0xB1>(v));
-        v = op(v, dpp_f64<0x4E>(v));
-        v = op(v, dpp_f64<0x141>(v));
-        v = op(v, dpp_f64<0x140>(v));
-        return op(op(readlane_f64(v, 0), readlane_f64(v, 16)), op(readlane_f64(v, 32), readlane_f64(v, 48)));
-    } else {
-        v = op(v, dpp_f32<0xB1>(v));
-        v = op(v, dpp_f32<0x4E>(v));
-        v = op(v, dpp_f32<0x141>(v));
-        v = op(v, dpp_f32<0x140>(v));
-        return op(op(readlane_f32(v, 0), readlane_f32(v, 16)), op(readlane_f32(v, 32), readlane_f32(v, 48)));
-    }
-}
-struct OpMin { __device__ double operator()(double a, double b) const { return fmin(a, b); } };
-struct OpAdd {
-    template <class T> __device__ T operator()(T a, T b) const { return a + b; }
-};
-__device__ __forceinline__ double wave_min_f64(double v) { return wave_reduce(v, OpMin{}); }
-__device__ __forceinline__ double wave_sum_f64(double v) { return wave_reduce(v, OpAdd{}); }
-__device__ __forceinline__ float wave_sum_f32(float v) { return wave_reduce(v, OpAdd{}); }
 
 // One semi-implicit Euler step of _F (control.py:234-263) in closed form:
 //   M = [[A + B c2, D + E c2], [D + E c2, D]]   (M22 = m2 lc2^2 + l2 = D)
@@ -170,451 +100,7 @@ __device__ __forceinline__ void dyn_step(ArmState& x, float v1, float v2, const 
     sincos_f32(x.q1 + x.q2, &x.s12, &x.c12);
 }
 
-// --------------------------------------------------- merge + update helpers
-
-constexpr int kMaxWaves = 16;       // up to 1024-thread workgroups
-constexpr int kGroup = 16;          // workgroups per first-level merge group
-// A partial whose rescale factor s = exp((rho - rho_i) / lambda) is below 2^-64
-// changes eta and N by less than 2^-64 * 512 relative to the leading term
-// (which has s = 1 and eta >= 1): far below the fp64 resolution of the result.
-constexpr double kMergeFloor = 5.421010862427522e-20;  // 2^-64
-
-// Rows {rho, eta, N[2T]} handed between workgroups of one launch travel
-// write-through: every store and every load of them is a `sc1` buffer access
-// (MI355X guide G16, "Valid forms" row 1), so neither side needs an
-// agent-scope fence (~1.7 us each) — only each storing wave's vmcnt drain, a
-// workgroup barrier and one relaxed agent atomic per workgroup.
-typedef unsigned int u32x2 __attribute__((__vector_size__(2 * sizeof(unsigned int))));
-constexpr int kSC1 = 16;  // buffer aux bit: sc1
-
-__device__ __forceinline__ __amdgpu_buffer_rsrc_t rows_rsrc(const double* p, int bytes) {
-    return __builtin_amdgcn_make_buffer_rsrc(const_cast<double*>(p), 0, bytes, 0x00020000);
-}
-__device__ __forceinline__ double ld_wt(__amdgpu_buffer_rsrc_t r, int idx) {
-    return __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(r, idx * 8, 0, kSC1));
-}
-// Element index past every rows buffer: a raw buffer load beyond num_records
-// returns 0 without a memory access, so a predicated-off load needs no branch
-// (a branch around each load makes the compiler wait for it at the join).
-constexpr int kOffRange = 1 << 27;   // x 8 B = 1 GiB > any rows buffer, no int overflow
-
-// Tagged granules (MI355X guide, Guideline 16 R2: "the data IS the flag").  One
-// fp64 value travels as {lo32, tag, hi32, tag} in ONE 16-B sc1 store; each 8-B
-// half is a naturally aligned {value, tag} granule, so a reader that sees both
-// tags equal to this launch's epoch holds the whole value — no drain, no flag,
-// no counter.  Tags come from a device-resident epoch (never a kernel argument:
-// graph replay freezes those), zeroed once at context creation.
-typedef unsigned int u32x4 __attribute__((__vector_size__(4 * sizeof(unsigned int))));
-__device__ __forceinline__ void st_gran(__amdgpu_buffer_rsrc_t r, int idx, double v, unsigned tag) {
-    const unsigned long long b = (unsigned long long)__double_as_longlong(v);
-    const u32x4 x = {(unsigned)b, tag, (unsigned)(b >> 32), tag};
-    __builtin_amdgcn_raw_buffer_store_b128(x, r, idx * 16, 0, kSC1);
-}
-// Poll loads are plain sc1 loads; every spin loop opens with an empty asm
-// memory clobber so the loads are re-issued each pass (without it LLVM hoists
-// the read-only loads out of the loop — nothing else in it writes memory — and
-// polls registers).
-__device__ __forceinline__ u32x4 ld_gran(__amdgpu_buffer_rsrc_t r, int idx) {
-    return __builtin_amdgcn_raw_buffer_load_b128(r, idx * 16, 0, kSC1);
-}
-__device__ __forceinline__ bool gran_ok(u32x4 x, unsigned tag) { return x[1] == tag && x[3] == tag; }
-__device__ __forceinline__ double gran_val(u32x4 x) {
-    return __longlong_as_double((long long)(((unsigned long long)x[2] << 32) | x[0]));
-}
-// Bounded spins: ~1 s of polling, then the hand-off reports a timeout (host
-// error word) instead of hanging the GPU; results of that launch are invalid.
-constexpr unsigned kSpinMax = 1u << 20;
-__device__ __forceinline__ void report_timeout(unsigned* tmo) {
-    if (tmo) __hip_atomic_store(tmo, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-}
-__device__ __forceinline__ double poll_gran(__amdgpu_buffer_rsrc_t r, int idx, unsigned tag, unsigned* tmo) {
-    for (unsigned spins = 0;; ++spins) {
-        asm volatile("" ::: "memory");
-        const u32x4 x = ld_gran(r, idx);
-        if (gran_ok(x, tag)) return gran_val(x);
-        if (spins >= kSpinMax) {
-            report_timeout(tmo);
-            return gran_val(x);
-        }
-        __builtin_amdgcn_s_sleep(1);
-    }
-}
-__device__ __forceinline__ void st_wt(__amdgpu_buffer_rsrc_t r, int idx, double v) {
-    __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u32x2, v), r, idx * 8, 0, kSC1);
-}
-
-constexpr int kMergeRows = 32;   // rows per load round in a merge (<= 64: one row per lane)
-
-struct MergeScratch {
-    double red[kMaxWaves];
-    double weps[2 * kMaxT];
-    double unew[2 * kMaxT];
-    int nrel;
-};
-
-// Workgroup minimum.  One use per kernel: the caller's next barrier protects
-// sm.red before any reuse.
-template <int NT>
-__device__ __forceinline__ double block_min_f64(double v, MergeScratch& sm) {
-    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-    v = wave_min_f64(v);
-    if (lane == 0) sm.red[wave] = v;
-    __syncthreads();
-    double r = sm.red[0];
-#pragma unroll
-    for (int w = 1; w < NT / 64; ++w) r = fmin(r, sm.red[w]);
-    return r;
-}
-
-// Merge n rows {rho, eta, N[2T]} (row stride 2 + 2T, read write-through from
-// `rows`) with a log-sum-exp rescale, rho = min rho_i, s_i = exp((rho - rho_i)
-// / lambda), eta = sum s_i eta_i, N = sum s_i N_i, in ascending row order
-// (deterministic).  Rows are consumed kMergeRows at a time, every load of a
-// round issued together (one memory round trip per round) with an online
-// rescale of the running sums when a round lowers rho; rows whose factor is
-// below 2^-64 of the running best are skipped (below fp64 resolution).
-// Wave-local: every wave loads the round's rho_i / eta_i into its lanes,
-// reduces rho with DPP and evaluates s_i, eta itself; s_i reach the column
-// FMAs as scalars (v_readlane) — no LDS traffic and no barrier per round.
-// Thread tid owns column tid (col 0 = eta, 1 + j = N[j]) and tid + NT.
-// The merged row goes to out_wt (write-through, next level) and/or out_row
-// (plain, read after the launch); with `final`, w_eps = N / eta
-// (control.py:112-118) goes to sm.weps and w_eps_out.
-//
-// GRAN: rows are tagged granules (16 B per value) published without any drain
-// or counter; every wave re-reads its round's loads until every tag matches
-// `tag` (kGranRows rows per round: 16 B per load in flight), and out_wt is
-// written as granules too.  Otherwise rows are 8-B sc1 words behind an
-// arrival counter (arrive_last).
-constexpr int kGranRows = 16;
-
-// Final merged row: {rho, eta, N} to out_row (plain, read after the launch) and
-// w_eps = N / eta (control.py:112-118) to sm.weps and w_eps_out.  Thread tid
-// holds column tid (col 0 = eta) and tid + NT.
-template <int NT>
-__device__ __forceinline__ void put_final(double rho, double acc0, double acc1, double eta, int nrel, bool has0,
-                                          bool has1, MergeScratch& sm, double* out_row, double* w_eps_out) {
-    const int tid = threadIdx.x;
-    if (tid == 0) {
-        sm.nrel = nrel;
-        if (out_row) {
-            out_row[0] = rho;
-            out_row[1] = acc0;
-        }
-    } else if (has0) {
-        if (out_row) out_row[1 + tid] = acc0;
-        const double w = acc0 / eta;
-        sm.weps[tid - 1] = w;
-        if (w_eps_out) w_eps_out[tid - 1] = w;
-    }
-    if (has1) {
-        if (out_row) out_row[1 + tid + NT] = acc1;
-        const double w = acc1 / eta;
-        sm.weps[tid + NT - 1] = w;
-        if (w_eps_out) w_eps_out[tid + NT - 1] = w;
-    }
-    __syncthreads();
-}
-
-template <int NT, bool final, bool GRAN>
-__device__ __forceinline__ void merge_rows_block(__amdgpu_buffer_rsrc_t rows, int row0, int n, const KConst& c,
-                                                 MergeScratch& sm, const __amdgpu_buffer_rsrc_t* out_wt, int out_idx,
-                                                 double* out_row, double* w_eps_out, unsigned tag, unsigned* tmo) {
-    constexpr int R = GRAN ? kGranRows : kMergeRows;
-    static_assert(R <= 64, "one row per lane");
-    const int tid = threadIdx.x, lane = tid & 63;
-    const int stride = 2 + 2 * c.T;
-    const int ncol = 2 * c.T + 1;
-    const bool has0 = tid < ncol, has1 = tid + NT < ncol;
-    double acc0 = 0.0, acc1 = 0.0, eta = 0.0, rho = INFINITY;
-    int nrel = 0;
-    for (int r0 = 0; r0 < n; r0 += R) {
-        const int nr = min(R, n - r0);   // uniform
-        const int rb = row0 + r0;
-        const int lrow = lane < nr ? (rb + lane) * stride : kOffRange;
-        double rho_r, eta_l, v[R];
-        if constexpr (GRAN) {
-            // phase 1: poll only the rho granules, one lane per row (a pass
-            // moves 16 B per row, so a row that lands is seen within ~one
-            // short round trip; the bulk of the row is fetched once, below)
-            u32x4 gr;
-            for (unsigned spins = 0;; ++spins) {
-                asm volatile("" ::: "memory");
-                gr = ld_gran(rows, lrow);
-                if (__all(lane >= nr || gran_ok(gr, tag))) break;
-                if (spins >= kSpinMax) {
-                    if (lane == 0) report_timeout(tmo);
-                    break;
-                }
-                __builtin_amdgcn_s_sleep(1);
-            }
-            rho_r = gran_val(gr);
-        } else {
-            rho_r = ld_wt(rows, lrow);
-            eta_l = ld_wt(rows, lrow + 1);
-#pragma unroll
-            for (int i = 0; i < R; ++i) v[i] = ld_wt(rows, (i < nr && has0) ? (rb + i) * stride + 1 + tid : kOffRange);
-        }
-        const double rho_l = lane < nr ? rho_r : INFINITY;
-        const double rnew = fmin(rho, wave_min_f64(rho_l));
-        double s_l = 0.0;
-        if (lane < nr) {
-            const double s = exp((rnew - rho_l) * c.inv_lambda);
-            s_l = s >= kMergeFloor ? s : 0.0;
-        }
-        const unsigned long long rel = __ballot(s_l != 0.0);   // rows that carry weight (uniform)
-        nrel += __popcll(rel);
-        if constexpr (GRAN) {
-            // phase 2: eta and the columns of the weighted rows only (usually one
-            // or two at run.py's lambda), re-read until every tag matches
-            u32x4 ge, gv[R];
-            for (unsigned spins = 0;; ++spins) {
-                asm volatile("" ::: "memory");
-                ge = ld_gran(rows, ((rel >> lane) & 1) ? lrow + 1 : kOffRange);
-#pragma unroll
-                for (int i = 0; i < R; ++i)
-                    gv[i] = ld_gran(rows, (((rel >> i) & 1) && has0) ? (rb + i) * stride + 1 + tid : kOffRange);
-                bool ok = !((rel >> lane) & 1) || gran_ok(ge, tag);
-#pragma unroll
-                for (int i = 0; i < R; ++i) ok = ok && (!(((rel >> i) & 1) && has0) || gran_ok(gv[i], tag));
-                if (__all(ok)) break;
-                if (spins >= kSpinMax) {
-                    if (lane == 0) report_timeout(tmo);
-                    break;
-                }
-                __builtin_amdgcn_s_sleep(1);
-            }
-            eta_l = gran_val(ge);
-#pragma unroll
-            for (int i = 0; i < R; ++i) v[i] = gran_val(gv[i]);
-        }
-        if (rnew < rho && rho != INFINITY) {  // uniform: rescale the running sums to the new minimum
-            const double f = exp((rnew - rho) * c.inv_lambda);
-            acc0 *= f;
-            acc1 *= f;
-            eta *= f;
-        }
-        rho = rnew;
-#pragma unroll
-        for (int i = 0; i < R; ++i) {
-            if (i < nr) {
-                const double s = readlane_f64(s_l, i);
-                if (s != 0.0) {
-                    acc0 = fma(s, v[i], acc0);
-                    eta = fma(s, readlane_f64(eta_l, i), eta);
-                }
-            }
-        }
-        if (ncol > NT) {  // second column pass (T = 128 only: 2T + 1 = 257 columns)
-            for (int i = 0; i < nr; ++i) {
-                const double s = readlane_f64(s_l, i);
-                if (s != 0.0 && has1) {
-                    const int idx = (rb + i) * stride + 1 + tid + NT;
-                    acc1 = fma(s, GRAN ? poll_gran(rows, idx, tag, tmo) : ld_wt(rows, idx), acc1);
-                }
-            }
-        }
-    }
-    if constexpr (final) {
-        put_final<NT>(rho, acc0, acc1, eta, nrel, has0, has1, sm, out_row, w_eps_out);
-    } else {
-        auto put = [&](int col, double v) {  // col 0 = rho, 1 = eta, 2 + j = N[j]
-            if constexpr (GRAN) st_gran(*out_wt, out_idx * stride + col, v, tag);
-            else st_wt(*out_wt, out_idx * stride + col, v);
-        };
-        if (tid == 0) {
-            put(0, rho);
-            put(1, acc0);
-        } else if (has0) {
-            put(1 + tid, acc0);
-        }
-        if (has1) put(1 + tid + NT, acc1);
-    }
-}
-
-// The k-th (0-based) set bit of m; k < popcount(m).
-__device__ __forceinline__ int select_bit(unsigned long long m, int k) {
-    int pos = 0;
-#pragma unroll
-    for (int w = 32; w > 0; w >>= 1) {
-        const int cnt = __popcll(m & ((1ull << w) - 1));
-        if (k >= cnt) {
-            k -= cnt;
-            m >>= w;
-            pos += w;
-        }
-    }
-    return pos;
-}
-
-constexpr int kDirectRows = 256;  // workgroup rows the direct merge scans (4 per lane)
-constexpr int kDirectMax = 16;    // weighted rows it merges; more go through the group rows
-
-// Single-level finish for the usual regime (few weighted rows, S spread >> lambda):
-// read rho of EVERY workgroup row (n <= kDirectRows), and when at most
-// kDirectMax rows carry weight relative to the global minimum, merge exactly
-// those rows in ascending order straight from the workgroup slab — one hand-off
-// on the critical path instead of two.  Returns false (uniformly) when more rows
-// carry weight; the caller then merges through the group rows.  Wave-local
-// like merge_rows_block; the result goes out as in a final merge.
-template <int NT, bool GRAN>
-__device__ __forceinline__ bool direct_merge(__amdgpu_buffer_rsrc_t rows, int n, const KConst& c, MergeScratch& sm,
-                                             double* out_row, double* w_eps_out, unsigned tag, unsigned* tmo) {
-    constexpr int P = kDirectRows / 64;
-    const int tid = threadIdx.x, lane = tid & 63;
-    const int stride = 2 + 2 * c.T;
-    const int ncol = 2 * c.T + 1;
-    const bool has0 = tid < ncol, has1 = tid + NT < ncol;
-    // phase 1: rho of row lane + 64 j in slot j
-    double rho_l[P];
-    if constexpr (GRAN) {
-        u32x4 gr[P];
-        for (unsigned spins = 0;; ++spins) {
-            asm volatile("" ::: "memory");
-            bool ok = true;
-#pragma unroll
-            for (int j = 0; j < P; ++j) {
-                const int r = lane + 64 * j;
-                gr[j] = ld_gran(rows, r < n ? r * stride : kOffRange);
-                ok = ok && (r >= n || gran_ok(gr[j], tag));
-            }
-            if (__all(ok)) break;
-            if (spins >= kSpinMax) {
-                if (lane == 0) report_timeout(tmo);
-                break;
-            }
-            __builtin_amdgcn_s_sleep(1);
-        }
-#pragma unroll
-        for (int j = 0; j < P; ++j) rho_l[j] = lane + 64 * j < n ? gran_val(gr[j]) : INFINITY;
-    } else {
-#pragma unroll
-        for (int j = 0; j < P; ++j) {
-            const int r = lane + 64 * j;
-            const double x = ld_wt(rows, r < n ? r * stride : kOffRange);
-            rho_l[j] = r < n ? x : INFINITY;
-        }
-    }
-    double m = rho_l[0];
-#pragma unroll
-    for (int j = 1; j < P; ++j) m = fmin(m, rho_l[j]);
-    const double rho = wave_min_f64(m);
-    double s_l[P];
-    unsigned long long rel[P];
-    int nrel = 0;
-#pragma unroll
-    for (int j = 0; j < P; ++j) {
-        const double s = exp((rho - rho_l[j]) * c.inv_lambda);
-        s_l[j] = (lane + 64 * j < n && s >= kMergeFloor) ? s : 0.0;
-        rel[j] = __ballot(s_l[j] != 0.0);
-        nrel += __popcll(rel[j]);
-    }
-    if (nrel > kDirectMax) return false;
-    // lane k < nrel: the k-th weighted row (ascending) and its factor
-    int k = lane, row = 0;
-    bool found = false;
-#pragma unroll
-    for (int j = 0; j < P; ++j) {
-        const int cnt = __popcll(rel[j]);
-        if (!found && k < cnt) {
-            row = 64 * j + select_bit(rel[j], k);
-            found = true;
-        } else if (!found) {
-            k -= cnt;
-        }
-    }
-    double sk = 0.0;
-#pragma unroll
-    for (int j = 0; j < P; ++j) {
-        const double sj = __shfl(s_l[j], row & 63);
-        if ((row >> 6) == j) sk = sj;
-    }
-    const bool mine = lane < nrel;
-    // phase 2: eta and the columns of the weighted rows
-    double eta_k, v[kDirectMax];
-    if constexpr (GRAN) {
-        u32x4 ge, gv[kDirectMax];
-        for (unsigned spins = 0;; ++spins) {
-            asm volatile("" ::: "memory");
-            ge = ld_gran(rows, mine ? row * stride + 1 : kOffRange);
-#pragma unroll
-            for (int i = 0; i < kDirectMax; ++i)
-                gv[i] = ld_gran(rows, (i < nrel && has0) ? __builtin_amdgcn_readlane(row, i) * stride + 1 + tid
-                                                         : kOffRange);
-            bool ok = !mine || gran_ok(ge, tag);
-#pragma unroll
-            for (int i = 0; i < kDirectMax; ++i) ok = ok && (!(i < nrel && has0) || gran_ok(gv[i], tag));
-            if (__all(ok)) break;
-            if (spins >= kSpinMax) {
-                if (lane == 0) report_timeout(tmo);
-                break;
-            }
-            __builtin_amdgcn_s_sleep(1);
-        }
-        eta_k = gran_val(ge);
-#pragma unroll
-        for (int i = 0; i < kDirectMax; ++i) v[i] = gran_val(gv[i]);
-    } else {
-        eta_k = ld_wt(rows, mine ? row * stride + 1 : kOffRange);
-#pragma unroll
-        for (int i = 0; i < kDirectMax; ++i)
-            v[i] = ld_wt(rows, (i < nrel && has0) ? __builtin_amdgcn_readlane(row, i) * stride + 1 + tid : kOffRange);
-    }
-    double acc0 = 0.0, acc1 = 0.0, eta = 0.0;
-#pragma unroll
-    for (int i = 0; i < kDirectMax; ++i) {
-        if (i < nrel) {
-            const double s = readlane_f64(sk, i);
-            acc0 = fma(s, v[i], acc0);
-            eta = fma(s, readlane_f64(eta_k, i), eta);
-        }
-    }
-    if (ncol > NT) {  // second column pass (T = 128 only)
-        for (int i = 0; i < nrel; ++i) {
-            const double s = readlane_f64(sk, i);
-            if (has1) {
-                const int idx = __builtin_amdgcn_readlane(row, i) * stride + 1 + tid + NT;
-                acc1 = fma(s, GRAN ? poll_gran(rows, idx, tag, tmo) : ld_wt(rows, idx), acc1);
-            }
-        }
-    }
-    put_final<NT>(rho, acc0, acc1, eta, nrel, has0, has1, sm, out_row, w_eps_out);
-    return true;
-}
-
-// Arrive on `counter` after this workgroup's write-through stores; true in
-// every thread of the workgroup that arrived last (which re-arms the counter).
-// sc1 loads alone stand in for the acquire only at one workgroup per CU (the
-// measured form, MI355X guide "Valid forms"); with `acquire` (larger grids)
-// the last arriver also runs an agent-scope acquire before the barrier.
-template <int NT>
-__device__ __forceinline__ bool arrive_last(unsigned* counter, unsigned expected, unsigned* s_flag, bool acquire) {
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every storing wave drains its sc1 stores
-    __syncthreads();
-    if (threadIdx.x == 0) {
-        const unsigned prev = __hip_atomic_fetch_add(counter, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        const bool last = prev == expected - 1;
-        if (last) __hip_atomic_store(counter, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        if (last && acquire) {
-            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        }
-        *s_flag = last ? 1u : 0u;
-    }
-    __syncthreads();
-    return *s_flag != 0;
-}
-
-// Upper median of 10 (rank 5): a 29-comparator sorting network (verified on all
-// 2^10 0/1 inputs), the element scipy.ndimage.median_filter(size=10) returns.
-__device__ __forceinline__ double median10(double* v) {
-#define CX(i, j) { const double lo = fmin(v[i], v[j]), hi = fmax(v[i], v[j]); v[i] = lo; v[j] = hi; }
-    CX(4, 9) CX(3, 8) CX(2, 7) CX(1, 6) CX(0, 5) CX(1, 4) CX(6, 9) CX(0, 3) CX(5, 8) CX(0, 2)
-    CX(3, 6) CX(7, 9) CX(0, 1) CX(2, 4) CX(5, 7) CX(8, 9) CX(1, 2) CX(4, 6) CX(7, 8) CX(3, 5)
-    CX(2, 5) CX(6, 8) CX(1, 3) CX(4, 7) CX(2, 3) CX(6, 7) CX(3, 4) CX(5, 6) CX(4, 5)
-#undef CX
-    return v[5];
-}
+using Scratch = MergeScratch<2 * kMaxT>;
 
 // Median filter (scipy.ndimage.median_filter(size=10, mode='reflect'),
 // control.py:319-327, window [t-5, t+4], valid for T >= 5), u += w_eps
@@ -622,22 +108,11 @@ __device__ __forceinline__ double median10(double* v) {
 // of the next launch.  u_cur: this thread's cur->u[t][d] (t = tid/2, d = tid%2),
 // read at kernel entry.
 template <int NT>
-__device__ void nominal_update_block(const DevStep* cur, DevStep* nxt, const KConst& c, MergeScratch& sm,
+__device__ void nominal_update_block(const DevStep* cur, DevStep* nxt, const KConst& c, Scratch& sm,
                                      double u_cur) {
     const int tid = threadIdx.x;
     const int T = c.T;
-    if (tid < 2 * T) {
-        const int t = tid >> 1, d = tid & 1;
-        double v[10];
-#pragma unroll
-        for (int i = 0; i < 10; ++i) {
-            int m = t - 5 + i;              // one reflection suffices for T >= 5
-            m = m < 0 ? -m - 1 : m;
-            m = m >= T ? 2 * T - 1 - m : m;
-            v[i] = sm.weps[2 * m + d];
-        }
-        sm.unew[tid] = u_cur + median10(v);
-    }
+    if (tid < 2 * T) sm.unew[tid] = u_cur + median_at(sm, tid >> 1, tid & 1, T, 2);
     __syncthreads();
     if (tid < T) {
         const int src = tid + 1 < T ? tid + 1 : T - 1;
@@ -667,77 +142,8 @@ __device__ __forceinline__ float2 noise_ld(const float2* p) {
 #else
 __device__ __forceinline__ float2 noise_ld(const float2* p) { return *p; }
 #endif
-#define PIN_LOADS() asm volatile("" ::: "memory")
-
-// The per-step constants are read through the constant address space: scalar
-// (SMEM) loads that stay scalar across the scheduling boundaries above.  The
-// block is written only by host copies or by the PREVIOUS launch (ping-pong).
-typedef __attribute__((address_space(4))) const float cfloat;
-__device__ __forceinline__ float4 const_ld4(cfloat* p) { return make_float4(p[0], p[1], p[2], p[3]); }
-
-typedef float f32x2 __attribute__((ext_vector_type(2)));
-
-// v_min3_f32 / v_min_f32 issued directly: the operands are bit-packed keys, and
-// fminf() would make hipcc canonicalise every one of them (v_max x, x) first.
-__device__ __forceinline__ float min3_raw(float a, float b, float c) {
-    float r;
-    asm("v_min3_f32 %0, %1, %2, %3" : "=v"(r) : "v"(a), "v"(b), "v"(c));
-    return r;
-}
-__device__ __forceinline__ float min_raw(float a, float b) {
-    float r;
-    asm("v_min_f32 %0, %1, %2" : "=v"(r) : "v"(a), "v"(b));
-    return r;
-}
-
-template <int LPS>
-struct Search {
-    // window slots per lane, even so they pair up for packed math
-    static constexpr int SL = ((MPPI_SEARCH_LEN + LPS - 1) / LPS + 1) & ~1;
-    static constexpr int SP = SL / 2;
-    f32x2 krx[SP], kry[SP], kc[SP];
-    int sub;
-    float cx, cy;
-
-    // Nearest waypoint of the shared window (control.py:208-215):
-    //   argmin_j |p - r_j|^2 = argmin_j (|r'_j|^2 - 2 p'.r'_j) (window-centred),
-    // two slots per v_pk_fma_f32; the slot index is packed into the 5 low
-    // mantissa bits so one v_min3 per two slots carries the argmin; the LPS
-    // lanes of a sample close it with DPP.
-    __device__ __forceinline__ unsigned nearest(float px, float py) const {
-        const float ax = -2.f * (px - cx), ay = -2.f * (py - cy);
-        const f32x2 ax2 = {ax, ax}, ay2 = {ay, ay};
-        float best = 3.0e38f;
-#pragma unroll
-        for (int i = 0; i < SP; ++i) {
-            const f32x2 key = __builtin_elementwise_fma(ax2, krx[i], __builtin_elementwise_fma(ay2, kry[i], kc[i]));
-            const unsigned j = (unsigned)(sub * SL + 2 * i);
-            const float k0 = __uint_as_float((__float_as_uint(key.x) & ~31u) | j);
-            const float k1 = __uint_as_float((__float_as_uint(key.y) & ~31u) | (j + 1));
-            best = min3_raw(best, k0, k1);
-        }
-        if (LPS >= 2) best = min_raw(best, dpp_f32<0xB1>(best));  // quad_perm xor 1
-        if (LPS >= 4) best = min_raw(best, dpp_f32<0x4E>(best));  // quad_perm xor 2
-        return __float_as_uint(best) & 31u;
-    }
-};
-
-__device__ __forceinline__ float weighted_sq(float ex, float ey, float e1, float e2, const float* w) {
-    return fmaf(w[0], ex * ex, fmaf(w[1], ey * ey, fmaf(w[2], e1 * e1, w[3] * e2 * e2)));
-}
-
-// Diagnostic builds only (-DMPPI_STAMPS, a separate .so): per-workgroup
-// timeline in s_memrealtime ticks (100 MHz) + counters.  Never in the product.
-#ifdef MPPI_STAMPS
-#define STAMP(slot, val) do { if (dbg && threadIdx.x == 0) dbg[(size_t)blockIdx.x * 16 + (slot)] = (val); } while (0)
-#define NOW() __builtin_amdgcn_s_memrealtime()
-#else
-#define STAMP(slot, val) do { (void)dbg; } while (0)
-#define NOW() 0ull
-#endif
 
 constexpr int kPF = 4;  // noise rows in flight per lane
-constexpr int kSparseMax = 16;  // weighted samples per workgroup handled by the gather path
 
 // POLL: the partial rows travel as tagged granules (see st_gran) to consumer
 // workgroups that poll for them — the highest-numbered workgroup of each group
@@ -760,7 +166,7 @@ __global__ __launch_bounds__(NT) void rollout_kernel(
     __shared__ int s_k[NT];
     __shared__ float s_e[NT];
     __shared__ unsigned s_flag;
-    __shared__ MergeScratch sm;
+    __shared__ Scratch sm;
 
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const int k_raw = (blockIdx.x * NT + tid) / LPS;
@@ -780,26 +186,7 @@ __global__ __launch_bounds__(NT) void rollout_kernel(
     const double u_cur = ((flags & MPPI_FLAG_FUSED_UPDATE) && tid < 2 * T) ? st->u[tid >> 1][tid & 1] : 0.0;
     if (tid < kSlots) s_win[tid] = st->win[tid];
     Search<LPS> sr;
-    if (LPS == 1) {
-        // lane-opaque zero: keeps the 30 window slots in VGPRs (as uniform
-        // values they would go to SGPRs and spill)
-        int z;
-        asm volatile("v_mov_b32 %0, 0" : "=v"(z));
-        sr.sub = z;
-    } else {
-        sr.sub = tid & (LPS - 1);
-    }
-    static_assert(Search<LPS>::SL * LPS <= kSlots, "window slots");
-#pragma unroll
-    for (int i = 0; i < Search<LPS>::SP; ++i) {
-        const float4 k0 = st->key[sr.sub * Search<LPS>::SL + 2 * i];
-        const float4 k1 = st->key[sr.sub * Search<LPS>::SL + 2 * i + 1];
-        sr.krx[i] = f32x2{k0.x, k1.x};
-        sr.kry[i] = f32x2{k0.y, k1.y};
-        sr.kc[i] = f32x2{k0.z, k1.z};
-    }
-    sr.cx = st->ctr.x;
-    sr.cy = st->ctr.y;
+    sr.load(st->key, st->ctr, tid & (LPS - 1));
     const float4 x0 = st->x0;
     ArmState x;
     x.q1 = x0.x;
@@ -899,6 +286,7 @@ __global__ __launch_bounds__(NT) void rollout_kernel(
     }
     __syncthreads();
     const int stride = 2 + 2 * T;
+    const RowGeo geo(2 * T);   // 2T + 1 merged columns <= NT: one column chunk (host keeps T <= 127 at NT = 256)
     const int nrows = c.nblocks;
     const int ngroups = (nrows + kGroup - 1) / kGroup;
     constexpr int kValBytes = POLL ? 16 : 8;
@@ -983,35 +371,37 @@ __global__ __launch_bounds__(NT) void rollout_kernel(
         if ((int)blockIdx.x != g * kGroup + gsz - 1) return;
         STAMP(3, NOW());
         if (ngroups == 1) {
-            merge_rows_block<NT, true, true>(slab_r, 0, gsz, c, sm, nullptr, 0, partial_out, w_eps_out, tag, tmo);
+            merge_rows_block<NT, 1, true, true>(slab_r, 0, gsz, geo, c.inv_lambda, sm, nullptr, 0, partial_out, w_eps_out, tag, tmo);
         } else if ((int)blockIdx.x == nrows - 1 && nrows <= kDirectRows &&
-                   direct_merge<NT, true>(slab_r, nrows, c, sm, partial_out, w_eps_out, tag, tmo)) {
+                   direct_merge<NT, 1, true>(slab_r, nrows, geo, c.inv_lambda, sm, partial_out, w_eps_out, tag, tmo)) {
             // few weighted rows: finished straight from the workgroup rows
         } else {
-            merge_rows_block<NT, false, true>(slab_r, g * kGroup, gsz, c, sm, &gslab_r, g, nullptr, nullptr, tag, tmo);
+            merge_rows_block<NT, 1, false, true>(slab_r, g * kGroup, gsz, geo, c.inv_lambda, sm, &gslab_r, g, nullptr, nullptr, tag,
+                                                 tmo);
             STAMP(10, NOW());
             // ---- level 2: the last workgroup polls and merges the group rows
             if ((int)blockIdx.x != nrows - 1) return;
             STAMP(4, NOW());
-            merge_rows_block<NT, true, true>(gslab_r, 0, ngroups, c, sm, nullptr, 0, partial_out, w_eps_out, tag,
-                                             tmo);
+            merge_rows_block<NT, 1, true, true>(gslab_r, 0, ngroups, geo, c.inv_lambda, sm, nullptr, 0, partial_out,
+                                                w_eps_out, tag, tmo);
         }
         // every workgroup read the epoch before publishing, and all have published
         if (threadIdx.x == 0) __hip_atomic_store(epoch, tag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     } else {
         // ---- level 1: the last workgroup of each group of kGroup merges the group
-        if (!arrive_last<NT>(counters + g, (unsigned)gsz, &s_flag, c.acquire != 0)) return;
+        if (!arrive_last(counters + g, (unsigned)gsz, &s_flag, c.acquire != 0)) return;
         STAMP(3, NOW());
-        merge_rows_block<NT, false, false>(slab_r, g * kGroup, gsz, c, sm, &gslab_r, g, nullptr, nullptr, 0u, nullptr);
+        merge_rows_block<NT, 1, false, false>(slab_r, g * kGroup, gsz, geo, c.inv_lambda, sm, &gslab_r, g, nullptr, nullptr,
+                                              0u, nullptr);
         STAMP(10, NOW());
         // ---- level 2: the last group merges the group rows and finishes the step
-        if (!arrive_last<NT>(counters + ngroups, (unsigned)ngroups, &s_flag, c.acquire != 0)) return;
+        if (!arrive_last(counters + ngroups, (unsigned)ngroups, &s_flag, c.acquire != 0)) return;
         STAMP(4, NOW());
         // the same decision as the poll form (identical results either way)
         if (!(ngroups > 1 && nrows <= kDirectRows &&
-              direct_merge<NT, false>(slab_r, nrows, c, sm, partial_out, w_eps_out, 0u, nullptr)))
-            merge_rows_block<NT, true, false>(gslab_r, 0, ngroups, c, sm, nullptr, 0, partial_out, w_eps_out, 0u,
-                                              nullptr);
+              direct_merge<NT, 1, false>(slab_r, nrows, geo, c.inv_lambda, sm, partial_out, w_eps_out, 0u, nullptr)))
+            merge_rows_block<NT, 1, true, false>(gslab_r, 0, ngroups, geo, c.inv_lambda, sm, nullptr, 0, partial_out,
+                                                 w_eps_out, 0u, nullptr);
     }
     STAMP(11, NOW());
     STAMP(6, (unsigned long long)sm.nrel);
@@ -1019,17 +409,17 @@ __global__ __launch_bounds__(NT) void rollout_kernel(
     STAMP(7, NOW());
 }
 
-constexpr int kMergeThreads = 256;
-
-__global__ __launch_bounds__(kMergeThreads) void merge_kernel(const KConst c, const double* parts, int n,
-                                                              double* w_eps_out, const DevStep* cur,
-                                                              DevStep* nxt, unsigned flags) {
-    __shared__ MergeScratch sm;
+// Merge of the all-gathered per-device rows (multi-GPU), plus the fused update.
+template <int NT>
+__global__ __launch_bounds__(NT) void merge_kernel(const KConst c, const double* parts, int n, double* w_eps_out,
+                                                   const DevStep* cur, DevStep* nxt, unsigned flags) {
+    __shared__ Scratch sm;
     const int tid = threadIdx.x;
     const double u_cur = ((flags & MPPI_FLAG_FUSED_UPDATE) && tid < 2 * c.T) ? cur->u[tid >> 1][tid & 1] : 0.0;
     const __amdgpu_buffer_rsrc_t r = rows_rsrc(parts, n * (2 + 2 * c.T) * 8);
-    merge_rows_block<kMergeThreads, true, false>(r, 0, n, c, sm, nullptr, 0, nullptr, w_eps_out, 0u, nullptr);
-    if (flags & MPPI_FLAG_FUSED_UPDATE) nominal_update_block<kMergeThreads>(cur, nxt, c, sm, u_cur);
+    merge_rows_block<NT, 1, true, false>(r, 0, n, RowGeo(2 * c.T), c.inv_lambda, sm, nullptr, 0, nullptr, w_eps_out,
+                                         0u, nullptr);
+    if (flags & MPPI_FLAG_FUSED_UPDATE) nominal_update_block<NT>(cur, nxt, c, sm, u_cur);
 }
 
 // Trajectory re-roll (control.py:129-145): control(t) = base[(t-1) mod T] (+ eps).
@@ -1063,19 +453,7 @@ __global__ __launch_bounds__(kThreads) void traj_kernel(const KConst c, const De
     }
 }
 
-// Philox4x32-10 (Salmon et al., SC'11) + Box-Muller; eps = L z, L = chol(Sigma).
-__device__ __forceinline__ uint4 philox4x32_10(uint4 ctr, uint2 key) {
-#pragma unroll
-    for (int r = 0; r < 10; ++r) {
-        const unsigned lo0 = 0xD2511F53u * ctr.x, hi0 = __umulhi(0xD2511F53u, ctr.x);
-        const unsigned lo1 = 0xCD9E8D57u * ctr.z, hi1 = __umulhi(0xCD9E8D57u, ctr.z);
-        ctr = make_uint4(hi1 ^ ctr.y ^ key.x, lo1, hi0 ^ ctr.w ^ key.y, lo0);
-        key.x += 0x9E3779B9u;
-        key.y += 0xBB67AE85u;
-    }
-    return ctr;
-}
-
+// Philox4x32-10 + Box-Muller (mppi_device.h); eps = L z, L = chol(Sigma).
 __global__ __launch_bounds__(kThreads) void philox_noise_kernel(int K_local, int T, long long k_offset,
                                                                 unsigned long long seed,
                                                                 unsigned long long step, float L00,
@@ -1089,16 +467,8 @@ __global__ __launch_bounds__(kThreads) void philox_noise_kernel(int K_local, int
     const uint4 ctr = make_uint4((unsigned)kg, (unsigned)(kg >> 32), (unsigned)t0, (unsigned)step);
     const uint2 key = make_uint2((unsigned)seed, (unsigned)(seed >> 32) ^ (unsigned)(step >> 32));
     const uint4 r = philox4x32_10(ctr, key);
-    const float inv = 2.3283064365386963e-10f;  // 2^-32
-    const float u0 = ((float)r.x + 1.0f) * inv, u1 = (float)r.y * inv;
-    const float u2 = ((float)r.z + 1.0f) * inv, u3 = (float)r.w * inv;
-    float s, co;
-    const float ra = sqrtf(-2.0f * logf(fminf(u0, 1.0f)));
-    sincospif(2.0f * u1, &s, &co);
-    const float z0 = ra * co, z1 = ra * s;
-    const float rb = sqrtf(-2.0f * logf(fminf(u2, 1.0f)));
-    sincospif(2.0f * u3, &s, &co);
-    const float z2 = rb * co, z3 = rb * s;
+    const float2 za = box_muller(r.x, r.y), zb = box_muller(r.z, r.w);
+    const float z0 = za.x, z1 = za.y, z2 = zb.x, z3 = zb.y;
     out[(size_t)t0 * K_local + k] = make_float2(L00 * z0, fmaf(L10, z0, L11 * z1));
     if (t0 + 1 < T) out[(size_t)(t0 + 1) * K_local + k] = make_float2(L00 * z2, fmaf(L10, z2, L11 * z3));
 }
@@ -1132,13 +502,19 @@ struct mppi_ctx {
     unsigned long long* d_dbg = nullptr;  // diagnostic stamp buffer (MPPI_STAMPS builds)
 };
 
+namespace mppi_host {
 namespace {
 thread_local std::string g_err;
-
+}
 int fail(int code, const std::string& msg) {
     g_err = msg;
     return code;
 }
+const char* last_error() { return g_err.c_str(); }
+}  // namespace mppi_host
+
+namespace {
+using mppi_host::fail;
 
 #define HIP_TRY(expr)                                                                 \
     do {                                                                              \
@@ -1182,7 +558,7 @@ int auto_lps(int K_local) {
 
 extern "C" {
 
-const char* mppi_last_error(void) { return g_err.c_str(); }
+const char* mppi_last_error(void) { return mppi_host::last_error(); }
 
 int mppi_ctx_create(const mppi_config* cfg, int device, void* stream, mppi_ctx** out) {
     if (!cfg || !out) return fail(MPPI_E_ARG, "null argument");
@@ -1213,6 +589,8 @@ int mppi_ctx_create(const mppi_config* cfg, int device, void* stream, mppi_ctx**
     const long long lanes = (long long)cfg->K_local * lps;
     c->nt = lanes >= 512LL * 256 ? 512 : 256;
     if (const char* ev = getenv("MPPI_BLOCK")) c->nt = atoi(ev) == 512 ? 512 : 256;
+    // a workgroup's merge thread owns one column of the 2T + 1 merged columns
+    if (2 * cfg->T + 1 > c->nt) c->nt = 512;
     c->nblocks = (int)((lanes + c->nt - 1) / c->nt);
     if (c->nblocks > 1024 * 1024) {
         delete c;
@@ -1420,8 +798,13 @@ int mppi_merge_partials(mppi_ctx* c, const double* partials_dev, int n, unsigned
         return fail(MPPI_E_ARG, "device median filter needs T >= 5 (use the host update)");
     const DevStep* cur = c->d_step + c->cur;
     DevStep* nxt = c->d_step + (c->cur ^ 1);
-    hipLaunchKernelGGL(merge_kernel, dim3(1), dim3(kMergeThreads), 0, c->stream, c->kc, partials_dev, n,
-                       c->d_weps, cur, nxt, flags);
+    // one workgroup, one thread per merged column (2T + 1 <= 256 up to T = 127)
+    if (2 * c->cfg.T + 1 <= 256)
+        hipLaunchKernelGGL(merge_kernel<256>, dim3(1), dim3(256), 0, c->stream, c->kc, partials_dev, n, c->d_weps,
+                           cur, nxt, flags);
+    else
+        hipLaunchKernelGGL(merge_kernel<512>, dim3(1), dim3(512), 0, c->stream, c->kc, partials_dev, n, c->d_weps,
+                           cur, nxt, flags);
     const int rc = launch_check("merge_kernel");
     if (rc == MPPI_OK && (flags & MPPI_FLAG_FUSED_UPDATE)) c->cur ^= 1;
     return rc;

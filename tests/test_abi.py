@@ -61,6 +61,31 @@ int main(void) {
                     Cc.lanes_per_sample.offset]
 
 
+def test_chain_struct_layout_matches_header(tmp_path):
+    from mppi_robotarm_amd import _native as N
+    probe = tmp_path / "probe.c"
+    probe.write_text(r'''
+#include <stddef.h>
+#include <stdio.h>
+#include "mppi_rocm.h"
+int main(void) {
+  printf("%zu %zu %zu %zu %zu %zu %zu %zu %zu %zu %d\n", sizeof(mppi_chain_config), sizeof(mppi_chain_params),
+         offsetof(mppi_chain_config, delta_t), offsetof(mppi_chain_config, sigma),
+         offsetof(mppi_chain_config, stage_cost_weight), offsetof(mppi_chain_config, terminal_cost_weight),
+         offsetof(mppi_chain_config, chain), offsetof(mppi_chain_params, m), offsetof(mppi_chain_params, fk),
+         offsetof(mppi_chain_params, g), MPPI_CHAIN_MAX_DOF);
+  return 0;
+}
+''')
+    exe = tmp_path / "probe"
+    subprocess.run(["gcc", "-I", os.path.dirname(HEADER), str(probe), "-o", str(exe)], check=True)
+    vals = [int(v) for v in subprocess.run([str(exe)], capture_output=True, text=True, check=True).stdout.split()]
+    Cc, Pc = N.ChainConfigC, N.ChainParamsC
+    assert vals == [C.sizeof(Cc), C.sizeof(Pc), Cc.delta_t.offset, Cc.sigma.offset, Cc.stage_cost_weight.offset,
+                    Cc.terminal_cost_weight.offset, Cc.chain.offset, Pc.m.offset, Pc.fk.offset, Pc.g.offset,
+                    N.CHAIN_MAX_DOF]
+
+
 def test_constants_match_header():
     from mppi_robotarm_amd import _native as N
     text = open(HEADER).read()

@@ -3,11 +3,9 @@
 # mppi_robotarm_amd/_lib/libmppi_rocm_<name>.so.  Usage: build_variants.sh name:"-DFLAGS" ...
 set -e
 cd "$(dirname "$0")/.."
-SRC=mppi_robotarm_amd/csrc/mppi_rocm.hip
-OUT=mppi_robotarm_amd/_lib
-F="--offload-arch=gfx950 -O3 -std=c++17 -fPIC -shared -Iinclude"
 for spec in "$@"; do
   name=${spec%%:*}; flags=${spec#*:}
-  hipcc $F $flags -o $OUT/libmppi_rocm_$name.so $SRC &
+  python3 -c "import sys; from mppi_robotarm_amd.build import build_native; build_native(True, sys.argv[1].split(), sys.argv[2])" \
+    "$flags" "mppi_robotarm_amd/_lib/libmppi_rocm_$name.so" &
 done
 wait

@@ -1,6 +1,6 @@
 """Per-kernel register / scratch / spill summary of the product build (gfx950).
 
-    python tools/resources.py [extra hipcc flags]
+    python tools/resources.py [--src mppi_chain.hip] [extra hipcc flags]
 """
 import os
 import re
@@ -14,9 +14,13 @@ KEYS = {"VGPRs": "vgpr", "TotalSGPRs": "sgpr", "ScratchSize [bytes/lane]": "scra
 
 def main():
     asm = "/tmp/mppi_res.s"
+    args = sys.argv[1:]
+    src = "mppi_rocm.hip"
+    if args[:1] == ["--src"]:
+        src, args = args[1], args[2:]
     cmd = ["/opt/rocm/bin/hipcc", "--offload-arch=gfx950", "-O3", "-std=c++17", "-I" + os.path.join(ROOT, "include"),
-           "--cuda-device-only", "-S", "-o", asm, os.path.join(ROOT, "mppi_robotarm_amd/csrc/mppi_rocm.hip"),
-           "-Rpass-analysis=kernel-resource-usage"] + sys.argv[1:]
+           "--cuda-device-only", "-S", "-o", asm, os.path.join(ROOT, "mppi_robotarm_amd/csrc", src),
+           "-Rpass-analysis=kernel-resource-usage"] + args
     out = subprocess.run(cmd, capture_output=True, text=True, cwd="/tmp").stderr
     rows, cur = [], None
     for line in out.splitlines():
