@@ -139,9 +139,10 @@ int mppi_debug_set_buffer(mppi_ctx *ctx, void *dbg_dev);
  * n-link planar chain (BASELINE config 5: "7-DoF arm dynamics (extended
  * sys_params.py), K=131072 T=128, xydq_circle.txt reference").  The reference
  * has no such model; it is BUILD-DEFINED (oracle/chain_oracle.py: mass matrix
- * D_ab = mu_ab cos(th_a - th_b) + delta_ab I_a in absolute angles, Coriolis,
- * gravity, Cholesky solve, semi-implicit Euler as control.py:256-259) and
- * reduces to the reference _F (control.py:234-263) at n = 2 with I = l.  The
+ * D_ab = mu_ab cos(th_a - th_b) + delta_ab I_a in absolute angles plus the joint
+ * armature J, Coriolis, gravity, joint damping b, Cholesky solve, semi-implicit
+ * Euler as control.py:256-259) and reduces to the reference _F
+ * (control.py:234-263) at n = 2 with I = l and J = b = 0.  The
  * cost is control.py:174-232 on (end-effector x, y, dq_1, dq_2).  Same
  * conventions as above; noise is [T][n][K_local] fp32, u and w_eps are T x n
  * row-major, x0 = [q(n), dq(n)].
@@ -155,6 +156,8 @@ typedef struct {
     double lc[MPPI_CHAIN_MAX_DOF];          /* joint-to-centre-of-mass distances          */
     double I[MPPI_CHAIN_MAX_DOF];           /* inertias about the centre of mass          */
     double fk[MPPI_CHAIN_MAX_DOF];          /* lengths used by the cost's kinematics      */
+    double J[MPPI_CHAIN_MAX_DOF];           /* joint armature (rotor inertia)             */
+    double b[MPPI_CHAIN_MAX_DOF];           /* joint viscous damping                      */
     double g;
 } mppi_chain_params;
 

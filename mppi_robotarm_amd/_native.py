@@ -50,7 +50,7 @@ CHAIN_MAX_DOF = 8
 
 
 class ChainParamsC(C.Structure):
-    _fields_ = [("n", C.c_int)] + [(f, C.c_double * CHAIN_MAX_DOF) for f in ("m", "l", "lc", "I", "fk")] + \
+    _fields_ = [("n", C.c_int)] + [(f, C.c_double * CHAIN_MAX_DOF) for f in ("m", "l", "lc", "I", "fk", "J", "b")] + \
                [("g", C.c_double)]
 
 

@@ -36,12 +36,17 @@ def _tup(v):
 class ChainParams:
     """Link constants of the chain ("extended sys_params.py").  Defaults: the
     config-5 arm — 7 uniform slender links of 1 kg, total reach 2 m (the 2-link
-    arm's l1 + l2), centre of mass at mid-link, I = m l^2 / 12."""
+    arm's l1 + l2), centre of mass at mid-link, I = m l^2 / 12, and joint drives
+    with 0.1 kg m^2 armature and 1 N m s / rad viscous damping (without them the
+    undamped 7-link chain collapses from its gravity-held pose and a few percent
+    of T = 128 rollouts overflow)."""
     m: tuple = _tup([1.0] * 7)
     l: tuple = _tup([2.0 / 7.0] * 7)
     lc: tuple = _tup([1.0 / 7.0] * 7)
     I: tuple = _tup([(2.0 / 7.0) ** 2 / 12.0] * 7)
     fk: tuple = _tup([2.0 / 7.0] * 7)
+    J: tuple = _tup([0.1] * 7)
+    b: tuple = _tup([1.0] * 7)
     g: float = 9.81
 
     @property
@@ -54,7 +59,7 @@ class ChainParams:
         from .params import ArmParams
         a = ArmParams() if arm is None else arm
         return ChainParams(m=(a.m1, a.m2), l=(a.l1, a.l2), lc=(a.lc1, a.lc2), I=(a.l1, a.l2),
-                           fk=(a.fk_l1, a.fk_l2), g=a.g)
+                           fk=(a.fk_l1, a.fk_l2), J=(0.0, 0.0), b=(0.0, 0.0), g=a.g)
 
 
 # Config-5 start pose: the end effector on xydq_circle.txt's first waypoint
@@ -112,7 +117,7 @@ class ChainEngine:
             cfg.stage_cost_weight[i] = float(stage_cost_weight[i])
             cfg.terminal_cost_weight[i] = float(terminal_cost_weight[i])
         cfg.chain.n = self.n
-        for f in ("m", "l", "lc", "I", "fk"):
+        for f in ("m", "l", "lc", "I", "fk", "J", "b"):
             arr = getattr(cfg.chain, f)
             for i, v in enumerate(getattr(chain, f)):
                 arr[i] = float(v)

@@ -56,7 +56,9 @@ struct ChainConst {
     int K_local, T, k_offset, k_exploit, nblocks, acquire, n, pad0;
     float dt;
     float mu[kCMax][kCMax];   // mu_ab (a != b), the constant part of D
-    float Dd[kCMax];          // D_aa = mu_aa + I_a (constant)
+    float Dd[kCMax];          // D'_aa = mu_aa + I_a + J_a + J_{a+1} (constant; J: joint armature)
+    float offj[kCMax];        // D'_{a,a+1} -= J_{a+1}
+    float damp[kCMax];        // joint viscous damping b_a
     float gnu[kCMax];         // g nu_a
     float fk[kCMax];          // cost kinematics lengths
     float sw[4], tw[4];       // stage / terminal weights x 10000
@@ -82,8 +84,9 @@ struct ChainState {
     }
 
     // One semi-implicit Euler step (oracle/chain_oracle.py chain_forward_dynamics):
-    //   D theta_ddot = tau - bias - g,  tau_a = v_a - v_{a+1},
-    //   D_ab = mu_ab cos(th_a - th_b) (+ I_a on the diagonal),
+    //   D' theta_ddot = tau - bias - g,  tau_a = v'_a - v'_{a+1},  v' = v - b dq,
+    //   D'_ab = mu_ab cos(th_a - th_b) (+ constants: I_a + J_a + J_{a+1} on the
+    //   diagonal, -J_{a+1} at (a, a+1): the joint armature in absolute angles),
     //   bias_a = sum_b mu_ab sin(th_a - th_b) thdot_b^2,  g_a = g nu_a cos th_a,
     //   q_ddot_a = theta_ddot_a - theta_ddot_{a-1};  dq += q_ddot dt;  q += dq dt.
     __device__ __forceinline__ void step(const float (&v)[N], const ChainConst& k) {
@@ -96,12 +99,14 @@ struct ChainState {
                 w[a] = acc * acc;   // thdot_a^2
             }
         }
-        float L[N][N];   // lower triangle: D, then its Cholesky factor in place
-        float r[N];
+        float L[N][N];   // lower triangle: D', then its Cholesky factor in place
+        float r[N], ve[N];
+#pragma unroll
+        for (int a = 0; a < N; ++a) ve[a] = fmaf(-k.damp[a], dq[a], v[a]);   // joint torque - damping
 #pragma unroll
         for (int a = 0; a < N; ++a) {
             L[a][a] = k.Dd[a];
-            r[a] = (a + 1 < N ? v[a] - v[a + 1] : v[a]) - k.gnu[a] * c[a];
+            r[a] = (a + 1 < N ? ve[a] - ve[a + 1] : ve[a]) - k.gnu[a] * c[a];
         }
 #pragma unroll
         for (int a = 0; a < N; ++a) {
@@ -110,7 +115,7 @@ struct ChainState {
                 const float cab = fmaf(c[a], c[b], s[a] * s[b]);   // cos(th_a - th_b)
                 const float sab = fmaf(s[a], c[b], -c[a] * s[b]);  // sin(th_a - th_b)
                 const float m = k.mu[a][b];
-                L[b][a] = m * cab;
+                L[b][a] = b == a + 1 ? fmaf(m, cab, -k.offj[a]) : m * cab;
                 const float ms = m * sab;
                 r[a] = fmaf(-ms, w[b], r[a]);   // - mu_ab sin(th_a - th_b) thdot_b^2
                 r[b] = fmaf(ms, w[a], r[b]);    // - mu_ba sin(th_b - th_a) thdot_a^2
@@ -232,7 +237,7 @@ __global__ __launch_bounds__(kCT) void chain_rollout_kernel(
         u_cur[ch] = ((flags & MPPI_FLAG_FUSED_UPDATE) && idx < T * N) ? st->u[idx / N][idx % N] : 0.0;
     }
     if (tid < kSlots) s_win[tid] = st->win[tid];
-    Search<1> sr;
+    Search<1, true> sr;   // precise keys: the config-5 start pose sits on a waypoint
     sr.load(st->key, st->ctr, 0);
     ChainState<N> x;
 #pragma unroll
@@ -646,7 +651,10 @@ int mppi_chain_ctx_create(const mppi_chain_config* cfg, int device, void* stream
         double tail = 0.0;
         for (int q = a + 1; q < n; ++q) tail += P.m[q];
         const double mu_aa = P.m[a] * P.lc[a] * P.lc[a] + P.l[a] * P.l[a] * tail;
-        k.Dd[a] = (float)(mu_aa + P.I[a]);
+        const double Jn = a + 1 < n ? P.J[a + 1] : 0.0;
+        k.Dd[a] = (float)(mu_aa + P.I[a] + P.J[a] + Jn);
+        k.offj[a] = (float)Jn;
+        k.damp[a] = (float)P.b[a];
         k.gnu[a] = (float)(P.g * (P.m[a] * P.lc[a] + P.l[a] * tail));
         k.fk[a] = (float)P.fk[a];
         for (int b = a + 1; b < n; ++b) {

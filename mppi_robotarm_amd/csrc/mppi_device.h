@@ -166,7 +166,17 @@ __device__ __forceinline__ float min_raw(float a, float b) {
 // bits so one v_min3 per two slots carries the argmin (first occurrence: equal
 // keys resolve to the lower slot); the LPS lanes of a sample split the window
 // and close the min with DPP.
-template <int LPS>
+//
+// Precision: packing quantises a key to 2^-18 of its magnitude, ~|r'|^2 (the
+// window's half-extent squared, ~5e-4 m^2 on xydq_circle.txt), so two
+// waypoints whose squared distances differ by less than ~1e-9 m^2 may resolve
+// to the lower slot.  PRECISE adds |p'|^2 to every key before packing (one
+// v_pk_add per two slots): the key is then the squared distance itself, the
+// quantisation acts on it, and what remains is the fp32 rounding of the key
+// (~1e-10 m^2).  The 2-link engine keeps the cheaper form (its parity on the
+// reference's fixtures is unaffected, +10 % instructions otherwise); the chain
+// engine, whose config-5 start pose sits ON a waypoint, uses PRECISE.
+template <int LPS, bool PRECISE = false>
 struct Search {
     static constexpr int SL = ((MPPI_SEARCH_LEN + LPS - 1) / LPS + 1) & ~1;  // slots per lane, even
     static constexpr int SP = SL / 2;
@@ -199,12 +209,16 @@ struct Search {
     }
 
     __device__ __forceinline__ unsigned nearest(float px, float py) const {
-        const float ax = -2.f * (px - cx), ay = -2.f * (py - cy);
+        const float dx = px - cx, dy = py - cy;
+        const float ax = -2.f * dx, ay = -2.f * dy;
         const f32x2 ax2 = {ax, ax}, ay2 = {ay, ay};
+        const float pp = fmaf(dx, dx, dy * dy);
+        const f32x2 pp2 = {pp, pp};
         float best = 3.0e38f;
 #pragma unroll
         for (int i = 0; i < SP; ++i) {
-            const f32x2 key = __builtin_elementwise_fma(ax2, krx[i], __builtin_elementwise_fma(ay2, kry[i], kc[i]));
+            f32x2 key = __builtin_elementwise_fma(ax2, krx[i], __builtin_elementwise_fma(ay2, kry[i], kc[i]));
+            if constexpr (PRECISE) key = key + pp2;   // |p - r_j|^2
             const unsigned j = (unsigned)(sub * SL + 2 * i);
             const float k0 = __uint_as_float((__float_as_uint(key.x) & ~31u) | j);
             const float k1 = __uint_as_float((__float_as_uint(key.y) & ~31u) | (j + 1));
@@ -346,9 +360,11 @@ __device__ __forceinline__ void put_final(double rho, const double (&acc)[MAXCH]
 // with DPP and evaluates the s_i itself; the s_i reach the column FMAs as
 // scalars (v_readlane) — no LDS traffic and no barrier per round.
 //
-// !GRAN: 8-B sc1 words behind an arrival counter; every load of a round —
-//   rho, eta and all (row, column chunk) entries — is issued together (one
-//   memory round trip per round of 32 / MAXCH rows).
+// !GRAN: 8-B sc1 words behind an arrival counter.  With one column chunk
+//   (MAXCH = 1) every load of a round — rho, eta and all entries of 32 rows —
+//   is issued together (one memory round trip per round); with more chunks the
+//   rounds are structured exactly as GRAN's (below) with plain sc1 loads, so
+//   both hand-off forms rescale and accumulate identically (same bits).
 // GRAN: 16-B tagged granules polled until every tag matches `tag`: rho first,
 //   one lane per row (16 rows per round), then eta and the entries of only the
 //   rows that carry weight, 16 / MAXCH rows per load batch.
@@ -359,9 +375,10 @@ __device__ __forceinline__ void merge_rows_block(__amdgpu_buffer_rsrc_t rows, in
                                                  double inv_lambda, SM& sm, const __amdgpu_buffer_rsrc_t* out_wt,
                                                  int out_idx, double* out_row, double* w_eps_out, unsigned tag,
                                                  unsigned* tmo) {
-    constexpr int LB = GRAN ? 16 : 32;          // loads per batch per thread
+    constexpr bool EAGER = !GRAN && MAXCH == 1;  // one round trip per round of 32 rows
+    constexpr int LB = EAGER ? 32 : 16;         // loads per batch per thread
     constexpr int RB = LB / MAXCH;              // rows per load batch
-    constexpr int R1 = GRAN ? 16 : RB;          // rows per round
+    constexpr int R1 = EAGER ? 32 : 16;         // rows per round
     static_assert(RB >= 1 && R1 <= 64, "one row per lane");
     const int tid = threadIdx.x, lane = tid & 63;
     const int stride = geo.stride, ncol = geo.ncol;
@@ -373,7 +390,7 @@ __device__ __forceinline__ void merge_rows_block(__amdgpu_buffer_rsrc_t rows, in
         const int nr = min(R1, n - r0);   // uniform
         const int rb = row0 + r0;
         const int lrow = lane < nr ? (rb + lane) * stride : kOffRange;
-        double rho_r, eta_l = 0.0, v[GRAN ? 1 : LB];
+        double rho_r, eta_l = 0.0, v[EAGER ? LB : 1];
         if constexpr (GRAN) {
             u32x4 gr;
             for (unsigned spins = 0;; ++spins) {
@@ -383,6 +400,8 @@ __device__ __forceinline__ void merge_rows_block(__amdgpu_buffer_rsrc_t rows, in
                 MPPI_SPIN_OR_GIVE_UP(spins, tmo, lane);
             }
             rho_r = gran_val(gr);
+        } else if constexpr (!EAGER) {
+            rho_r = ld_wt(rows, lrow);
         } else {
             rho_r = ld_wt(rows, lrow);
             eta_l = ld_wt(rows, lrow + 1);
@@ -409,7 +428,7 @@ __device__ __forceinline__ void merge_rows_block(__amdgpu_buffer_rsrc_t rows, in
             eta *= f;
         }
         rho = rnew;
-        if constexpr (!GRAN) {
+        if constexpr (EAGER) {
 #pragma unroll
             for (int j = 0; j < LB; ++j) {
                 const int i = j / MAXCH, ch = j % MAXCH;
@@ -425,29 +444,45 @@ __device__ __forceinline__ void merge_rows_block(__amdgpu_buffer_rsrc_t rows, in
             // lane k < nrr: the round's k-th weighted row (ascending)
             const int krow = lane < nrr ? select_bit(rel, lane) : 0;
             for (int b0 = 0; b0 < nrr; b0 += RB) {
-                u32x4 ge, gv[LB];
-                for (unsigned spins = 0;; ++spins) {
-                    asm volatile("" ::: "memory");
-                    ge = ld_gran(rows, (b0 == 0 && lane < nrr) ? (rb + krow) * stride + 1 : kOffRange);
-                    bool ok = !(b0 == 0 && lane < nrr) || gran_ok(ge, tag);
+                const bool eta_on = b0 == 0 && lane < nrr;
+                const int eidx = eta_on ? (rb + krow) * stride + 1 : kOffRange;
+                double x[LB];
+                if constexpr (GRAN) {
+                    u32x4 ge, gv[LB];
+                    for (unsigned spins = 0;; ++spins) {
+                        asm volatile("" ::: "memory");
+                        ge = ld_gran(rows, eidx);
+                        bool ok = !eta_on || gran_ok(ge, tag);
+#pragma unroll
+                        for (int j = 0; j < LB; ++j) {
+                            const int i = b0 + j / MAXCH, col = tid + (j % MAXCH) * NT;
+                            const bool on = i < nrr && col < ncol;
+                            gv[j] = ld_gran(rows, on ? (rb + __builtin_amdgcn_readlane(krow, i)) * stride + 1 + col
+                                                     : kOffRange);
+                            ok = ok && (!on || gran_ok(gv[j], tag));
+                        }
+                        if (__all(ok)) break;
+                        MPPI_SPIN_OR_GIVE_UP(spins, tmo, lane);
+                    }
+                    if (b0 == 0) eta_l = gran_val(ge);
+#pragma unroll
+                    for (int j = 0; j < LB; ++j) x[j] = gran_val(gv[j]);
+                } else {
+                    if (b0 == 0) eta_l = ld_wt(rows, eidx);
 #pragma unroll
                     for (int j = 0; j < LB; ++j) {
                         const int i = b0 + j / MAXCH, col = tid + (j % MAXCH) * NT;
-                        const bool on = i < nrr && col < ncol;
-                        gv[j] = ld_gran(rows, on ? (rb + __builtin_amdgcn_readlane(krow, i)) * stride + 1 + col
-                                                 : kOffRange);
-                        ok = ok && (!on || gran_ok(gv[j], tag));
+                        x[j] = ld_wt(rows, (i < nrr && col < ncol)
+                                               ? (rb + __builtin_amdgcn_readlane(krow, i)) * stride + 1 + col
+                                               : kOffRange);
                     }
-                    if (__all(ok)) break;
-                    MPPI_SPIN_OR_GIVE_UP(spins, tmo, lane);
                 }
-                if (b0 == 0) eta_l = gran_val(ge);
 #pragma unroll
                 for (int j = 0; j < LB; ++j) {
                     const int i = b0 + j / MAXCH, ch = j % MAXCH;
                     if (i < nrr) {
                         const double s = readlane_f64(s_l, __builtin_amdgcn_readlane(krow, i));
-                        acc[ch] = fma(s, gran_val(gv[j]), acc[ch]);
+                        acc[ch] = fma(s, x[j], acc[ch]);
                         if (ch == 0) eta = fma(s, readlane_f64(eta_l, i), eta);
                     }
                 }

@@ -22,23 +22,26 @@
 
 typedef struct {
     int n;
-    double mu[CH_MAX][CH_MAX], nu[CH_MAX], Dd[CH_MAX], fk[CH_MAX], g;
+    double mu[CH_MAX][CH_MAX], nu[CH_MAX], Dd[CH_MAX], fk[CH_MAX], J[CH_MAX], b[CH_MAX], g;
 } chain_model;
 
-/* chain[] = m[n], l[n], lc[n], I[n], fk[n], g  (chain_oracle.py ChainParams) */
+/* chain[] = m[n], l[n], lc[n], I[n], fk[n], J[n], b[n], g  (chain_oracle.py ChainParams) */
 static int chain_setup(chain_model *M, const double *chain, int n) {
     if (n < 1 || n > CH_MAX) return -1;
     const double *m = chain, *l = chain + n, *lc = chain + 2 * n, *I = chain + 3 * n, *fk = chain + 4 * n;
+    const double *J = chain + 5 * n, *b = chain + 6 * n;
     memset(M, 0, sizeof(*M));
     M->n = n;
-    M->g = chain[5 * n];
+    M->g = chain[7 * n];
     for (int a = 0; a < n; ++a) {
         double tail = 0.0;
         for (int k = a + 1; k < n; ++k) tail += m[k];
         M->mu[a][a] = m[a] * lc[a] * lc[a] + l[a] * l[a] * tail;
         M->nu[a] = m[a] * lc[a] + l[a] * tail;
-        M->Dd[a] = M->mu[a][a] + I[a];
+        M->Dd[a] = M->mu[a][a] + I[a] + J[a] + (a + 1 < n ? J[a + 1] : 0.0);  /* + S^-T diag(J) S^-1 */
         M->fk[a] = fk[a];
+        M->J[a] = J[a];
+        M->b[a] = b[a];
         for (int b = a + 1; b < n; ++b) {
             double tb = 0.0;
             for (int k = b + 1; k < n; ++k) tb += m[k];
@@ -67,10 +70,12 @@ static void chain_step(double *x, const double *v, double dt, const chain_model 
             if (b == a) continue;
             const double cab = c[a] * c[b] + s[a] * s[b]; /* cos(th_a - th_b) */
             const double sab = s[a] * c[b] - c[a] * s[b]; /* sin(th_a - th_b) */
-            D[a][b] = M->mu[a][b] * cab;
+            D[a][b] = M->mu[a][b] * cab - (b == a + 1 ? M->J[b] : 0.0) - (a == b + 1 ? M->J[a] : 0.0);
             bias += M->mu[a][b] * sab * thd[b] * thd[b];
         }
-        const double tau = v[a] - (a + 1 < n ? v[a + 1] : 0.0);
+        const double va = v[a] - M->b[a] * x[n + a];                      /* joint torque - damping */
+        const double vn = a + 1 < n ? v[a + 1] - M->b[a + 1] * x[n + a + 1] : 0.0;
+        const double tau = va - vn;
         r[a] = tau - bias - M->g * M->nu[a] * c[a];
     }
     /* Cholesky D = L L^T (in place, lower), then L y = r, L^T z = y */

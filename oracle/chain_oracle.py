@@ -20,11 +20,15 @@ triangular ones, so theta_a = q_1 + ... + q_a):
   mu_aa           = m_a lc_a^2 + l_a^2 sum_{k>a} m_k
   bias            c_a = sum_b mu_ab sin(theta_a - theta_b) theta_dot_b^2
   gravity         g_a = g nu_a cos theta_a,  nu_a = m_a lc_a + l_a sum_{k>a} m_k
-  joint torques   u map to theta-space as tau_a = u_a - u_{a+1}  (u_{n+1} = 0)
-  D theta_ddot = tau - c - g;  q_ddot_1 = theta_ddot_1, q_ddot_a = theta_ddot_a - theta_ddot_{a-1}
+  joint drives    armature (rotor inertia) J_a and viscous damping b_a per joint: the
+                  joint-space mass matrix S^T D S + diag(J) is, in theta-space,
+                  D' = D + S^-T diag(J) S^-1  (diagonal + J_a + J_{a+1}, first
+                  off-diagonal - J_{a+1}); the joint torques are u - b dq
+  joint torques   u' = u - b dq map to theta-space as tau_a = u'_a - u'_{a+1}  (u'_{n+1} = 0)
+  D' theta_ddot = tau - c - g;  q_ddot_1 = theta_ddot_1, q_ddot_a = theta_ddot_a - theta_ddot_{a-1}
   semi-implicit Euler as control.py:256-259: dq += q_ddot dt; q += dq dt
 
-(At n = 2: M = S^T D S gives M11 = m1 lc1^2 + m2 l1^2 + I1 + 2 m2 l1 lc2 c2 + m2 lc2^2 + I2,
+(At n = 2 with J = b = 0: M = S^T D S gives M11 = m1 lc1^2 + m2 l1^2 + I1 + 2 m2 l1 lc2 c2 + m2 lc2^2 + I2,
 M12 = m2 l1 lc2 c2 + m2 lc2^2 + I2, M22 = m2 lc2^2 + I2 — control.py:241-245 with I = l.)
 
 Cost: end-effector (x, y) from forward kinematics with the fk
@@ -57,6 +61,8 @@ class ChainParams:
     lc: tuple = _default([1.0 / 7.0] * 7)
     I: tuple = _default([(2.0 / 7.0) ** 2 / 12.0] * 7)   # slender rods, m l^2 / 12
     fk: tuple = _default([2.0 / 7.0] * 7)                # lengths used by the cost's kinematics
+    J: tuple = _default([0.1] * 7)                       # joint armature (rotor inertia), kg m^2
+    b: tuple = _default([1.0] * 7)                       # joint viscous damping, N m s / rad
     g: float = 9.81
 
     @property
@@ -67,11 +73,11 @@ class ChainParams:
     def from_arm2(a: O.ArmParams = O.ArmParams()) -> "ChainParams":
         """The reference 2-link model (control.py:11-18, 241-245): inertia := link length."""
         return ChainParams(m=(a.m1, a.m2), l=(a.l1, a.l2), lc=(a.lc1, a.lc2), I=(a.l1, a.l2),
-                           fk=(a.fk_l1, a.fk_l2), g=a.g)
+                           fk=(a.fk_l1, a.fk_l2), J=(0.0, 0.0), b=(0.0, 0.0), g=a.g)
 
 
 def coefficients(P: ChainParams):
-    """(mu n x n, nu n, D diagonal n): the constant parts of D and gravity."""
+    """(mu n x n, nu n, D' diagonal n): the constant parts of D' and gravity."""
     n = P.n
     m, l, lc = map(np.asarray, (P.m, P.l, P.lc))
     tail = np.array([m[k + 1:].sum() for k in range(n)])        # sum_{k>a} m_k
@@ -81,7 +87,8 @@ def coefficients(P: ChainParams):
         for b in range(a + 1, n):
             mu[a, b] = mu[b, a] = l[a] * (m[b] * lc[b] + l[b] * tail[b])
     nu = m * lc + l * tail
-    return mu, nu, np.diag(mu) + np.asarray(P.I)
+    J = np.asarray(P.J, dtype=np.float64)
+    return mu, nu, np.diag(mu) + np.asarray(P.I) + J + np.append(J[1:], 0.0)
 
 
 def chain_forward_dynamics(q, dq, v, dt, P: ChainParams):
@@ -93,9 +100,13 @@ def chain_forward_dynamics(q, dq, v, dt, P: ChainParams):
     D = mu * np.cos(dth)
     idx = np.arange(P.n)
     D[..., idx, idx] = Dd
+    J = np.asarray(P.J, dtype=np.float64)
+    D[..., idx[:-1], idx[1:]] -= J[1:]
+    D[..., idx[1:], idx[:-1]] -= J[1:]
     c = np.einsum("ab,...ab,...b->...a", mu, np.sin(dth), thd ** 2)
     gt = P.g * nu * np.cos(th)
-    tau = v - np.concatenate([v[..., 1:], np.zeros(v.shape[:-1] + (1,))], axis=-1)
+    ve = v - np.asarray(P.b) * dq
+    tau = ve - np.concatenate([ve[..., 1:], np.zeros(ve.shape[:-1] + (1,))], axis=-1)
     thdd = np.linalg.solve(D, (tau - c - gt)[..., None])[..., 0]
     qdd = np.diff(thdd, axis=-1, prepend=0.0)
     dq_n = dq + qdd * dt

@@ -73,7 +73,7 @@ def rollout_costs(x0, u, eps, window, dt, lam, alpha, sigma, stage_w, term_w, ar
     k0, k1 = (0, K) if k_range is None else k_range
     k_exploit = K if k_exploit is None else k_exploit
     S = np.zeros(k1 - k0)
-    win = np.ascontiguousarray(window, dtype=np.float64)
+    win = np.ascontiguousarray(np.asarray(window, dtype=np.float64)[:, :4])  # rows [x, y, dq1, dq2]
     rc = lib().oracle_rollout_costs_f64(
         np.ascontiguousarray(x0, np.float64), np.ascontiguousarray(u, np.float64), eps, sk, st,
         k0, k1, T, win, win.shape[0], dt, lam, alpha,
@@ -106,8 +106,8 @@ def max_threads() -> int:
 # ---------------------------------------------------------------- n-link chain
 
 def chain_array(P) -> np.ndarray:
-    """ChainParams -> m[n], l[n], lc[n], I[n], fk[n], g (chain_oracle.c chain_setup)."""
-    return np.concatenate([P.m, P.l, P.lc, P.I, P.fk, [P.g]]).astype(np.float64)
+    """ChainParams -> m[n], l[n], lc[n], I[n], fk[n], J[n], b[n], g (chain_oracle.c chain_setup)."""
+    return np.concatenate([P.m, P.l, P.lc, P.I, P.fk, P.J, P.b, [P.g]]).astype(np.float64)
 
 
 def _chain_strides(eps, layout):
@@ -126,7 +126,7 @@ def chain_rollout_costs(x0, u, eps, window, dt, lam, alpha, sigma, stage_w, term
     k0, k1 = (0, K) if k_range is None else k_range
     k_exploit = K if k_exploit is None else k_exploit
     S = np.zeros(k1 - k0)
-    win = np.ascontiguousarray(window, dtype=np.float64)
+    win = np.ascontiguousarray(np.asarray(window, dtype=np.float64)[:, :4])  # rows [x, y, dq1, dq2]
     rc = lib().oracle_chain_rollout_costs_f64(
         np.ascontiguousarray(x0, np.float64), np.ascontiguousarray(u, np.float64), eps, sk, st, sd, k0, k1, T, n,
         win, win.shape[0], dt, lam, alpha, np.ascontiguousarray(np.linalg.inv(sigma), np.float64),

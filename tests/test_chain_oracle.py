@@ -84,3 +84,19 @@ def test_gravity_torque_holds_the_chain():
 def test_c5_start_pose_is_on_the_path(paths):
     x, y = CO.chain_fk(np.array([1.481492] + [-0.320757] * 6), P7)
     assert np.hypot(x - paths["xydq_circle"][0, 0], y - paths["xydq_circle"][0, 1]) < 1e-5
+
+
+def test_theta_space_dynamics_equal_the_joint_space_equations():
+    """D' (with the armature) and tau (with the damping) in absolute angles give the
+    accelerations of M q_ddot = u - b dq - S^T (c + g), M = S^T D S + diag(J)."""
+    rng = np.random.default_rng(2)
+    q, dq, v = rng.normal(0, 1, 7), rng.normal(0, 2, 7), rng.normal(0, 5, 7)
+    mu, nu, _ = CO.coefficients(CO.ChainParams(J=(0.0,) * 7, b=(0.0,) * 7))
+    th, thd = np.cumsum(q), np.cumsum(dq)
+    D = mu * np.cos(th[:, None] - th[None, :])
+    np.fill_diagonal(D, np.diag(mu) + np.asarray(P7.I))
+    S = np.tril(np.ones((7, 7)))
+    M = S.T @ D @ S + np.diag(P7.J)
+    rhs = v - np.asarray(P7.b) * dq - S.T @ ((mu * np.sin(th[:, None] - th[None, :])) @ thd ** 2 + P7.g * nu * np.cos(th))
+    qn, dqn = CO.chain_forward_dynamics(q[None], dq[None], v[None], 0.006, P7)
+    np.testing.assert_allclose((dqn[0] - dq) / 0.006, np.linalg.solve(M, rhs), rtol=1e-10, atol=1e-10)

@@ -1,0 +1,217 @@
+"""GPU: the n-link chain engine (BASELINE config 5) through the C ABI.
+
+Parity anchors:
+  * n = 2 with the reference constants (inertia := length, no armature or
+    damping) through the chain kernel reproduces the reference's golden steps
+    (control.py:67-152) — same tolerances as tests/test_gpu_parity.py;
+  * n = 7 (build-defined model, parity unpinned by the reference) against the
+    fp64 C chain oracle (oracle/chain_oracle.c, itself checked against the NumPy
+    restatement and, at n = 2, the reference).
+
+Tolerances at n = 7 (fp32 device vs fp64 oracle): the weighted noise / control
+within 1e-4 of max(|.|, 1) (BASELINE.json); the same argmin; S at the 99th
+percentile within 2e-5 at T <= 8, 5e-4 at T = 32 and 1e-3 at T = 128 (measured
+~3e-6, ~1e-4, ~1e-4: the 7-link chain amplifies fp32 rounding over the horizon;
+1e-5 when the exact control-cost term dominates S, lambda = 1e9); and at most
+1 % of samples beyond 1e-3.  That 1 %
+is the nearest-waypoint tie rate: xydq_circle.txt starts with waypoints 6e-5 m
+apart whose dq columns step by ~2e-3, and one fp32 step rounds the joint angles
+to ~2e-7 rad, so in ~0.2 % of sample-steps the fp32 end effector lies across
+the bisector of two waypoints from the fp64 one and picks the neighbour (the
+same with OCML sincosf: measured, tools/chain_cost_check.py).
+"""
+import numpy as np
+import pytest
+
+torch = pytest.importorskip("torch")
+pytestmark = pytest.mark.gpu
+
+import chain_oracle as CO  # noqa: E402
+import coracle  # noqa: E402
+from conftest import STEP_FIXTURES, load_step  # noqa: E402
+
+U_TOL = 1e-4
+S_TOL = 5e-5
+W, TW = [0.5, 0.5, 5.0, 5.0], [5.0, 5.0, 50.0, 50.0]
+
+
+@pytest.fixture(scope="module", autouse=True)
+def _gpu():
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    torch.cuda.set_device(0)
+
+
+def _urel(a, b):
+    return float(np.max(np.abs(a - b)) / max(1.0, float(np.max(np.abs(b)))))
+
+
+def _c5():
+    from mppi_robotarm_amd.chain import CHAIN7_SIGMA, CHAIN7_X0, ChainParams, gravity_torque
+    return ChainParams(), CHAIN7_X0, CHAIN7_SIGMA, gravity_torque(CHAIN7_X0[:7])
+
+
+def _engine(K, T, lam=100.0, **kw):
+    from mppi_robotarm_amd.chain import ChainEngine
+    P, _, sig, _ = _c5()
+    return ChainEngine(K, T, 0.006, lam, 0.98, sig, W, TW, kw.pop("expl", 0.0), kw.pop("chain", P), device=0, **kw)
+
+
+@pytest.mark.parametrize("name", STEP_FIXTURES)
+def test_chain_at_n2_reproduces_reference_steps(name, paths):
+    from mppi_robotarm_amd.chain import ChainMPPIController, ChainParams
+    g = load_step(name)
+    c = ChainMPPIController(float(g["delta_t"]), paths[str(g["path"])], int(g["T"]), int(g["K"]),
+                            float(g["param_exploration"]), float(g["param_lambda"]), float(g["param_alpha"]),
+                            g["sigma"], g["stage_cost_weight"], g["terminal_cost_weight"],
+                            visualze_sampled_trajs="sampled_traj" in g, chain=ChainParams.from_arm2(),
+                            u_init=g["u_prev"])
+    c.prev_waypoints_idx = int(g["prev_idx"])
+    eps = g["eps"].astype(np.float64)
+    c._calc_epsilon = lambda *a, **k: eps
+    c.keep_costs = True
+    u0, u_seq, opt, samp = c.calc_control_input(g["x0"])
+    S = c.last_S
+    assert int(np.argmin(S)) == int(np.argmin(g["S"]))
+    assert float(np.max(np.abs(S - g["S"]) / np.abs(g["S"]))) < S_TOL
+    assert _urel(u_seq, g["u_seq"]) < U_TOL
+    assert c.prev_waypoints_idx == int(g["prev_idx_after"])
+    np.testing.assert_allclose(opt, g["optimal_traj"], rtol=1e-4, atol=1e-4)   # dim_x = 4 at n = 2
+    if "sampled_traj" in g:
+        np.testing.assert_allclose(samp, g["sampled_traj"], rtol=1e-4, atol=1e-4)
+    c.close()
+
+
+@pytest.mark.parametrize("K,T,lam,s99", [(4096, 32, 100.0, 5e-4), (4096, 32, 1.0e9, 1e-5),
+                                        (131072, 128, 100.0, 1e-3), (3000, 7, 100.0, 2e-5)])
+def test_chain_n7_against_c_oracle(K, T, lam, s99, paths):
+    """Config 5 (K=131072 T=128) and smaller shapes: S and the weighted noise vs fp64."""
+    P, x0, sig, ug = _c5()
+    eng = _engine(K, T, lam)
+    win = paths["xydq_circle"][:30]
+    u = np.tile(ug, (T, 1)) + np.random.default_rng(4).normal(0, 0.3, (T, 7))
+    eng.set_step_inputs(x0, win, u)
+    noise = eng.philox_noise(11, 2)
+    S_dev = torch.empty(K, dtype=torch.float64, device="cuda")
+    eng.rollout(noise, S_out=S_dev)
+    w = eng.weighted_noise()
+    S = S_dev.cpu().numpy()
+    nz = noise.cpu().numpy()
+    Sr = coracle.chain_rollout_costs(x0, u, nz, win, 0.006, lam, 0.98, sig, W, TW, CO.ChainParams(), layout="TNK")
+    _, wr = coracle.chain_weighted_noise(Sr, nz, lam, layout="TNK")
+    rel = np.abs(S - Sr) / np.abs(Sr)
+    assert np.all(np.isfinite(S))
+    assert int(np.argmin(S)) == int(np.argmin(Sr))
+    assert float(np.percentile(rel, 99)) < s99
+    assert float(np.mean(rel > 1e-3)) < 0.01
+    assert _urel(w, wr) < U_TOL
+    eng.close()
+
+
+def _fused(eng, paths, noises, u0):
+    from mppi_robotarm_amd.chain import CHAIN7_X0
+    eng.set_step_inputs(CHAIN7_X0, paths["xydq_circle"][2:32], u0)
+    out = []
+    for nz in noises:
+        eng.rollout(nz, fused_update=True)
+        out.append((eng.weighted_noise(), eng.nominal()))
+    return out
+
+
+@pytest.mark.parametrize("lam", [100.0, 1.0e9])
+def test_chain_handoff_forms_are_bit_identical(lam, paths, monkeypatch):
+    K, T = 32768, 48
+    _, _, _, ug = _c5()
+    runs = {}
+    for form in ("poll", "counter"):
+        if form == "counter":
+            monkeypatch.setenv("MPPI_HANDOFF", "counter")
+        eng = _engine(K, T, lam)
+        assert eng.handoff == form
+        noises = [eng.philox_noise(5, s) for s in range(3)]
+        runs[form] = _fused(eng, paths, noises, np.tile(ug, (T, 1)))
+        eng.close()
+    for (wp, up), (wc, uc) in zip(runs["poll"], runs["counter"]):
+        assert np.array_equal(wp, wc) and np.array_equal(up, uc)
+
+
+def test_chain_fused_update_matches_host_update(paths):
+    from scipy.ndimage import median_filter
+    K, T = 8192, 40
+    _, _, _, ug = _c5()
+    u = np.tile(ug, (T, 1)) + np.random.default_rng(1).normal(0, 0.5, (T, 7))
+    eng = _engine(K, T, 1.0e6)
+    noise = eng.philox_noise(9, 0)
+    from mppi_robotarm_amd.chain import CHAIN7_X0
+    eng.set_step_inputs(CHAIN7_X0, paths["xydq_circle"][:30], u)
+    eng.rollout(noise)
+    w = eng.weighted_noise()
+    filt = np.stack([median_filter(w[:, d], size=10, mode="reflect") for d in range(7)], 1)
+    un = u + filt
+    expect = np.vstack([un[1:], un[-1:]])                       # control.py:148-149
+    eng.set_step_inputs(CHAIN7_X0, paths["xydq_circle"][:30], u)
+    eng.rollout(noise, fused_update=True)
+    np.testing.assert_allclose(eng.nominal(), expect, rtol=1e-12, atol=1e-12)
+    eng.close()
+
+
+def test_chain_shards_and_device_merge(paths):
+    """Virtual shards (Philox slices of the unsharded draw) + device merge == unsharded."""
+    K, T, G = 12288, 24, 3
+    _, x0, _, ug = _c5()
+    u = np.tile(ug, (T, 1))
+    full = _engine(K, T, 1.0e7)
+    full.set_step_inputs(x0, paths["xydq_circle"][:30], u)
+    noise = full.philox_noise(21, 4)
+    full.rollout(noise)
+    w_full = full.weighted_noise()
+    Kl = K // G
+    parts = torch.empty(G * full.partial_len, dtype=torch.float64, device="cuda")
+    engs = []
+    for g in range(G):
+        e = _engine(Kl, T, 1.0e7, K_total=K, k_offset=g * Kl)
+        e.set_step_inputs(x0, paths["xydq_circle"][:30], u)
+        nz = e.philox_noise(21, 4)
+        assert torch.equal(nz, noise[:, :, g * Kl:(g + 1) * Kl])
+        e.rollout(nz, partial_out=parts[g * e.partial_len:(g + 1) * e.partial_len])
+        engs.append(e)
+    engs[0].merge(parts, G)
+    np.testing.assert_allclose(engs[0].weighted_noise(), w_full, rtol=1e-10, atol=1e-12)
+    for e in engs + [full]:
+        e.close()
+
+
+def test_chain_philox_noise_has_covariance_sigma():
+    K, T = 65536, 4
+    _, _, sig, _ = _c5()
+    eng = _engine(K, T)
+    z = eng.philox_noise(3, 0).cpu().numpy()                    # (T, 7, K)
+    x = z.transpose(0, 2, 1).reshape(-1, 7).astype(np.float64)
+    assert np.max(np.abs(x.mean(0))) < 0.05
+    cov = np.cov(x.T)
+    np.testing.assert_allclose(cov, sig, atol=0.1 * np.sqrt(np.outer(np.diag(sig), np.diag(sig))).max() / 4)
+    eng.close()
+
+
+def test_chain_trajectories_match_oracle(paths):
+    K, T = 64, 20
+    P, x0, _, ug = _c5()
+    eng = _engine(K, T)
+    u = np.tile(ug, (T, 1))
+    eng.set_step_inputs(x0, paths["xydq_circle"][:30], u)
+    noise = eng.philox_noise(2, 0)
+    tr = eng.trajectories(base_u=u, noise=noise).double().cpu().numpy()
+    nz = noise.cpu().numpy()
+    ctrl = np.roll(u[None] + nz.transpose(2, 0, 1), 1, axis=1)    # control(t) = u[t-1] + eps[t-1]
+    ref = coracle.chain_traj(x0, ctrl, 0.006, CO.ChainParams())
+    np.testing.assert_allclose(tr, ref, rtol=1e-4, atol=1e-4)
+    eng.close()
+
+
+def test_chain_errors():
+    from mppi_robotarm_amd.chain import ChainEngine, ChainParams
+    with pytest.raises(np.linalg.LinAlgError):
+        ChainEngine(256, 8, 0.006, 100.0, 0.98, -np.eye(7), W, TW, device=0)
+    with pytest.raises(ValueError):
+        ChainEngine(256, 8, 0.006, 100.0, 0.98, np.eye(8), W, TW, chain=ChainParams(*(tuple([1.0] * 8),) * 7),
+                    device=0)

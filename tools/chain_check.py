@@ -48,7 +48,7 @@ for name in STEP_FIXTURES:
 K = int(sys.argv[1]) if len(sys.argv) > 1 else 131072
 T = int(sys.argv[2]) if len(sys.argv) > 2 else 128
 P7 = ChainParams()
-for (Kc, Tc, lam) in [(4096, 32, 100.0), (4096, 32, 1e9), (K, T, 100.0)]:
+for (Kc, Tc, lam) in [(4096, 8, 100.0), (4096, 32, 100.0), (4096, 32, 1e9), (K, T, 100.0)]:
     eng = ChainEngine(Kc, Tc, 0.006, lam, 0.98, CHAIN7_SIGMA, W, TW, 0.0, P7, device=0)
     u = np.tile(gravity_torque(CHAIN7_X0[:7], P7), (Tc, 1))
     win = paths["xydq_circle"][:30]
