@@ -17,6 +17,11 @@ xydq_circle.txt, noise N(0, Sigma) from the device Philox generator, 10
 distinct buffers rotated so their total (335 MB at K=65536 T=64) exceeds the
 256 MiB Infinity Cache.  Everything is resident in HBM before timing starts.
 
+``--workload c5``: BASELINE config 5 instead — the 7-DoF chain
+(mppi_robotarm_amd/chain.py, build-defined model) at K=131072 T=128, strong
+scaling (K fixed, split over the ranks), 28 B of noise per state-step, the
+config-5 start pose on xydq_circle.txt and gravity-holding nominal torques.
+
 Prints ONE JSON line on rank 0.
 """
 from __future__ import annotations
@@ -39,6 +44,7 @@ from mppi_robotarm_amd.params import ArmParams, X0_RUNPY  # noqa: E402
 
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md, chip-level parameters)
 BYTES_PER_STATE_STEP = 8  # fp32 eps[t][k][0:2] read once
+C5_BYTES_PER_STATE_STEP = 28  # fp32 eps[t][0:7][k] read once ("C5 (du=7): 28 B/state-step")
 
 
 def parse():
@@ -46,12 +52,15 @@ def parse():
     p.add_argument("--gpus", type=int, default=1)
     p.add_argument("--steps", type=int, default=200)
     p.add_argument("--warmup", type=int, default=20)
-    p.add_argument("--K", type=int, default=65536, help="samples per GPU")
-    p.add_argument("--T", type=int, default=64)
-    p.add_argument("--nbuf", type=int, default=10, help="rotated noise buffers")
+    p.add_argument("--workload", choices=("c3", "c5"), default="c3",
+                   help="c3: 2-DoF arm, K per GPU (BASELINE metric); c5: 7-DoF chain, K total (config 5)")
+    p.add_argument("--K", type=int, default=None, help="c3: samples per GPU (65536); c5: samples in total (131072)")
+    p.add_argument("--T", type=int, default=None, help="horizon (c3: 64, c5: 128)")
+    p.add_argument("--nbuf", type=int, default=None, help="rotated noise buffers (c3: 10, c5: 4)")
     p.add_argument("--lps", type=int, default=0, help="lanes per sample (0 = auto)")
     p.add_argument("--cpu-seconds", type=float, default=10.0, help="CPU baseline budget (0 = skip)")
-    p.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "traffic.json"))
+    p.add_argument("--traffic-json", default=None,
+                   help="measured HBM bytes per launch (default profiles/traffic.json, c5: profiles/traffic_c5.json)")
     p.add_argument("--launch", choices=("eager", "graph"), default="eager",
                    help="N = 1: back-to-back launches from the host loop (default) or replay of a captured HIP graph")
     p.add_argument("--backend", default="nccl", help="torch.distributed backend for N > 1 (nccl = RCCL)")
@@ -83,8 +92,40 @@ def cpu_baseline(args, window, x0, u):
                       f"C fp64 restatement oracle/mppi_oracle.c, OpenMP, {el:.1f} s"}
 
 
+def cpu_baseline_c5(args, window, x0, u, K, T):
+    """C chain oracle (OpenMP over samples) on the host cores, rank 0, N = 1."""
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import chain_oracle
+    import coracle  # checker / baseline only
+    from mppi_robotarm_amd.chain import CHAIN7_SIGMA
+    rng = np.random.default_rng(7)
+    eps = (rng.standard_normal((T, 7, K)) * np.sqrt(np.diag(CHAIN7_SIGMA))[None, :, None]).astype(np.float32)
+    t0 = time.perf_counter()
+    n = 0
+    while True:
+        S = coracle.chain_rollout_costs(x0, u, eps, window, 0.006, 100.0, 0.98, CHAIN7_SIGMA, [0.5, 0.5, 5.0, 5.0],
+                                        [5.0, 5.0, 50.0, 50.0], chain_oracle.ChainParams(), layout="TNK")
+        coracle.chain_weighted_noise(S, eps, 100.0, layout="TNK")
+        n += 1
+        el = time.perf_counter() - t0
+        if el >= args.cpu_seconds:
+            break
+    return {"value": K * T * n / el, "unit": "state-steps/s", "cores": coracle.max_threads(), "kind": "port",
+            "sample": f"{n} full steps of K={K} T={T} (7-link rollout+cost+softmin+weighted noise), C fp64 "
+                      f"restatement oracle/chain_oracle.c, OpenMP, {el:.1f} s"}
+
+
 def main():
     args = parse()
+    c5 = args.workload == "c5"
+    if args.K is None:
+        args.K = 131072 if c5 else 65536
+    if args.T is None:
+        args.T = 128 if c5 else 64
+    if args.nbuf is None:
+        args.nbuf = 4 if c5 else 10
+    if args.traffic_json is None:
+        args.traffic_json = os.path.join(ROOT, "profiles", "traffic_c5.json" if c5 else "traffic.json")
     rank = int(os.environ.get("RANK", "0"))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
@@ -96,15 +137,26 @@ def main():
             dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
         else:
             dist.init_process_group(args.backend)
-    K, T = args.K, args.T
-    K_total, k_offset = K * world, K * rank
-    eng = RolloutEngine(K, T, 0.006, 100.0, 0.98, np.eye(2) * 20.0, [0.5, 0.5, 5.0, 5.0],
-                        [5.0, 5.0, 50.0, 50.0], 0.0, ArmParams(), K_total=K_total, k_offset=k_offset,
-                        device=local_rank, lanes_per_sample=args.lps)
+    T = args.T
     path = np.load(os.path.join(ROOT, "tests", "golden", "paths.npz"))["xydq_circle"][:, :4]
     window = path[0:30]
-    x0 = X0_RUNPY.copy()
-    u = np.array([[10.0, -2.0]] * T)
+    if c5:
+        from mppi_robotarm_amd.chain import CHAIN7_SIGMA, CHAIN7_X0, ChainEngine, ChainParams, gravity_torque
+        from mppi_robotarm_amd.distributed import shard_geometry
+        K_total = args.K                                   # strong scaling: config 5 fixes K
+        K, k_offset = shard_geometry(K_total, world, rank)
+        eng = ChainEngine(K, T, 0.006, 100.0, 0.98, CHAIN7_SIGMA, [0.5, 0.5, 5.0, 5.0], [5.0, 5.0, 50.0, 50.0],
+                          0.0, ChainParams(), K_total=K_total, k_offset=k_offset, device=local_rank)
+        x0 = CHAIN7_X0.copy()
+        u = np.tile(gravity_torque(x0[:7]), (T, 1))
+    else:
+        K = args.K
+        K_total, k_offset = K * world, K * rank
+        eng = RolloutEngine(K, T, 0.006, 100.0, 0.98, np.eye(2) * 20.0, [0.5, 0.5, 5.0, 5.0],
+                            [5.0, 5.0, 50.0, 50.0], 0.0, ArmParams(), K_total=K_total, k_offset=k_offset,
+                            device=local_rank, lanes_per_sample=args.lps)
+        x0 = X0_RUNPY.copy()
+        u = np.array([[10.0, -2.0]] * T)
     eng.set_step_inputs(x0, window, u)
     noise = [eng.philox_noise(1234, i) for i in range(args.nbuf)]
     partial = eng.new_partial()
@@ -191,18 +243,19 @@ def main():
     if rank == 0:
         ms_per_step = elapsed * 1e3 / args.steps
         value = K_total * T * args.steps / elapsed
-        alg_bytes = BYTES_PER_STATE_STEP * K * T
+        alg_bytes = (C5_BYTES_PER_STATE_STEP if c5 else BYTES_PER_STATE_STEP) * K * T
         achieved = alg_bytes / (kern_ms * 1e-3) / 1e9
         traffic = None
         if os.path.exists(args.traffic_json):
             try:
                 tj = json.load(open(args.traffic_json))
-                if tj.get("K") == K and tj.get("T") == T:
+                if tj.get("K") == K and tj.get("T") == T and tj.get("workload", "c3") == args.workload:
                     traffic = tj.get("hbm_bytes_per_launch")
             except Exception:
                 traffic = None
         out = {
-            "metric": "MPPI rollouts/sec (K×T state-steps/s) + control-step latency, K=65536 T=64",
+            "metric": ("MPPI rollouts/sec (K×T state-steps/s), 7-DoF chain K=131072 T=128 (BASELINE config 5)" if c5
+                       else "MPPI rollouts/sec (K×T state-steps/s) + control-step latency, K=65536 T=64"),
             "value": value,
             "unit": "state-steps/s",
             "n_gpus": world,
@@ -213,13 +266,17 @@ def main():
             "control_step_latency_ms": ms_per_step,
             "kernel_ms": kern_ms,
             "higher_is_better": True,
-            "scaling": "weak",
+            "scaling": "strong" if c5 else "weak",
             "vs_baseline": None,
             "dtype": "f32",
             "data": "synthetic",
-            "config": {"workload": f"2-DoF arm MPPI step, K={K_total} (K/GPU={K}) T={T}, run.py constants, "
-                                   f"xydq_circle.txt window, Philox N(0,20I) noise x{args.nbuf} buffers",
-                       "K_total": K_total, "K_per_gpu": K, "T": T, "lanes_per_sample": eng.lanes_per_sample,
+            "config": {"workload": (f"7-DoF chain MPPI step (build-defined model, armature + damping), K={K_total} "
+                                    f"(K/GPU={K}) T={T}, run.py constants, config-5 start pose, xydq_circle.txt "
+                                    f"window, Philox N(0,Sigma7) noise x{args.nbuf} buffers" if c5 else
+                                    f"2-DoF arm MPPI step, K={K_total} (K/GPU={K}) T={T}, run.py constants, "
+                                    f"xydq_circle.txt window, Philox N(0,20I) noise x{args.nbuf} buffers"),
+                       "K_total": K_total, "K_per_gpu": K, "T": T,
+                       "lanes_per_sample": 1 if c5 else eng.lanes_per_sample,
                        "parallelism": f"samples sharded x{world}, RCCL all_gather of partials" if world > 1
                        else "single device, fused update" + (f", HIP graph of {chunk} steps" if use_graph
                                                                else ", back-to-back launches")},
@@ -227,7 +284,8 @@ def main():
                          "frac": achieved / HBM_PEAK_GBS, "traffic": traffic},
         }
         if world == 1 and args.cpu_seconds > 0:
-            out["cpu_baseline"] = cpu_baseline(args, window, x0, u)
+            out["cpu_baseline"] = (cpu_baseline_c5(args, window, x0, u, K, T) if c5
+                                   else cpu_baseline(args, window, x0, u))
         print(json.dumps(out))
     if world > 1:
         dist.destroy_process_group()

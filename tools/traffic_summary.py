@@ -1,6 +1,6 @@
 """Summarise one tools/profile_round.sh run into the committed profile files.
 
-    python tools/traffic_summary.py gpurun_out/prof_TAG profiles/TAG [K T]
+    python tools/traffic_summary.py gpurun_out/prof_TAG profiles/TAG [K T [c3|c5]]
 
 Reads the kernel-trace stats and the PMC passes (each counter in its own
 rocprofv3 run, as the MI355X guide prescribes), applies the measured gfx950
@@ -37,6 +37,9 @@ def main():
     src, dst = sys.argv[1], sys.argv[2]
     K = int(sys.argv[3]) if len(sys.argv) > 3 else 65536
     T = int(sys.argv[4]) if len(sys.argv) > 4 else 64
+    workload = sys.argv[5] if len(sys.argv) > 5 else "c3"
+    bps = 28 if workload == "c5" else 8     # algorithmic noise bytes per state-step
+    kpat = "chain_rollout_kernel" if workload == "c5" else "rollout_kernel"
     os.makedirs(dst, exist_ok=True)
     shutil.copy(os.path.join(src, "stats", "run_kernel_stats.csv"), os.path.join(dst, "kernel_stats.csv"))
     for p in ("fetch", "write", "cfetch", "cwrite", "sq", "grbm"):
@@ -46,12 +49,12 @@ def main():
     avg_ns = None
     with open(os.path.join(src, "stats", "run_kernel_stats.csv")) as f:
         for row in csv.DictReader(f):
-            if "rollout_kernel" in row["Name"]:
+            if kpat in row["Name"] and (workload == "c5" or "chain" not in row["Name"]):
                 avg_ns = float(row["AverageNs"])
-                m = re.search(r"rollout_kernel<[^>]*>", row["Name"])
+                m = re.search(kpat + r"<[^>]*>", row["Name"])
                 kname = m.group(0) if m else row["Name"][:60]
-    fetch = np.median(counters(os.path.join(src, "fetch", "p_counter_collection.csv"), "rollout")["FETCH_SIZE"])
-    write = np.median(counters(os.path.join(src, "write", "p_counter_collection.csv"), "rollout")["WRITE_SIZE"])
+    fetch = np.median(counters(os.path.join(src, "fetch", "p_counter_collection.csv"), kpat)["FETCH_SIZE"])
+    write = np.median(counters(os.path.join(src, "write", "p_counter_collection.csv"), kpat)["WRITE_SIZE"])
     cf = counters(os.path.join(src, "cfetch", "p_counter_collection.csv"), "calib")["FETCH_SIZE"]
     cw = counters(os.path.join(src, "cwrite", "p_counter_collection.csv"), "calib")["WRITE_SIZE"]
     known_read, known_write = 33554432, 262144     # tools/calib_fetch.hip
@@ -59,9 +62,9 @@ def main():
     w_ratio = np.median(cw) * 1024 / known_write
     read_b = fetch * 1024 / f_ratio
     write_b = write * 1024 / w_ratio
-    alg = 8 * K * T
+    alg = bps * K * T
     out = {
-        "K": K, "T": T, "kernel": kname + " (fused update)",
+        "workload": workload, "K": K, "T": T, "kernel": kname + " (fused update)",
         "hbm_bytes_per_launch": int(round(read_b + write_b)),
         "read_bytes_per_launch": int(round(read_b)),
         "write_bytes_per_launch": int(round(write_b)),
@@ -75,14 +78,15 @@ def main():
         "rocprof_avg_kernel_ns": avg_ns,
         "source": f"rocprofv3 --pmc FETCH_SIZE / --pmc WRITE_SIZE (separate passes), bench.py; {os.path.basename(dst)}",
     }
-    json.dump(out, open(os.path.join(os.path.dirname(dst.rstrip('/')), "traffic.json"), "w"), indent=1)
+    name = "traffic_c5.json" if workload == "c5" else "traffic.json"
+    json.dump(out, open(os.path.join(os.path.dirname(dst.rstrip('/')), name), "w"), indent=1)
     sqf = os.path.join(src, "sq", "p_counter_collection.csv")
     if os.path.exists(sqf):
-        sq = {k: float(np.median(v)) for k, v in counters(sqf, "rollout").items()}
+        sq = {k: float(np.median(v)) for k, v in counters(sqf, kpat).items()}
         gr = {}
         grf = os.path.join(src, "grbm", "p_counter_collection.csv")
         if os.path.exists(grf):
-            gr = {k: float(np.median(v)) for k, v in counters(grf, "rollout").items()}
+            gr = {k: float(np.median(v)) for k, v in counters(grf, kpat).items()}
         summ = {"SQ": sq, "GRBM": gr}
         if "SQ_WAVE_CYCLES" in sq:
             summ["wait_any_frac"] = sq.get("SQ_WAIT_ANY", 0) / sq["SQ_WAVE_CYCLES"]
