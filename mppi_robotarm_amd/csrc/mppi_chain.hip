@@ -68,6 +68,39 @@ struct ChainConst {
 
 using CScratch = MergeScratch<kCMaxVals>;
 
+// The per-step dynamics / cost constants, packed (floats): mu_ab for a < b in
+// row order, then D'_aa, the armature off-diagonal, damping, g nu, fk, stage and
+// terminal weights, dt.  The rollout kernel reads them from a device copy through
+// the constant address space every step (scalar loads, re-issued after each
+// step's scheduling boundary) instead of holding ~64 uniform values in SGPRs
+// across the loop — held, they spill and come back as v_readlane, ~28 per step.
+constexpr int kTri = kCMax * (kCMax - 1) / 2;
+enum : int { kOffDd = kTri, kOffOffj = kOffDd + kCMax, kOffDamp = kOffOffj + kCMax, kOffGnu = kOffDamp + kCMax,
+             kOffFk = kOffGnu + kCMax, kOffSw = kOffFk + kCMax, kOffTw = kOffSw + 4, kOffDt = kOffTw + 4,
+             kDynFloats = kOffDt + 4 };
+__host__ __device__ constexpr int tri_index(int a, int b) { return a * kCMax - a * (a + 1) / 2 + (b - a - 1); }
+
+struct DynMem {   // rollout kernel: constant-address-space reads
+    cfloat* p;
+    __device__ float mu(int a, int b) const { return p[tri_index(a, b)]; }
+    __device__ float Dd(int a) const { return p[kOffDd + a]; }
+    __device__ float offj(int a) const { return p[kOffOffj + a]; }
+    __device__ float damp(int a) const { return p[kOffDamp + a]; }
+    __device__ float gnu(int a) const { return p[kOffGnu + a]; }
+    __device__ float fk(int a) const { return p[kOffFk + a]; }
+    __device__ float dt() const { return p[kOffDt]; }
+};
+struct DynArg {   // other kernels: the kernel-argument copy
+    const ChainConst& k;
+    __device__ float mu(int a, int b) const { return k.mu[a][b]; }
+    __device__ float Dd(int a) const { return k.Dd[a]; }
+    __device__ float offj(int a) const { return k.offj[a]; }
+    __device__ float damp(int a) const { return k.damp[a]; }
+    __device__ float gnu(int a) const { return k.gnu[a]; }
+    __device__ float fk(int a) const { return k.fk[a]; }
+    __device__ float dt() const { return k.dt; }
+};
+
 // Chain state of one sample: joint angles / rates and the cached sin / cos of
 // the absolute angles theta_a = q_1 + ... + q_a.
 template <int N>
@@ -89,7 +122,8 @@ struct ChainState {
     //   diagonal, -J_{a+1} at (a, a+1): the joint armature in absolute angles),
     //   bias_a = sum_b mu_ab sin(th_a - th_b) thdot_b^2,  g_a = g nu_a cos th_a,
     //   q_ddot_a = theta_ddot_a - theta_ddot_{a-1};  dq += q_ddot dt;  q += dq dt.
-    __device__ __forceinline__ void step(const float (&v)[N], const ChainConst& k) {
+    template <class KC>
+    __device__ __forceinline__ void step(const float (&v)[N], const KC& k) {
         float w[N];
         {
             float acc = 0.f;
@@ -102,11 +136,11 @@ struct ChainState {
         float L[N][N];   // lower triangle: D', then its Cholesky factor in place
         float r[N], ve[N];
 #pragma unroll
-        for (int a = 0; a < N; ++a) ve[a] = fmaf(-k.damp[a], dq[a], v[a]);   // joint torque - damping
+        for (int a = 0; a < N; ++a) ve[a] = fmaf(-k.damp(a), dq[a], v[a]);   // joint torque - damping
 #pragma unroll
         for (int a = 0; a < N; ++a) {
-            L[a][a] = k.Dd[a];
-            r[a] = (a + 1 < N ? ve[a] - ve[a + 1] : ve[a]) - k.gnu[a] * c[a];
+            L[a][a] = k.Dd(a);
+            r[a] = (a + 1 < N ? ve[a] - ve[a + 1] : ve[a]) - k.gnu(a) * c[a];
         }
 #pragma unroll
         for (int a = 0; a < N; ++a) {
@@ -114,8 +148,8 @@ struct ChainState {
             for (int b = a + 1; b < N; ++b) {
                 const float cab = fmaf(c[a], c[b], s[a] * s[b]);   // cos(th_a - th_b)
                 const float sab = fmaf(s[a], c[b], -c[a] * s[b]);  // sin(th_a - th_b)
-                const float m = k.mu[a][b];
-                L[b][a] = b == a + 1 ? fmaf(m, cab, -k.offj[a]) : m * cab;
+                const float m = k.mu(a, b);
+                L[b][a] = b == a + 1 ? fmaf(m, cab, -k.offj(a)) : m * cab;
                 const float ms = m * sab;
                 r[a] = fmaf(-ms, w[b], r[a]);   // - mu_ab sin(th_a - th_b) thdot_b^2
                 r[b] = fmaf(ms, w[a], r[b]);    // - mu_ba sin(th_b - th_a) thdot_a^2
@@ -153,19 +187,20 @@ struct ChainState {
         float prev = 0.f;
 #pragma unroll
         for (int a = 0; a < N; ++a) {
-            dq[a] = fmaf(r[a] - prev, k.dt, dq[a]);
+            dq[a] = fmaf(r[a] - prev, k.dt(), dq[a]);
             prev = r[a];
-            q[a] = fmaf(dq[a], k.dt, q[a]);
+            q[a] = fmaf(dq[a], k.dt(), q[a]);
         }
         angles();
     }
 
-    __device__ __forceinline__ void effector(const ChainConst& k, float* px, float* py) const {
+    template <class KC>
+    __device__ __forceinline__ void effector(const KC& k, float* px, float* py) const {
         float x = 0.f, y = 0.f;
 #pragma unroll
         for (int a = 0; a < N; ++a) {
-            x = fmaf(k.fk[a], c[a], x);
-            y = fmaf(k.fk[a], s[a], y);
+            x = fmaf(k.fk(a), c[a], x);
+            y = fmaf(k.fk(a), s[a], y);
         }
         *px = x;
         *py = y;
@@ -207,13 +242,14 @@ __device__ void chain_update_block(ChainStep* nxt, const ChainConst& c, CScratch
 // POLL / counter hand-off and the merges as in rollout_kernel (mppi_rocm.hip).
 template <int N, bool POLL>
 __global__ __launch_bounds__(kCT) void chain_rollout_kernel(
-    const ChainConst c, const ChainStep* __restrict__ st, const float* __restrict__ noise,
-    double* __restrict__ S_out, double* __restrict__ slab, double* __restrict__ gslab,
+    const ChainConst c, const ChainStep* __restrict__ st, const float* __restrict__ dyn,
+    const float* __restrict__ noise, double* __restrict__ S_out, double* __restrict__ slab, double* __restrict__ gslab,
     unsigned* __restrict__ counters, double* __restrict__ partial_out, double* __restrict__ w_eps_out,
     ChainStep* __restrict__ nxt, unsigned flags, unsigned* __restrict__ epoch, unsigned* __restrict__ tmo,
     unsigned long long* __restrict__ dbg) {
     static_assert(N <= kCMax && N >= 2, "links");
     __shared__ float4 s_win[kSlots];
+    __shared__ KeyPair s_keys[kKeyPairs];
     __shared__ float s_redf[kCT / 64];
     __shared__ int s_cnt[kCT / 64];
     __shared__ int s_k[kCT];
@@ -237,8 +273,11 @@ __global__ __launch_bounds__(kCT) void chain_rollout_kernel(
         u_cur[ch] = ((flags & MPPI_FLAG_FUSED_UPDATE) && idx < T * N) ? st->u[idx / N][idx % N] : 0.0;
     }
     if (tid < kSlots) s_win[tid] = st->win[tid];
-    Search<1, true> sr;   // precise keys: the config-5 start pose sits on a waypoint
-    sr.load(st->key, st->ctr, 0);
+    // window keys in LDS (broadcast reads): the 90 key registers would cost the
+    // chain kernel its second wave per SIMD; precise keys: the config-5 start
+    // pose sits on a waypoint
+    SearchLDS<true>::fill(s_keys, st->key, tid);
+    SearchLDS<true> sr{s_keys, st->ctr.x, st->ctr.y};
     ChainState<N> x;
 #pragma unroll
     for (int a = 0; a < N; ++a) {
@@ -263,6 +302,7 @@ __global__ __launch_bounds__(kCT) void chain_rollout_kernel(
         for (int d = 0; d < 2 * N; ++d) uring[j][d] = cua[j * 2 * kCMax + (d < N ? d : kCMax + d - N)];
     __syncthreads();
 
+    const DynMem kd{(cfloat*)dyn};
     // Horizon loop (control.py:95-109 with the chain model), S in fp64.
     double S = 0.0;
     float S4 = 0.f;
@@ -282,15 +322,16 @@ __global__ __launch_bounds__(kCT) void chain_rollout_kernel(
         for (int d = 0; d < 2 * N; ++d)
             uring[i % kCPU][d] = cua[(t + kCPU) * 2 * kCMax + (d < N ? d : kCMax + d - N)];
         PIN_LOADS();
-        x.step(v, c);
+        x.step(v, kd);
         float px, py;
-        x.effector(c, &px, &py);
+        x.effector(kd, &px, &py);
         const float4 r = s_win[sr.nearest(px, py)];
         ex = px - r.x;
         ey = py - r.y;
         e1 = x.dq[0] - r.z;
         e2 = x.dq[1] - r.w;
-        S4 += weighted_sq(ex, ey, e1, e2, c.sw) + g;
+        const float sw[4] = {kd.p[kOffSw], kd.p[kOffSw + 1], kd.p[kOffSw + 2], kd.p[kOffSw + 3]};
+        S4 += weighted_sq(ex, ey, e1, e2, sw) + g;
         if constexpr ((i & 3) == 3) {
             S += (double)S4;
             S4 = 0.f;
@@ -481,7 +522,7 @@ __global__ __launch_bounds__(kCT) void chain_traj_kernel(const ChainConst c, con
             v[d] = base[ti * N + d];
             if (noise) v[d] = fmaf(exf, v[d], noise[((size_t)ti * N + d) * c.K_local + k]);
         }
-        x.step(v, c);
+        x.step(v, DynArg{c});
         float* o = out + ((size_t)k * T + t) * 2 * N;
 #pragma unroll
         for (int a = 0; a < N; ++a) {
@@ -544,6 +585,7 @@ struct mppi_chain_ctx {
     float* d_base = nullptr;
     float* h_base = nullptr;
     float* d_chol = nullptr;       // Cholesky factor of Sigma (kCMax x kCMax, fp32) for the Philox noise
+    float* d_dyn = nullptr;        // packed per-step constants (DynMem)
     unsigned* h_tmo = nullptr;
     unsigned* d_tmo = nullptr;
     unsigned long long* d_dbg = nullptr;
@@ -556,7 +598,7 @@ using mppi_host::fail;
 template <int N, bool P>
 void launch_rollout(mppi_chain_ctx* c, const ChainStep* cur, const float* noise, double* S, double* part, ChainStep* nxt,
                     unsigned flags) {
-    hipLaunchKernelGGL((chain_rollout_kernel<N, P>), dim3(c->nblocks), dim3(kCT), 0, c->stream, c->kc, cur, noise, S,
+    hipLaunchKernelGGL((chain_rollout_kernel<N, P>), dim3(c->nblocks), dim3(kCT), 0, c->stream, c->kc, cur, c->d_dyn, noise, S,
                        c->d_slab, c->d_gslab, c->d_counter, part, c->d_weps, nxt, flags, c->d_epoch, c->d_tmo,
                        c->d_dbg);
 }
@@ -696,6 +738,21 @@ int mppi_chain_ctx_create(const mppi_chain_config* cfg, int device, void* stream
     const int ngroups = (c->nblocks + kGroup - 1) / kGroup;
     const size_t gslab = (size_t)ngroups * stride * val;
     const size_t ctr_bytes = ((size_t)(ngroups + 2) * sizeof(unsigned) + 255) & ~(size_t)255;
+    float dyn[kDynFloats] = {};
+    for (int a = 0; a < kCMax; ++a)
+        for (int b = a + 1; b < kCMax; ++b) dyn[tri_index(a, b)] = k.mu[a][b];
+    for (int a = 0; a < kCMax; ++a) {
+        dyn[kOffDd + a] = k.Dd[a];
+        dyn[kOffOffj + a] = k.offj[a];
+        dyn[kOffDamp + a] = k.damp[a];
+        dyn[kOffGnu + a] = k.gnu[a];
+        dyn[kOffFk + a] = k.fk[a];
+    }
+    for (int i = 0; i < 4; ++i) {
+        dyn[kOffSw + i] = k.sw[i];
+        dyn[kOffTw + i] = k.tw[i];
+    }
+    dyn[kOffDt] = k.dt;
     float chol[kCMax * kCMax] = {};
     for (int i = 0; i < n; ++i)
         for (int j = 0; j <= i; ++j) chol[i * kCMax + j] = (float)Lc[i][j];
@@ -705,6 +762,7 @@ int mppi_chain_ctx_create(const mppi_chain_config* cfg, int device, void* stream
         (e = hipMalloc(&c->d_weps, kCMaxVals * sizeof(double))) != hipSuccess ||
         (e = hipMalloc(&c->d_base, kCMaxVals * sizeof(float))) != hipSuccess ||
         (e = hipMalloc(&c->d_chol, sizeof(chol))) != hipSuccess ||
+        (e = hipMalloc(&c->d_dyn, sizeof(dyn))) != hipSuccess ||
         (e = hipHostMalloc(&c->h_step, sizeof(ChainStep), hipHostMallocDefault)) != hipSuccess ||
         (e = hipHostMalloc(&c->h_buf, kCMaxVals * sizeof(double), hipHostMallocDefault)) != hipSuccess ||
         (e = hipHostMalloc(&c->h_base, kCMaxVals * sizeof(float), hipHostMallocDefault)) != hipSuccess ||
@@ -716,6 +774,7 @@ int mppi_chain_ctx_create(const mppi_chain_config* cfg, int device, void* stream
         (e = hipMemset(c->d_step, 0, 2 * sizeof(ChainStep))) != hipSuccess ||
         (e = hipMemset(c->d_weps, 0, kCMaxVals * sizeof(double))) != hipSuccess ||
         (e = hipMemcpy(c->d_chol, chol, sizeof(chol), hipMemcpyHostToDevice)) != hipSuccess ||
+        (e = hipMemcpy(c->d_dyn, dyn, sizeof(dyn), hipMemcpyHostToDevice)) != hipSuccess ||
         (e = hipDeviceSynchronize()) != hipSuccess)
         return cleanup_fail(fail(MPPI_E_HIP, std::string("allocation: ") + hipGetErrorString(e)));
     memset(c->h_step, 0, sizeof(ChainStep));
@@ -736,6 +795,7 @@ void mppi_chain_ctx_destroy(mppi_chain_ctx* c) {
     (void)hipFree(c->d_weps);
     (void)hipFree(c->d_base);
     (void)hipFree(c->d_chol);
+    (void)hipFree(c->d_dyn);
     if (c->h_step) (void)hipHostFree(c->h_step);
     if (c->h_buf) (void)hipHostFree(c->h_buf);
     if (c->h_base) (void)hipHostFree(c->h_base);

@@ -230,6 +230,54 @@ struct Search {
     }
 };
 
+// The same search with the window keys in LDS instead of registers: the keys
+// are uniform across the workgroup, so every read is a broadcast ds_read_b128
+// (two per two slots: {rx'0, rx'1, ry'0, ry'1}, {c'0, c'1, -, -}).  Costs one
+// LDS read per slot and per step, frees the 3 x 30 key registers — for kernels
+// whose per-lane state is large (the n-link chain) that buys occupancy.
+struct alignas(16) KeyPair {
+    float4 xy;   // rx'(2i), rx'(2i+1), ry'(2i), ry'(2i+1)
+    float4 c;    // c'(2i), c'(2i+1), 0, 0
+};
+constexpr int kKeyPairs = kSlots / 2;
+
+template <bool PRECISE = false>
+struct SearchLDS {
+    const KeyPair* kp;   // LDS, kKeyPairs entries
+    float cx, cy;
+
+    // cooperative fill by the first kKeyPairs threads; a barrier must follow
+    __device__ __forceinline__ static void fill(KeyPair* dst, const float4* key, int tid) {
+        if (tid < kKeyPairs) {
+            const float4 k0 = key[2 * tid], k1 = key[2 * tid + 1];
+            dst[tid].xy = make_float4(k0.x, k1.x, k0.y, k1.y);
+            dst[tid].c = make_float4(k0.z, k1.z, 0.f, 0.f);
+        }
+    }
+
+    __device__ __forceinline__ unsigned nearest(float px, float py) const {
+        const float dx = px - cx, dy = py - cy;
+        const float ax = -2.f * dx, ay = -2.f * dy;
+        const f32x2 ax2 = {ax, ax}, ay2 = {ay, ay};
+        const float pp = fmaf(dx, dx, dy * dy);
+        const f32x2 pp2 = {pp, pp};
+        float best = 3.0e38f;
+        constexpr int SP = (MPPI_SEARCH_LEN + 1) / 2;
+#pragma unroll
+        for (int i = 0; i < SP; ++i) {
+            const float4 xy = kp[i].xy, cc = kp[i].c;
+            f32x2 key = __builtin_elementwise_fma(ax2, f32x2{xy.x, xy.y},
+                                                  __builtin_elementwise_fma(ay2, f32x2{xy.z, xy.w}, f32x2{cc.x, cc.y}));
+            if constexpr (PRECISE) key = key + pp2;   // |p - r_j|^2
+            const unsigned j = (unsigned)(2 * i);
+            const float k0 = __uint_as_float((__float_as_uint(key.x) & ~31u) | j);
+            const float k1 = __uint_as_float((__float_as_uint(key.y) & ~31u) | (j + 1));
+            best = min3_raw(best, k0, k1);
+        }
+        return __float_as_uint(best) & 31u;
+    }
+};
+
 // stage / terminal cost terms (control.py:185-198, weights x 10000 folded in)
 __device__ __forceinline__ float weighted_sq(float ex, float ey, float e1, float e2, const float* w) {
     return fmaf(w[0], ex * ex, fmaf(w[1], ey * ey, fmaf(w[2], e1 * e1, w[3] * e2 * e2)));
