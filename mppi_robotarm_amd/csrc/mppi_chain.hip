@@ -52,161 +52,252 @@ struct alignas(16) ChainStep {
 };
 
 // Launch constants (kernel argument, by value).
+constexpr int kCDyn = 72;
 struct ChainConst {
     int K_local, T, k_offset, k_exploit, nblocks, acquire, n, pad0;
-    float dt;
-    float mu[kCMax][kCMax];   // mu_ab (a != b), the constant part of D
-    float Dd[kCMax];          // D'_aa = mu_aa + I_a + J_a + J_{a+1} (constant; J: joint armature)
-    float offj[kCMax];        // D'_{a,a+1} -= J_{a+1}
-    float damp[kCMax];        // joint viscous damping b_a
-    float gnu[kCMax];         // g nu_a
-    float fk[kCMax];          // cost kinematics lengths
-    float sw[4], tw[4];       // stage / terminal weights x 10000
+    alignas(8) float dyn[kCDyn];   // packed dynamics / cost constants (layout: kOff* below)
     double lambda, inv_lambda, gamma;
     double sig_inv[kCMax * kCMax];
 };
 
 using CScratch = MergeScratch<kCMaxVals>;
 
-// The per-step dynamics / cost constants, packed (floats): mu_ab for a < b in
-// row order, then D'_aa, the armature off-diagonal, damping, g nu, fk, stage and
-// terminal weights, dt.  The rollout kernel reads them from a device copy through
-// the constant address space every step (scalar loads, re-issued after each
-// step's scheduling boundary) instead of holding ~64 uniform values in SGPRs
-// across the loop — held, they spill and come back as v_readlane, ~28 per step.
-constexpr int kTri = kCMax * (kCMax - 1) / 2;
-enum : int { kOffDd = kTri, kOffOffj = kOffDd + kCMax, kOffDamp = kOffOffj + kCMax, kOffGnu = kOffDamp + kCMax,
-             kOffFk = kOffGnu + kCMax, kOffSw = kOffFk + kCMax, kOffTw = kOffSw + 4, kOffDt = kOffTw + 4,
-             kDynFloats = kOffDt + 4 };
-__host__ __device__ constexpr int tri_index(int a, int b) { return a * kCMax - a * (a + 1) / 2 + (b - a - 1); }
-
-struct DynMem {   // rollout kernel: constant-address-space reads
-    cfloat* p;
-    __device__ float mu(int a, int b) const { return p[tri_index(a, b)]; }
-    __device__ float Dd(int a) const { return p[kOffDd + a]; }
-    __device__ float offj(int a) const { return p[kOffOffj + a]; }
-    __device__ float damp(int a) const { return p[kOffDamp + a]; }
-    __device__ float gnu(int a) const { return p[kOffGnu + a]; }
-    __device__ float fk(int a) const { return p[kOffFk + a]; }
-    __device__ float dt() const { return p[kOffDt]; }
+// The dynamics / cost constants, packed (floats, pairs 8-byte aligned).  The
+// chain's coupling is separable: mu_ab = l_a nu_b for a < b (chain_oracle.py
+// coefficients), so D' and the bias need only the per-link l and nu.  Pairs
+// hold links / rows (2p, 2p+1); the pad link of an odd chain has l = nu = fk =
+// damping = 0 and D'_aa = 1.  The rollout kernel reads them from a device copy
+// through the constant address space every step (scalar loads re-issued after
+// each step's scheduling boundary) rather than holding them in SGPRs across the
+// loop, where they spill and return as v_readlane (~28 per step at n = 7).
+enum : int {
+    kOffL = 0,                    // l_a (dynamics link lengths)
+    kOffNu = kOffL + kCMax,       // nu_a = m_a lc_a + l_a sum_{b>a} m_b
+    kOffDd = kOffNu + kCMax,      // D'_aa = mu_aa + I_a + J_a + J_{a+1}
+    kOffJ = kOffDd + kCMax,       // [a]: the pair holding row a+1 of column a: -J_{a+1} at row a+1, 0 beside it
+    kOffDamp = kOffJ + 2 * kCMax, // joint viscous damping b_a
+    kOffFk = kOffDamp + kCMax,    // cost kinematics lengths
+    kOffSw = kOffFk + kCMax,      // stage weights x 10000
+    kOffTw = kOffSw + 4,          // terminal weights x 10000
+    kOffDt = kOffTw + 4,
+    kOffG = kOffDt + 1,
+    kDynFloats = kOffG + 7,
 };
-struct DynArg {   // other kernels: the kernel-argument copy
-    const ChainConst& k;
-    __device__ float mu(int a, int b) const { return k.mu[a][b]; }
-    __device__ float Dd(int a) const { return k.Dd[a]; }
-    __device__ float offj(int a) const { return k.offj[a]; }
-    __device__ float damp(int a) const { return k.damp[a]; }
-    __device__ float gnu(int a) const { return k.gnu[a]; }
-    __device__ float fk(int a) const { return k.fk[a]; }
-    __device__ float dt() const { return k.dt; }
-};
+static_assert(kDynFloats == kCDyn, "dyn layout");
 
-// Chain state of one sample: joint angles / rates and the cached sin / cos of
-// the absolute angles theta_a = q_1 + ... + q_a.
+template <class F>   // F: const float (generic, kernel argument) or cfloat (constant address space)
+struct Dyn {
+    F* p;
+    __device__ __forceinline__ f32x2 pair(int off, int i) const { return f32x2{p[off + 2 * i], p[off + 2 * i + 1]}; }
+    __device__ __forceinline__ f32x2 l2(int i) const { return pair(kOffL, i); }
+    __device__ __forceinline__ f32x2 nu2(int i) const { return pair(kOffNu, i); }
+    __device__ __forceinline__ f32x2 damp2(int i) const { return pair(kOffDamp, i); }
+    __device__ __forceinline__ f32x2 fk2(int i) const { return pair(kOffFk, i); }
+    __device__ __forceinline__ f32x2 joff2(int a) const { return pair(kOffJ, a); }
+    __device__ __forceinline__ float Dd(int a) const { return p[kOffDd + a]; }
+    __device__ __forceinline__ float dt() const { return p[kOffDt]; }
+    __device__ __forceinline__ float g() const { return p[kOffG]; }
+};
+using DynMem = Dyn<cfloat>;
+using DynArg = Dyn<const float>;
+
+__device__ __forceinline__ f32x2 splat(float x) { return f32x2{x, x}; }
+__device__ __forceinline__ f32x2 pfma(f32x2 a, f32x2 b, f32x2 c) { return __builtin_elementwise_fma(a, b, c); }
+template <int P> __device__ __forceinline__ float get(const f32x2 (&v)[P], int i) { return v[i >> 1][i & 1]; }
+template <int P> __device__ __forceinline__ void put(f32x2 (&v)[P], int i, float x) { v[i >> 1][i & 1] = x; }
+
+// Chain state of one sample in row pairs: joint angles / rates and the cached
+// cos / sin of the absolute angles theta_a = q_1 + ... + q_a.  Pad entries of an
+// odd chain stay 0.
 template <int N>
 struct ChainState {
-    float q[N], dq[N], s[N], c[N];
+    static constexpr int P = (N + 1) / 2;
+    f32x2 q[P], dq[P], c[P], s[P];
+
+    __device__ __forceinline__ void load(const float* x0) {
+#pragma unroll
+        for (int p = 0; p < P; ++p) q[p] = dq[p] = c[p] = s[p] = f32x2{0.f, 0.f};
+#pragma unroll
+        for (int a = 0; a < N; ++a) {
+            put(q, a, x0[a]);
+            put(dq, a, x0[N + a]);
+        }
+        angles();
+    }
+    __device__ __forceinline__ float qa(int a) const { return get(q, a); }
+    __device__ __forceinline__ float dqa(int a) const { return get(dq, a); }
 
     __device__ __forceinline__ void angles() {
         float th = 0.f;
 #pragma unroll
         for (int a = 0; a < N; ++a) {
-            th += q[a];
-            sincos_f32(th, &s[a], &c[a]);
+            th += get(q, a);
+            float sa, ca;
+            sincos_f32(th, &sa, &ca);
+            put(s, a, sa);
+            put(c, a, ca);
         }
     }
 
     // One semi-implicit Euler step (oracle/chain_oracle.py chain_forward_dynamics):
     //   D' theta_ddot = tau - bias - g,  tau_a = v'_a - v'_{a+1},  v' = v - b dq,
-    //   D'_ab = mu_ab cos(th_a - th_b) (+ constants: I_a + J_a + J_{a+1} on the
-    //   diagonal, -J_{a+1} at (a, a+1): the joint armature in absolute angles),
-    //   bias_a = sum_b mu_ab sin(th_a - th_b) thdot_b^2,  g_a = g nu_a cos th_a,
-    //   q_ddot_a = theta_ddot_a - theta_ddot_{a-1};  dq += q_ddot dt;  q += dq dt.
+    //   D'_ab = l_a nu_b cos(th_a - th_b) (a < b; constants I_a + J_a + J_{a+1} on
+    //   the diagonal and -J_{a+1} at (a+1, a): the joint armature in absolute
+    //   angles), bias_a = sum_b mu_ab sin(th_a - th_b) thdot_b^2,
+    //   g_a = g nu_a cos th_a, q_ddot_a = theta_ddot_a - theta_ddot_{a-1},
+    //   dq += q_ddot dt, q += dq dt.
+    // Packed (v_pk_*) over row pairs; D' is factored in place by a right-looking
+    // Cholesky on column-major row pairs; the bias is O(n) through the prefix /
+    // suffix sums the separable mu allows:
+    //   bias_a = s_a X_a - c_a Y_a,  X_a = l_a C+_a + nu_a C-_a,  Y_a = l_a S+_a + nu_a S-_a,
+    //   C+_a = sum_{b>a} nu_b w_b c_b,  C-_a = sum_{b<a} l_b w_b c_b  (S: s_b).
     template <class KC>
     __device__ __forceinline__ void step(const float (&v)[N], const KC& k) {
-        float w[N];
+        f32x2 lc[P], ls[P], vc[P], vs[P], w[P];
         {
             float acc = 0.f;
 #pragma unroll
             for (int a = 0; a < N; ++a) {
-                acc += dq[a];
-                w[a] = acc * acc;   // thdot_a^2
+                acc += get(dq, a);
+                put(w, a, acc);
             }
         }
-        float L[N][N];   // lower triangle: D', then its Cholesky factor in place
-        float r[N], ve[N];
 #pragma unroll
-        for (int a = 0; a < N; ++a) ve[a] = fmaf(-k.damp(a), dq[a], v[a]);   // joint torque - damping
-#pragma unroll
-        for (int a = 0; a < N; ++a) {
-            L[a][a] = k.Dd(a);
-            r[a] = (a + 1 < N ? ve[a] - ve[a + 1] : ve[a]) - k.gnu(a) * c[a];
+        for (int p = 0; p < P; ++p) {
+            const f32x2 l = k.l2(p), nu = k.nu2(p);
+            w[p] = w[p] * w[p];   // thdot^2
+            lc[p] = l * c[p];
+            ls[p] = l * s[p];
+            vc[p] = nu * c[p];
+            vs[p] = nu * s[p];
         }
+        // r = tau - g - bias
+        f32x2 r[P];
+        {
+            f32x2 ve[P], vv[P], Cs[P], Ss[P], Cp[P], Sp[P];
 #pragma unroll
-        for (int a = 0; a < N; ++a) {
+            for (int a = 0; a < N; ++a) put(vv, a, v[a]);
 #pragma unroll
-            for (int b = a + 1; b < N; ++b) {
-                const float cab = fmaf(c[a], c[b], s[a] * s[b]);   // cos(th_a - th_b)
-                const float sab = fmaf(s[a], c[b], -c[a] * s[b]);  // sin(th_a - th_b)
-                const float m = k.mu(a, b);
-                L[b][a] = b == a + 1 ? fmaf(m, cab, -k.offj(a)) : m * cab;
-                const float ms = m * sab;
-                r[a] = fmaf(-ms, w[b], r[a]);   // - mu_ab sin(th_a - th_b) thdot_b^2
-                r[b] = fmaf(ms, w[a], r[b]);    // - mu_ba sin(th_b - th_a) thdot_a^2
+            for (int p = 0; p < P; ++p) ve[p] = pfma(-k.damp2(p), dq[p], vv[p]);
+            f32x2 wvc[P], wvs[P], wlc[P], wls[P];
+#pragma unroll
+            for (int p = 0; p < P; ++p) {
+                wvc[p] = w[p] * vc[p];
+                wvs[p] = w[p] * vs[p];
+                wlc[p] = w[p] * lc[p];
+                wls[p] = w[p] * ls[p];
+            }
+            float cs = 0.f, ss = 0.f, cp = 0.f, sp = 0.f;
+#pragma unroll
+            for (int a = N - 1; a >= 0; --a) {
+                put(Cs, a, cs);
+                put(Ss, a, ss);
+                cs += get(wvc, a);
+                ss += get(wvs, a);
+            }
+#pragma unroll
+            for (int a = 0; a < N; ++a) {
+                put(Cp, a, cp);
+                put(Sp, a, sp);
+                cp += get(wlc, a);
+                sp += get(wls, a);
+                put(r, a, a + 1 < N ? get(ve, a) - get(ve, a + 1) : get(ve, a));   // tau
+            }
+            const f32x2 mg = splat(-k.g());
+#pragma unroll
+            for (int p = 0; p < P; ++p) {
+                const f32x2 l = k.l2(p), nu = k.nu2(p);
+                const f32x2 X = pfma(l, Cs[p], nu * Cp[p]);
+                const f32x2 Y = pfma(l, Ss[p], nu * Sp[p]);
+                r[p] = pfma(c[p], Y, pfma(-s[p], X, pfma(mg, vc[p], r[p])));
             }
         }
+        // D' lower triangle, column-major row pairs: col[a][p] = rows (2p, 2p+1) of
+        // column a; rows < a are don't-cares (kept finite).
+        f32x2 col[N][P];
+#pragma unroll
+        for (int a = 0; a < N; ++a) {
+            const f32x2 ca = splat(get(lc, a)), sa = splat(get(ls, a));
+#pragma unroll
+            for (int p = a / 2; p < P; ++p) {
+                if ((a & 1) && p == a / 2) {
+                    col[a][p] = splat(k.Dd(a));   // row a - 1: a don't-care
+                    continue;
+                }
+                const f32x2 t = p == (a + 1) / 2 && a + 1 < N ? pfma(sa, vs[p], k.joff2(a)) : sa * vs[p];
+                col[a][p] = pfma(ca, vc[p], t);
+            }
+            if (!(a & 1)) col[a][a / 2].x = k.Dd(a);
+        }
+        // Cholesky, right-looking: column j scaled by 1 / L_jj, then the trailing
+        // columns k > j updated on the rows >= k.
         float inv[N];
 #pragma unroll
         for (int j = 0; j < N; ++j) {
-            float d = L[j][j];
+            inv[j] = __builtin_amdgcn_rsqf(col[j][j / 2][j & 1]);
+            const f32x2 ij = splat(inv[j]);
 #pragma unroll
-            for (int q2 = 0; q2 < j; ++q2) d = fmaf(-L[j][q2], L[j][q2], d);
-            inv[j] = __builtin_amdgcn_rsqf(d);
+            for (int p = (j + 1) / 2; p < P; ++p) col[j][p] = col[j][p] * ij;
 #pragma unroll
-            for (int i = j + 1; i < N; ++i) {
-                float e = L[i][j];
+            for (int kk = j + 1; kk < N; ++kk) {
+                const f32x2 m = splat(-col[j][kk / 2][kk & 1]);
 #pragma unroll
-                for (int q2 = 0; q2 < j; ++q2) e = fmaf(-L[i][q2], L[j][q2], e);
-                L[i][j] = e * inv[j];
+                for (int p = kk / 2; p < P; ++p) col[kk][p] = pfma(m, col[j][p], col[kk][p]);
             }
         }
+        // L y = r, column-oriented (row j's own pair: only its partner row)
 #pragma unroll
-        for (int i = 0; i < N; ++i) {           // L y = r
-            float e = r[i];
+        for (int j = 0; j < N; ++j) {
+            const float y = r[j / 2][j & 1] * inv[j];
+            r[j / 2][j & 1] = y;
+            if (!(j & 1) && j + 1 < N) r[j / 2].y = fmaf(-y, col[j][j / 2].y, r[j / 2].y);
 #pragma unroll
-            for (int q2 = 0; q2 < i; ++q2) e = fmaf(-L[i][q2], r[q2], e);
-            r[i] = e * inv[i];
+            for (int p = j / 2 + 1; p < P; ++p) r[p] = pfma(splat(-y), col[j][p], r[p]);
         }
+        // L^T x = y, row dots over column i's rows > i (x_i itself is still 0)
+        // (full pairs packed; row i's partner and the pad row of an odd chain scalar)
+        f32x2 xs[P];
 #pragma unroll
-        for (int i = N - 1; i >= 0; --i) {      // L^T z = y
-            float e = r[i];
+        for (int i = N - 1; i >= 0; --i) {
+            float e = r[i / 2][i & 1];
+            if (!(i & 1) && i + 1 < N) e = fmaf(-col[i][i / 2].y, xs[i / 2].y, e);
+            constexpr int PF = N / 2;   // pairs [0, PF) hold two real rows
+            const int p0 = i / 2 + 1;
+            if (p0 < PF) {
+                f32x2 acc = col[i][p0] * xs[p0];
 #pragma unroll
-            for (int q2 = i + 1; q2 < N; ++q2) e = fmaf(-L[q2][i], r[q2], e);
-            r[i] = e * inv[i];
+                for (int p = p0 + 1; p < PF; ++p) acc = pfma(col[i][p], xs[p], acc);
+                e -= acc.x + acc.y;
+            }
+            if ((N & 1) && i < N - 1 && N / 2 >= p0) e = fmaf(-col[i][N / 2].x, xs[N / 2].x, e);
+            xs[i / 2][i & 1] = e * inv[i];
         }
-        float prev = 0.f;
+        // q_ddot = diff(theta_ddot); integrate
+        f32x2 qdd[P];
 #pragma unroll
-        for (int a = 0; a < N; ++a) {
-            dq[a] = fmaf(r[a] - prev, k.dt(), dq[a]);
-            prev = r[a];
-            q[a] = fmaf(dq[a], k.dt(), q[a]);
+        for (int a = 0; a < N; ++a) put(qdd, a, a ? get(xs, a) - get(xs, a - 1) : get(xs, 0));
+        const f32x2 dt = splat(k.dt());
+#pragma unroll
+        for (int p = 0; p < P; ++p) {
+            dq[p] = pfma(qdd[p], dt, dq[p]);
+            q[p] = pfma(dq[p], dt, q[p]);
         }
         angles();
     }
 
     template <class KC>
     __device__ __forceinline__ void effector(const KC& k, float* px, float* py) const {
-        float x = 0.f, y = 0.f;
+        f32x2 x = k.fk2(0) * c[0], y = k.fk2(0) * s[0];
 #pragma unroll
-        for (int a = 0; a < N; ++a) {
-            x = fmaf(k.fk(a), c[a], x);
-            y = fmaf(k.fk(a), s[a], y);
+        for (int p = 1; p < P; ++p) {
+            const f32x2 f = k.fk2(p);
+            x = pfma(f, c[p], x);
+            y = pfma(f, s[p], y);
         }
-        *px = x;
-        *py = y;
+        *px = x.x + x.y;
+        *py = y.x + y.y;
     }
 };
-
 // Median filter (control.py:319-327) of the T x N weighted noise, u += w_eps
 // (control.py:126), shift (control.py:148-149) and the next launch's fp32
 // per-step constants.  u_cur[ch]: this thread's cur->u value idx = tid + ch kCT,
@@ -241,7 +332,7 @@ __device__ void chain_update_block(ChainStep* nxt, const ChainConst& c, CScratch
 
 // POLL / counter hand-off and the merges as in rollout_kernel (mppi_rocm.hip).
 template <int N, bool POLL>
-__global__ __launch_bounds__(kCT) void chain_rollout_kernel(
+__global__ __launch_bounds__(kCT) __attribute__((amdgpu_waves_per_eu(2, 2))) void chain_rollout_kernel(
     const ChainConst c, const ChainStep* __restrict__ st, const float* __restrict__ dyn,
     const float* __restrict__ noise, double* __restrict__ S_out, double* __restrict__ slab, double* __restrict__ gslab,
     unsigned* __restrict__ counters, double* __restrict__ partial_out, double* __restrict__ w_eps_out,
@@ -265,6 +356,10 @@ __global__ __launch_bounds__(kCT) void chain_rollout_kernel(
     const int K = c.K_local, T = c.T;
 
     STAMP(0, NOW());
+#ifdef MPPI_STAMPS
+    STAMP(8, (unsigned long long)__builtin_amdgcn_s_getreg(0xF804));   // HW_ID
+    STAMP(9, (unsigned long long)__builtin_amdgcn_s_getreg(0xF814));   // XCC_ID
+#endif
     const unsigned tag_v = POLL ? __hip_atomic_load(epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) + 1u : 0u;
     double u_cur[kCMaxCh];
 #pragma unroll
@@ -279,16 +374,15 @@ __global__ __launch_bounds__(kCT) void chain_rollout_kernel(
     SearchLDS<true>::fill(s_keys, st->key, tid);
     SearchLDS<true> sr{s_keys, st->ctr.x, st->ctr.y};
     ChainState<N> x;
-#pragma unroll
-    for (int a = 0; a < N; ++a) {
-        x.q[a] = st->x0[a];
-        x.dq[a] = st->x0[N + a];
-    }
-    x.angles();
+    x.load(st->x0);
     // noise row (t, d) of sample k: noise[(t N + d) K + k]; prefetches past the
     // last step read row T - 1 again (never used)
-    const float* nk = noise + k;
-    auto nrow = [&](int t, int d) { return nk[((size_t)min(t, T - 1) * N + d) * K]; };
+    // (uniform row base + a 32-bit lane byte offset: the saddr form of global_load)
+    const unsigned kb = (unsigned)k * 4u;
+    auto nrow = [&](int t, int d) {
+        const char* row = (const char*)(noise + ((size_t)min(t, T - 1) * N + d) * K);
+        return *(const float*)(row + kb);
+    };
     cfloat* cua = (cfloat*)(&st->ua[0][0]);
     float ring[kCPF][N];
     float uring[kCPU][2 * N];
@@ -328,9 +422,9 @@ __global__ __launch_bounds__(kCT) void chain_rollout_kernel(
         const float4 r = s_win[sr.nearest(px, py)];
         ex = px - r.x;
         ey = py - r.y;
-        e1 = x.dq[0] - r.z;
-        e2 = x.dq[1] - r.w;
-        const float sw[4] = {kd.p[kOffSw], kd.p[kOffSw + 1], kd.p[kOffSw + 2], kd.p[kOffSw + 3]};
+        e1 = x.dqa(0) - r.z;
+        e2 = x.dqa(1) - r.w;
+        const float sw[4] = {kd.p[kOffSw], kd.p[kOffSw + 1], kd.p[kOffSw + 2], kd.p[kOffSw + 3]};   // control.py:185
         S4 += weighted_sq(ex, ey, e1, e2, sw) + g;
         if constexpr ((i & 3) == 3) {
             S += (double)S4;
@@ -344,7 +438,7 @@ __global__ __launch_bounds__(kCT) void chain_rollout_kernel(
         if (t + decltype(i_c)::value < T) step(t + decltype(i_c)::value, i_c);
     }, std::make_integer_sequence<int, 3>{});
     S += (double)S4;
-    S += (double)weighted_sq(ex, ey, e1, e2, c.tw);  // terminal cost, control.py:109
+    S += (double)weighted_sq(ex, ey, e1, e2, c.dyn + kOffTw);  // terminal cost, control.py:109
 
     STAMP(1, NOW());
     if (S_out && valid) S_out[k] = S;
@@ -508,12 +602,7 @@ __global__ __launch_bounds__(kCT) void chain_traj_kernel(const ChainConst c, con
     const int T = c.T;
     const float exf = noise ? ((c.k_offset + k) < c.k_exploit ? 1.f : 0.f) : 1.f;
     ChainState<N> x;
-#pragma unroll
-    for (int a = 0; a < N; ++a) {
-        x.q[a] = st->x0[a];
-        x.dq[a] = st->x0[N + a];
-    }
-    x.angles();
+    x.load(st->x0);
     for (int t = 0; t < T; ++t) {
         const int ti = t == 0 ? T - 1 : t - 1;
         float v[N];
@@ -522,12 +611,12 @@ __global__ __launch_bounds__(kCT) void chain_traj_kernel(const ChainConst c, con
             v[d] = base[ti * N + d];
             if (noise) v[d] = fmaf(exf, v[d], noise[((size_t)ti * N + d) * c.K_local + k]);
         }
-        x.step(v, DynArg{c});
+        x.step(v, DynArg{c.dyn});
         float* o = out + ((size_t)k * T + t) * 2 * N;
 #pragma unroll
         for (int a = 0; a < N; ++a) {
-            o[a] = x.q[a];
-            o[N + a] = x.dq[a];
+            o[a] = x.qa(a);
+            o[N + a] = x.dqa(a);
         }
     }
 }
@@ -687,28 +776,27 @@ int mppi_chain_ctx_create(const mppi_chain_config* cfg, int device, void* stream
     }
     k.nblocks = c->nblocks;
     k.n = n;
-    k.dt = (float)cfg->delta_t;
     const mppi_chain_params& P = cfg->chain;
+    float* dyn = k.dyn;
+    for (int a = 0; a < kCMax; ++a) dyn[kOffDd + a] = 1.f;   // pad rows
     for (int a = 0; a < n; ++a) {
         double tail = 0.0;
         for (int q = a + 1; q < n; ++q) tail += P.m[q];
         const double mu_aa = P.m[a] * P.lc[a] * P.lc[a] + P.l[a] * P.l[a] * tail;
         const double Jn = a + 1 < n ? P.J[a + 1] : 0.0;
-        k.Dd[a] = (float)(mu_aa + P.I[a] + P.J[a] + Jn);
-        k.offj[a] = (float)Jn;
-        k.damp[a] = (float)P.b[a];
-        k.gnu[a] = (float)(P.g * (P.m[a] * P.lc[a] + P.l[a] * tail));
-        k.fk[a] = (float)P.fk[a];
-        for (int b = a + 1; b < n; ++b) {
-            double tb = 0.0;
-            for (int q = b + 1; q < n; ++q) tb += P.m[q];
-            k.mu[a][b] = k.mu[b][a] = (float)(P.l[a] * (P.m[b] * P.lc[b] + P.l[b] * tb));
-        }
+        dyn[kOffL + a] = (float)P.l[a];
+        dyn[kOffNu + a] = (float)(P.m[a] * P.lc[a] + P.l[a] * tail);
+        dyn[kOffDd + a] = (float)(mu_aa + P.I[a] + P.J[a] + Jn);
+        dyn[kOffJ + 2 * a + ((a + 1) & 1)] = (float)(-Jn);   // row a+1 within its pair
+        dyn[kOffDamp + a] = (float)P.b[a];
+        dyn[kOffFk + a] = (float)P.fk[a];
     }
     for (int i = 0; i < 4; ++i) {
-        k.sw[i] = (float)(cfg->stage_cost_weight[i] * 10000.0);     // control.py:185
-        k.tw[i] = (float)(cfg->terminal_cost_weight[i] * 10000.0);  // control.py:198
+        dyn[kOffSw + i] = (float)(cfg->stage_cost_weight[i] * 10000.0);     // control.py:185
+        dyn[kOffTw + i] = (float)(cfg->terminal_cost_weight[i] * 10000.0);  // control.py:198
     }
+    dyn[kOffDt] = (float)cfg->delta_t;
+    dyn[kOffG] = (float)P.g;
     k.lambda = cfg->param_lambda;
     k.inv_lambda = 1.0 / cfg->param_lambda;
     k.gamma = cfg->param_lambda * (1.0 - cfg->param_alpha);
@@ -738,21 +826,6 @@ int mppi_chain_ctx_create(const mppi_chain_config* cfg, int device, void* stream
     const int ngroups = (c->nblocks + kGroup - 1) / kGroup;
     const size_t gslab = (size_t)ngroups * stride * val;
     const size_t ctr_bytes = ((size_t)(ngroups + 2) * sizeof(unsigned) + 255) & ~(size_t)255;
-    float dyn[kDynFloats] = {};
-    for (int a = 0; a < kCMax; ++a)
-        for (int b = a + 1; b < kCMax; ++b) dyn[tri_index(a, b)] = k.mu[a][b];
-    for (int a = 0; a < kCMax; ++a) {
-        dyn[kOffDd + a] = k.Dd[a];
-        dyn[kOffOffj + a] = k.offj[a];
-        dyn[kOffDamp + a] = k.damp[a];
-        dyn[kOffGnu + a] = k.gnu[a];
-        dyn[kOffFk + a] = k.fk[a];
-    }
-    for (int i = 0; i < 4; ++i) {
-        dyn[kOffSw + i] = k.sw[i];
-        dyn[kOffTw + i] = k.tw[i];
-    }
-    dyn[kOffDt] = k.dt;
     float chol[kCMax * kCMax] = {};
     for (int i = 0; i < n; ++i)
         for (int j = 0; j <= i; ++j) chol[i * kCMax + j] = (float)Lc[i][j];
@@ -762,7 +835,7 @@ int mppi_chain_ctx_create(const mppi_chain_config* cfg, int device, void* stream
         (e = hipMalloc(&c->d_weps, kCMaxVals * sizeof(double))) != hipSuccess ||
         (e = hipMalloc(&c->d_base, kCMaxVals * sizeof(float))) != hipSuccess ||
         (e = hipMalloc(&c->d_chol, sizeof(chol))) != hipSuccess ||
-        (e = hipMalloc(&c->d_dyn, sizeof(dyn))) != hipSuccess ||
+        (e = hipMalloc(&c->d_dyn, sizeof(k.dyn))) != hipSuccess ||
         (e = hipHostMalloc(&c->h_step, sizeof(ChainStep), hipHostMallocDefault)) != hipSuccess ||
         (e = hipHostMalloc(&c->h_buf, kCMaxVals * sizeof(double), hipHostMallocDefault)) != hipSuccess ||
         (e = hipHostMalloc(&c->h_base, kCMaxVals * sizeof(float), hipHostMallocDefault)) != hipSuccess ||
@@ -774,7 +847,7 @@ int mppi_chain_ctx_create(const mppi_chain_config* cfg, int device, void* stream
         (e = hipMemset(c->d_step, 0, 2 * sizeof(ChainStep))) != hipSuccess ||
         (e = hipMemset(c->d_weps, 0, kCMaxVals * sizeof(double))) != hipSuccess ||
         (e = hipMemcpy(c->d_chol, chol, sizeof(chol), hipMemcpyHostToDevice)) != hipSuccess ||
-        (e = hipMemcpy(c->d_dyn, dyn, sizeof(dyn), hipMemcpyHostToDevice)) != hipSuccess ||
+        (e = hipMemcpy(c->d_dyn, k.dyn, sizeof(k.dyn), hipMemcpyHostToDevice)) != hipSuccess ||
         (e = hipDeviceSynchronize()) != hipSuccess)
         return cleanup_fail(fail(MPPI_E_HIP, std::string("allocation: ") + hipGetErrorString(e)));
     memset(c->h_step, 0, sizeof(ChainStep));

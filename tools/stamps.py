@@ -1,6 +1,6 @@
 """Diagnostic timeline of the rollout kernel (stamp build, not the product).
 
-Usage: python tools/stamps.py LIB.so [K T steps]
+Usage: python tools/stamps.py LIB.so [K T steps]     (WORKLOAD=c5: the 7-link chain engine)
 Prints, per recorded step: kernel span, per-workgroup rollout / epilogue
 durations, the last workgroup's merge / update, and the sample / partial counts.
 """
@@ -24,13 +24,21 @@ T = int(sys.argv[3]) if len(sys.argv) > 3 else 64
 steps = int(sys.argv[4]) if len(sys.argv) > 4 else 12
 lam = float(os.environ.get("LAMBDA", "100"))
 torch.cuda.set_device(0)
-eng = RolloutEngine(K, T, 0.006, lam, 0.98, np.eye(2) * 20.0, [0.5, 0.5, 5, 5], [5, 5, 50, 50], 0.0, ArmParams(),
-                    device=0, lanes_per_sample=int(os.environ.get("LPS", "0")))
 path = np.load(os.path.join(ROOT, "tests", "golden", "paths.npz"))["xydq_circle"][:, :4]
-eng.set_step_inputs(X0_RUNPY, path[:30], np.array([[10.0, -2.0]] * T))
+if os.environ.get("WORKLOAD") == "c5":   # the 7-link chain engine (config 5)
+    from mppi_robotarm_amd.chain import CHAIN7_SIGMA, CHAIN7_X0, ChainEngine, gravity_torque
+    eng = ChainEngine(K, T, 0.006, lam, 0.98, CHAIN7_SIGMA, [0.5, 0.5, 5, 5], [5, 5, 50, 50], 0.0, device=0)
+    eng.set_step_inputs(CHAIN7_X0, path[:30], np.tile(gravity_torque(CHAIN7_X0[:7]), (T, 1)))
+    set_dbg = eng._lib.mppi_chain_debug_set_buffer
+    eng.lanes_per_sample = 1
+else:
+    eng = RolloutEngine(K, T, 0.006, lam, 0.98, np.eye(2) * 20.0, [0.5, 0.5, 5, 5], [5, 5, 50, 50], 0.0, ArmParams(),
+                        device=0, lanes_per_sample=int(os.environ.get("LPS", "0")))
+    eng.set_step_inputs(X0_RUNPY, path[:30], np.array([[10.0, -2.0]] * T))
+    set_dbg = eng._lib.mppi_debug_set_buffer
 noise = [eng.philox_noise(1234, i) for i in range(4)]
 dbg = torch.zeros(eng.blocks * 16, dtype=torch.int64, device="cuda")
-N.check(eng._lib.mppi_debug_set_buffer(eng._ctx, N.C.c_void_p(dbg.data_ptr())), "dbg")
+N.check(set_dbg(eng._ctx, N.C.c_void_p(dbg.data_ptr())), "dbg")
 print(f"K={K} T={T} lps={eng.lanes_per_sample} blocks={eng.blocks} lambda={lam} lib={os.path.basename(lib)}")
 S_dev = torch.empty(K, dtype=torch.float64, device="cuda")
 for i in range(steps):
