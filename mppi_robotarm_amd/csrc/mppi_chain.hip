@@ -54,7 +54,7 @@ struct alignas(16) ChainStep {
 // Launch constants (kernel argument, by value).
 constexpr int kCDyn = 72;
 struct ChainConst {
-    int K_local, T, k_offset, k_exploit, nblocks, acquire, n, pad0;
+    int K_local, T, k_offset, k_exploit, nblocks, acquire, n, cu_off;   // cu_off: per-CU tickets in counters[]
     alignas(8) float dyn[kCDyn];   // packed dynamics / cost constants (layout: kOff* below)
     double lambda, inv_lambda, gamma;
     double sig_inv[kCMax * kCMax];
@@ -345,11 +345,12 @@ __global__ __launch_bounds__(kCT) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
     __shared__ int s_cnt[kCT / 64];
     __shared__ int s_k[kCT];
     __shared__ float s_e[kCT];
-    __shared__ unsigned s_flag;
+    __shared__ unsigned s_flag, s_parity;
     __shared__ CScratch sm;
 
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const int k_raw = blockIdx.x * kCT + tid;
+    draw_cu_ticket(counters + c.cu_off, &s_parity);
     const bool valid = k_raw < c.K_local;
     const int k = valid ? k_raw : c.K_local - 1;
     const float exf = (c.k_offset + k) < c.k_exploit ? 1.f : 0.f;  // control.py:98-101
@@ -432,8 +433,11 @@ __global__ __launch_bounds__(kCT) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
         }
     };
     int t = 0;
-    for (; t + 4 <= T; t += 4)
+    const unsigned parity = __builtin_amdgcn_readfirstlane(s_parity);
+    for (; t + 4 <= T; t += 4) {
+        fair_priority(parity);
         unroll_seq([&](auto i_c) { step(t + decltype(i_c)::value, i_c); }, std::make_integer_sequence<int, 4>{});
+    }
     unroll_seq([&](auto i_c) {
         if (t + decltype(i_c)::value < T) step(t + decltype(i_c)::value, i_c);
     }, std::make_integer_sequence<int, 3>{});
@@ -825,7 +829,9 @@ int mppi_chain_ctx_create(const mppi_chain_config* cfg, int device, void* stream
     const size_t slab = (size_t)c->nblocks * stride * val;
     const int ngroups = (c->nblocks + kGroup - 1) / kGroup;
     const size_t gslab = (size_t)ngroups * stride * val;
-    const size_t ctr_bytes = ((size_t)(ngroups + 2) * sizeof(unsigned) + 255) & ~(size_t)255;
+    const size_t cu_off = (((size_t)(ngroups + 2) * sizeof(unsigned) + 255) & ~(size_t)255) / sizeof(unsigned);
+    const size_t ctr_bytes = (cu_off + kCuSlots) * sizeof(unsigned);
+    c->kc.cu_off = (int)cu_off;
     float chol[kCMax * kCMax] = {};
     for (int i = 0; i < n; ++i)
         for (int j = 0; j <= i; ++j) chol[i * kCMax + j] = (float)Lc[i][j];

@@ -755,6 +755,34 @@ __device__ __forceinline__ float2 box_muller(unsigned a, unsigned b) {
 
 }  // namespace mppi
 
+// Issue fairness between workgroups that share a CU.  The SIMD arbiter serves
+// the oldest ready wave first, so of two co-resident rollout waves the younger
+// one only fills the older one's issue gaps and then finishes alone at the
+// single-wave rate (measured on the chain kernel: older workgroups 174 us,
+// younger 277 us).  Each workgroup draws a per-CU ticket with one relaxed
+// atomic (co-resident workgroups draw consecutive tickets: different
+// parities), and waves raise their priority in alternate real-time phases of
+// 2^kPrioShift ticks (100 MHz: ~41 us), the phase flipped by the ticket parity.
+// Priority steers scheduling only; no result depends on it.
+constexpr int kCuSlots = 2048;   // (XCC, SE, SH, CU) keys
+constexpr int kPrioShift = 12;
+__device__ __forceinline__ unsigned cu_key() {
+    const unsigned hw = __builtin_amdgcn_s_getreg(0xF804);    // HW_ID
+    const unsigned xcc = __builtin_amdgcn_s_getreg(0xF814);   // XCC_ID
+    return ((xcc & 7u) << 8) | (((hw >> 13) & 7u) << 5) | (((hw >> 12) & 1u) << 4) | ((hw >> 8) & 0xFu);
+}
+// Thread 0 draws the ticket into *s_parity (read after the caller's next barrier).
+__device__ __forceinline__ void draw_cu_ticket(unsigned* cu_ctr, unsigned* s_parity) {
+    if (threadIdx.x == 0)
+        *s_parity = __hip_atomic_fetch_add(cu_ctr + cu_key(), 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) & 1u;
+}
+__device__ __forceinline__ void fair_priority(unsigned parity) {
+    if ((((unsigned)__builtin_amdgcn_s_memrealtime() >> kPrioShift) & 1u) ^ parity)
+        __builtin_amdgcn_s_setprio(1);
+    else
+        __builtin_amdgcn_s_setprio(0);
+}
+
 // Diagnostic builds only (-DMPPI_STAMPS, a separate .so): per-workgroup
 // timeline in s_memrealtime ticks (100 MHz) + counters.  Never in the product.
 #ifdef MPPI_STAMPS

@@ -2,10 +2,11 @@
 (diagnostic tool, not product).  Batches of fused launches alternate between
 the builds, so clock and thermal drift hit both alike.
 
-    python tools/ab.py LIB_A.so LIB_B.so [K T batches launches_per_batch]
+    python tools/ab.py LIB_A.so LIB_B.so [LIB_C.so ...] [K T batches launches_per_batch]
+    WORKLOAD=c5: the 7-link chain engine (default K 131072, T 128)
 
 Prints, per build, the median / min per-launch time (HIP events around each
-batch on the launching stream) and B / A.
+batch on the launching stream) and each build's ratio to the first.
 """
 import ctypes as C
 import os
@@ -36,15 +37,30 @@ def make_ctx(L, K, T, lam, stream):
     return ctx
 
 
-def main():
-    libs = [os.path.abspath(p) for p in sys.argv[1:3]]
-    K = int(sys.argv[3]) if len(sys.argv) > 3 else 65536
-    T = int(sys.argv[4]) if len(sys.argv) > 4 else 64
-    batches = int(sys.argv[5]) if len(sys.argv) > 5 else 40
-    per = int(sys.argv[6]) if len(sys.argv) > 6 else 50
-    lam = float(os.environ.get("LAMBDA", "100"))
-    torch.cuda.set_device(0)
-    stream = torch.cuda.current_stream().cuda_stream
+def chain_runs(libs, K, T, lam):
+    from mppi_robotarm_amd import chain as CH
+    path = np.load(os.path.join(ROOT, "tests", "golden", "paths.npz"))["xydq_circle"][:, :4]
+    runs = []
+    for p in libs:
+        L = N.open_library(p)
+        orig = N.load
+        N.load = lambda L=L: L
+        try:
+            eng = CH.ChainEngine(K, T, 0.006, lam, 0.98, CH.CHAIN7_SIGMA, [0.5, 0.5, 5, 5], [5, 5, 50, 50], 0.0,
+                                 device=0)
+        finally:
+            N.load = orig
+        eng.set_step_inputs(CH.CHAIN7_X0, path[:30], np.tile(CH.gravity_torque(CH.CHAIN7_X0[:7]), (T, 1)))
+        noise = [eng.philox_noise(1234, i) for i in range(4)]
+
+        def batch(n, eng=eng, noise=noise):
+            for i in range(n):
+                eng.rollout(noise[i % len(noise)], fused_update=True)
+        runs.append((p, batch, eng.close, []))
+    return runs
+
+
+def arm_runs(libs, K, T, lam, stream):
     path = np.load(os.path.join(ROOT, "tests", "golden", "paths.npz"))["xydq_circle"][:, :4]
     win = np.ascontiguousarray(path[:30])
     u = np.array([[10.0, -2.0]] * T)
@@ -58,33 +74,47 @@ def main():
         noise = [torch.empty(T * K * 2, dtype=torch.float32, device="cuda") for _ in range(8)]
         for i, nz in enumerate(noise):
             assert L.mppi_noise_philox(ctx, 1234, i, C.c_void_p(nz.data_ptr())) == 0
-        runs.append((L, ctx, noise, []))
+
+        def batch(n, L=L, ctx=ctx, noise=noise):
+            for i in range(n):
+                assert L.mppi_rollout(ctx, C.c_void_p(noise[i % len(noise)].data_ptr()), None, None, 1) == 0
+        runs.append((p, batch, lambda L=L, ctx=ctx: L.mppi_ctx_destroy(ctx), []))
+    return runs
+
+
+def main():
+    libs = [os.path.abspath(a) for a in sys.argv[1:] if a.endswith(".so")]
+    nums = [a for a in sys.argv[1:] if not a.endswith(".so")]
+    c5 = os.environ.get("WORKLOAD") == "c5"
+    K = int(nums[0]) if len(nums) > 0 else (131072 if c5 else 65536)
+    T = int(nums[1]) if len(nums) > 1 else (128 if c5 else 64)
+    batches = int(nums[2]) if len(nums) > 2 else (16 if c5 else 40)
+    per = int(nums[3]) if len(nums) > 3 else (20 if c5 else 50)
+    lam = float(os.environ.get("LAMBDA", "100"))
+    torch.cuda.set_device(0)
+    stream = torch.cuda.current_stream().cuda_stream
+    runs = chain_runs(libs, K, T, lam) if c5 else arm_runs(libs, K, T, lam, stream)
     torch.cuda.synchronize()
-
-    def batch(L, ctx, noise, n):
-        for i in range(n):
-            rc = L.mppi_rollout(ctx, C.c_void_p(noise[i % len(noise)].data_ptr()), None, None, 1)
-            assert rc == 0
-
-    for L, ctx, noise, _ in runs:   # warm-up
-        batch(L, ctx, noise, 20)
+    for _, batch, _, _ in runs:   # warm-up
+        batch(10)
     torch.cuda.synchronize()
     for b in range(batches):
         order = runs if b % 2 == 0 else runs[::-1]
-        for L, ctx, noise, times in order:
+        for _, batch, _, times in order:
             e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
             e0.record()
-            batch(L, ctx, noise, per)
+            batch(per)
             e1.record()
             torch.cuda.synchronize()
             times.append(e0.elapsed_time(e1) * 1e3 / per)
-    med = []
-    for p, (L, ctx, noise, times) in zip(libs, runs):
+    base = None
+    for p, _, close, times in runs:
         t = np.array(times)
-        med.append(np.median(t))
-        print(f"{os.path.basename(p):36s} median {np.median(t):7.2f} us  min {t.min():7.2f}  max {t.max():7.2f}")
-        L.mppi_ctx_destroy(ctx)
-    print(f"B/A = {med[1] / med[0]:.4f}  (K={K} T={T} lambda={lam}, {batches} x {per} launches each)")
+        base = np.median(t) if base is None else base
+        print(f"{os.path.basename(p):36s} median {np.median(t):7.2f} us  min {t.min():7.2f}  max {t.max():7.2f}"
+              f"  x{np.median(t) / base:.4f}")
+        close()
+    print(f"(K={K} T={T} lambda={lam} {'chain' if c5 else 'arm'}, {batches} x {per} launches each)")
 
 
 if __name__ == "__main__":

@@ -63,5 +63,28 @@ for i in range(steps):
           f"grp-arrive {us(d[last, 3]):5.1f} grp-merge {us(d[last, 10]):5.1f} fin-arrive {us(d[last, 4]):5.1f} "
           f"fin-merge {us(d[last, 11]):5.1f} update {us(d[last, 7]):5.1f} | nl med {np.median(d[:, 5]):.0f} max {d[:, 5].max()} "
           f"| rows {d[last, 6]}")
+if os.environ.get("DUMP"):   # the last step: rollout time of the older / younger workgroup sharing a CU
+    order = np.argsort(d[:, 0])
+    first = {}
+    older, younger = [], []
+    for b in order:
+        if cu[b] in first:
+            younger.append(roll[b]); older.append(roll[first[cu[b]]])
+        else:
+            first[cu[b]] = b
+    older, younger = np.array(older), np.array(younger)
+    pct = lambda a: " ".join(f"{np.percentile(a, q):6.1f}" for q in (0, 10, 50, 90, 100))
+    print(f"rollout pct 0/10/50/90/100: all {pct(roll)}")
+    if len(older):
+        print(f"  older wg on its CU {pct(older)} | younger {pct(younger)} | start skew med "
+              f"{np.median([(d[b, 0] - d[first[cu[b]], 0]) / 100.0 for b in order if first[cu[b]] != b]):.2f} us")
+    wid = hw & 0xF
+    ob = [first[cu[b]] for b in order if first[cu[b]] != b]
+    yb = [b for b in order if first[cu[b]] != b]
+    print(f"  HW_ID.WAVE_ID of wave 0: older {np.bincount(wid[ob], minlength=8).tolist()} younger "
+          f"{np.bincount(wid[yb], minlength=8).tolist()} | younger blockIdx >= nblocks/2: "
+          f"{np.mean(np.array(yb) >= len(d) // 2):.2f}")
+    xcc = d[:, 9] & 0xF
+    print("  per-XCD median rollout " + " ".join(f"{np.median(roll[xcc == x]):6.1f}" for x in np.unique(xcc)))
 u = eng.nominal()
 print("final nominal u range", u.min(0), u.max(0))

@@ -57,7 +57,8 @@ def main():
     write = np.median(counters(os.path.join(src, "write", "p_counter_collection.csv"), kpat)["WRITE_SIZE"])
     cf = counters(os.path.join(src, "cfetch", "p_counter_collection.csv"), "calib")["FETCH_SIZE"]
     cw = counters(os.path.join(src, "cwrite", "p_counter_collection.csv"), "calib")["WRITE_SIZE"]
-    known_read, known_write = 33554432, 262144     # tools/calib_fetch.hip
+    # tools/calib_fetch.hip: 8 B/lane [T][K][2] (K 65536, T 64), or `4`: 4 B/lane [T][7][K] (K 131072, T 16)
+    known_read, known_write = (58720256, 524288) if workload == "c5" else (33554432, 262144)
     f_ratio = np.median(cf) * 1024 / known_read
     w_ratio = np.median(cw) * 1024 / known_write
     read_b = fetch * 1024 / f_ratio
@@ -71,7 +72,8 @@ def main():
         "algorithmic_bytes_per_launch": alg,
         "traffic_over_algorithmic": (read_b + write_b) / alg,
         "FETCH_SIZE_KB_median": fetch, "WRITE_SIZE_KB_median": write,
-        "calibration": {"kernel": "tools/calib_fetch.hip (same 8 B/lane [T][K][2] row pattern)",
+        "calibration": {"kernel": "tools/calib_fetch.hip " + ("4 (the chain's 4 B/lane [T][7][K] rows)" if workload == "c5"
+                                                              else "(same 8 B/lane [T][K][2] row pattern)"),
                         "known_read_bytes": known_read, "FETCH_SIZE_KB": float(np.median(cf)),
                         "fetch_reported_over_true": f_ratio, "known_write_bytes": known_write,
                         "WRITE_SIZE_KB": float(np.median(cw)), "write_reported_over_true": w_ratio},
