@@ -50,8 +50,11 @@ C5_BYTES_PER_STATE_STEP = 28  # fp32 eps[t][0:7][k] read once ("C5 
 def parse():
     p = argparse.ArgumentParser()
     p.add_argument("--gpus", type=int, default=1)
-    p.add_argument("--steps", type=int, default=200)
-    p.add_argument("--warmup", type=int, default=20)
+    p.add_argument("--steps", type=int, default=1000)
+    p.add_argument("--warmup", type=int, default=100)
+    p.add_argument("--settle-ms", type=float, default=200.0,
+                   help="untimed steps for this long before the W warmup steps: the GPU clock takes ~0.1 s of "
+                        "load to ramp (measured: 33.4 us/step after 20 warmup steps, 30.9 after 2000)")
     p.add_argument("--workload", choices=("c3", "c5"), default="c3",
                    help="c3: 2-DoF arm, K per GPU (BASELINE metric); c5: 7-DoF chain, K total (config 5)")
     p.add_argument("--K", type=int, default=None, help="c3: samples per GPU (65536); c5: samples in total (131072)")
@@ -187,6 +190,18 @@ def main():
             exchange_partials(partial, gathered)
             eng.merge(gathered, world, fused_update=True)
 
+    # clock settle (untimed): a controller runs continuously, so the metric is
+    # the steady-state rate; then the W warmup steps of the contract
+    t_settle = time.perf_counter()
+    i = 0
+    while (time.perf_counter() - t_settle) * 1e3 < args.settle_ms:   # rank-local: no collectives
+        for _ in range(16):
+            if world == 1:
+                eng.rollout(noise[i % args.nbuf], fused_update=True)
+            else:
+                eng.rollout(noise[i % args.nbuf], partial_out=partial)
+            i += 1
+        torch.cuda.synchronize()
     for i in range(args.warmup):
         step(i)
     torch.cuda.synchronize()
@@ -260,7 +275,7 @@ def main():
             "unit": "state-steps/s",
             "n_gpus": world,
             "steps": args.steps,
-            "warmup": args.warmup,
+            "warmup": args.warmup, "settle_ms": args.settle_ms,
             "ms_per_step": ms_per_step,
             "rollouts_per_s": K_total * args.steps / elapsed,
             "control_step_latency_ms": ms_per_step,

@@ -4,6 +4,7 @@ the builds, so clock and thermal drift hit both alike.
 
     python tools/ab.py LIB_A.so LIB_B.so [LIB_C.so ...] [K T batches launches_per_batch]
     WORKLOAD=c5: the 7-link chain engine (default K 131072, T 128)
+    LPS=n: lanes per sample of every arm build; LPS_LIST=a,b,...: per build (the same .so may repeat)
 
 Prints, per build, the median / min per-launch time (HIP events around each
 batch on the launching stream) and each build's ratio to the first.
@@ -21,7 +22,7 @@ from mppi_robotarm_amd import _native as N  # noqa: E402
 from mppi_robotarm_amd.params import X0_RUNPY, ArmParams  # noqa: E402
 
 
-def make_ctx(L, K, T, lam, stream):
+def make_ctx(L, K, T, lam, stream, lps=0):
     a = ArmParams()
     cfg = N.ConfigC()
     cfg.K_local, cfg.T, cfg.K_total, cfg.k_offset = K, T, K, 0
@@ -30,7 +31,7 @@ def make_ctx(L, K, T, lam, stream):
     cfg.stage_cost_weight = (C.c_double * 4)(0.5, 0.5, 5, 5)
     cfg.terminal_cost_weight = (C.c_double * 4)(5, 5, 50, 50)
     cfg.arm = N.ArmParamsC(a.m1, a.m2, a.l1, a.l2, a.lc1, a.lc2, a.g, a.fk_l1, a.fk_l2)
-    cfg.lanes_per_sample = int(os.environ.get("LPS", "0"))
+    cfg.lanes_per_sample = lps
     ctx = C.c_void_p()
     rc = L.mppi_ctx_create(C.byref(cfg), 0, C.c_void_p(stream), C.byref(ctx))
     assert rc == 0, L.mppi_last_error()
@@ -66,9 +67,10 @@ def arm_runs(libs, K, T, lam, stream):
     u = np.array([[10.0, -2.0]] * T)
     dp = lambda a: a.ctypes.data_as(C.POINTER(C.c_double))
     runs = []
-    for p in libs:
+    lps = [int(x) for x in os.environ.get("LPS_LIST", "").split(",") if x] or [int(os.environ.get("LPS", "0"))] * len(libs)
+    for p, lp in zip(libs, lps):
         L = N.open_library(p)
-        ctx = make_ctx(L, K, T, lam, stream)
+        ctx = make_ctx(L, K, T, lam, stream, lp)
         x0 = np.asarray(X0_RUNPY, dtype=np.float64)
         assert L.mppi_set_step_inputs(ctx, dp(x0), dp(win), 30, dp(u)) == 0
         noise = [torch.empty(T * K * 2, dtype=torch.float32, device="cuda") for _ in range(8)]
@@ -78,7 +80,7 @@ def arm_runs(libs, K, T, lam, stream):
         def batch(n, L=L, ctx=ctx, noise=noise):
             for i in range(n):
                 assert L.mppi_rollout(ctx, C.c_void_p(noise[i % len(noise)].data_ptr()), None, None, 1) == 0
-        runs.append((p, batch, lambda L=L, ctx=ctx: L.mppi_ctx_destroy(ctx), []))
+        runs.append((f"{os.path.basename(p)} lps={lp}", batch, lambda L=L, ctx=ctx: L.mppi_ctx_destroy(ctx), []))
     return runs
 
 
