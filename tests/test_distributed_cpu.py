@@ -105,3 +105,65 @@ def test_exchange_rejects_bad_shapes(tmp_path):
         assert g.tolist() == [0.0, 1.0, 2.0, 3.0]
     finally:
         dist.destroy_process_group()
+
+
+def _chain_inputs(K, T):
+    import chain_oracle as CO
+    rng = np.random.default_rng(8)
+    x0 = np.concatenate([[1.481492] + [-0.320757] * 6, [0.0] * 7])
+    sig = np.diag([20.0, 16.0, 12.0, 8.0, 4.0, 2.0, 1.0])
+    u = np.tile(CO.gravity_torque(x0[:7], CO.ChainParams()), (T, 1))
+    eps = (rng.standard_normal((K, T, 7)) * np.sqrt(np.diag(sig))).astype(np.float32)
+    return x0, u, sig, eps
+
+
+def _chain_worker(rank, world, port, K, T, out_path):
+    import sys
+    sys.path.insert(0, ROOT)
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import chain_oracle as CO
+    import coracle
+    from mppi_robotarm_amd.distributed import exchange_partials, shard_geometry
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        path = np.load(os.path.join(GOLDEN, "paths.npz"))["xydq_circle"][:, :4]
+        x0, u, sig, eps = _chain_inputs(K, T)
+        n, off = shard_geometry(K, world, rank)
+        S = coracle.chain_rollout_costs(x0, u, eps, path[:30], 0.006, CHAIN_LAM, 0.98, sig, [0.5, 0.5, 5.0, 5.0],
+                                        [5.0, 5.0, 50.0, 50.0], CO.ChainParams(), k_range=(off, off + n))
+        partial = torch.from_numpy(_partial_row(S, eps[off:off + n], CHAIN_LAM))   # 2 + 7 T values
+        gathered = torch.empty(world * partial.numel(), dtype=torch.float64)
+        exchange_partials(partial, gathered)
+        rows = gathered.numpy().reshape(world, -1)
+        rho = rows[:, 0].min()
+        s = np.exp((rho - rows[:, 0]) / CHAIN_LAM)
+        w_eps = ((s[:, None] * rows[:, 2:]).sum(0) / (s * rows[:, 1]).sum()).reshape(T, 7)
+        np.save(f"{out_path}.{rank}.npy", w_eps)
+    finally:
+        dist.destroy_process_group()
+
+
+CHAIN_LAM = 1.0e4
+
+
+@pytest.mark.parametrize("K,T", [(300, 12), (131, 5)])
+def test_chain_sharded_exchange_matches_unsharded(tmp_path, K, T):
+    """Config 5's exchange: the 7-link chain's (2 + 7T) partial rows over 2 ranks."""
+    import sys
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import chain_oracle as CO
+    import coracle
+    world = 2
+    out = str(tmp_path / "weps")
+    mp.start_processes(_chain_worker, args=(world, _free_port(), K, T, out), nprocs=world, join=True,
+                       start_method="spawn")
+    r0, r1 = np.load(out + ".0.npy"), np.load(out + ".1.npy")
+    assert np.array_equal(r0, r1)
+    path = np.load(os.path.join(GOLDEN, "paths.npz"))["xydq_circle"][:, :4]
+    x0, u, sig, eps = _chain_inputs(K, T)
+    S = coracle.chain_rollout_costs(x0, u, eps, path[:30], 0.006, CHAIN_LAM, 0.98, sig, [0.5, 0.5, 5.0, 5.0],
+                                    [5.0, 5.0, 50.0, 50.0], CO.ChainParams())
+    w, ref = coracle.chain_weighted_noise(S, eps, CHAIN_LAM)
+    assert 1.0 / np.sum(w ** 2) > 3            # several samples carry weight
+    np.testing.assert_allclose(r0, ref, rtol=1e-10, atol=1e-12)
