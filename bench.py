@@ -38,7 +38,7 @@ import torch
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
-from mppi_robotarm_amd.distributed import exchange_partials  # noqa: E402
+from mppi_robotarm_amd.distributed import attach_exchange, check_exchange, exchange_partials  # noqa: E402
 from mppi_robotarm_amd.engine import RolloutEngine  # noqa: E402
 from mppi_robotarm_amd.params import ArmParams, X0_RUNPY  # noqa: E402
 
@@ -67,6 +67,9 @@ def parse():
     p.add_argument("--launch", choices=("eager", "graph"), default="eager",
                    help="N = 1: back-to-back launches from the host loop (default) or replay of a captured HIP graph")
     p.add_argument("--backend", default="nccl", help="torch.distributed backend for N > 1 (nccl = RCCL)")
+    p.add_argument("--exchange", choices=("auto", "launch", "rccl"), default="auto",
+                   help="N > 1: partial rows exchanged inside the rollout launch (IPC inboxes over xGMI; auto: "
+                        "after a one-step check against RCCL, else RCCL) or by an RCCL all_gather + merge launch")
     return p.parse_args()
 
 
@@ -177,16 +180,25 @@ def main():
     chunk = args.nbuf if use_graph else 1
     steps = (args.steps + chunk - 1) // chunk * chunk
 
+    xmode = "none" if world == 1 else "rccl"
+    if world > 1 and args.exchange != "rccl":
+        ok = attach_exchange(eng) and check_exchange(eng, noise[0], partial, gathered)
+        if not ok and args.exchange == "launch":
+            raise RuntimeError("in-launch exchange unavailable")
+        xmode = "launch" if ok else "rccl"
+
     def step(i, ev_pair=None):
         if ev_pair is not None:
             ev_pair[0].record(stream)
         if world == 1:
             eng.rollout(noise[i % args.nbuf], fused_update=True)
+        elif xmode == "launch":
+            eng.rollout(noise[i % args.nbuf], fused_update=True, exchange=True)
         else:
             eng.rollout(noise[i % args.nbuf], partial_out=partial)
         if ev_pair is not None:
             ev_pair[1].record(stream)
-        if world > 1:
+        if xmode == "rccl":
             exchange_partials(partial, gathered)
             eng.merge(gathered, world, fused_update=True)
 
@@ -224,7 +236,7 @@ def main():
     ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(nev)]
     whole = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
     t0 = time.perf_counter()
-    if world == 1:
+    if world == 1 or xmode == "launch":
         # one event pair around the whole timed region on the launch stream
         whole[0].record(stream)
         for c in range(nev):
@@ -243,7 +255,7 @@ def main():
     elapsed = time.perf_counter() - t0
     # average duration per launch of the rollout kernel (events on the launch
     # stream); at N = 1 the back-to-back launches' average, boundaries included
-    if world == 1:
+    if world == 1 or xmode == "launch":
         kern_ms = whole[0].elapsed_time(whole[1]) / steps
     else:
         kern_ms = sum(a.elapsed_time(b) for a, b in ev) / steps
@@ -292,7 +304,9 @@ def main():
                                     f"xydq_circle.txt window, Philox N(0,20I) noise x{args.nbuf} buffers"),
                        "K_total": K_total, "K_per_gpu": K, "T": T,
                        "lanes_per_sample": 1 if c5 else eng.lanes_per_sample,
-                       "parallelism": f"samples sharded x{world}, RCCL all_gather of partials" if world > 1
+                       "parallelism": (f"samples sharded x{world}, " + (
+                           "partial rows exchanged inside the rollout launch (IPC inboxes over xGMI)"
+                           if xmode == "launch" else "RCCL all_gather of partials + merge launch")) if world > 1
                        else "single device, fused update" + (f", HIP graph of {chunk} steps" if use_graph
                                                                else ", back-to-back launches")},
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",

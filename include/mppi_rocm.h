@@ -35,6 +35,10 @@ extern "C" {
 /* rollout flags */
 #define MPPI_FLAG_FUSED_UPDATE 1u  /* last workgroup also runs median filter, u += w_eps, */
                                    /* shift (control.py:122-149) on device                */
+#define MPPI_FLAG_EXCHANGE 2u      /* multi-GPU: the launch exchanges the ranks' partial  */
+                                   /* rows itself and merges them (mppi_exchange_attach)  */
+#define MPPI_IPC_HANDLE_BYTES 64   /* hipIpcMemHandle_t                                    */
+#define MPPI_MAX_WORLD 8           /* ranks of one node for the in-launch exchange         */
 
 /* Arm constants.  m1..g: sys_params.py:1-13, read by _F (control.py:11-18,
  * 241-251).  fk_l1/fk_l2: the link lengths the cost's forward kinematics uses,
@@ -105,6 +109,24 @@ int mppi_rollout(mppi_ctx *ctx, const float *noise_dev, double *S_dev, double *p
  * rank's partial_dev) with a log-sum-exp rescale into w_eps; with
  * MPPI_FLAG_FUSED_UPDATE also run the update of control.py:122-149 on device. */
 int mppi_merge_partials(mppi_ctx *ctx, const double *partials_dev, int n, unsigned flags);
+
+/* In-launch multi-GPU exchange (one process per GPU on one node; the reference
+ * is single-process, so this, like mppi_merge_partials, completes
+ * control.py:112-118 across devices).  Setup, once per context:
+ *   mppi_exchange_handle(ctx, world, h)  allocates this rank's inbox (uncached
+ *     device memory, 2 x world partial rows of tagged granules) and writes its
+ *     IPC handle (MPPI_IPC_HANDLE_BYTES) to h;
+ *   the caller all-gathers the handles over its process group (rank order);
+ *   mppi_exchange_attach(ctx, rank, world, handles)  maps every peer's inbox.
+ * Then mppi_rollout(..., partial_dev = NULL, MPPI_FLAG_EXCHANGE [| FUSED_UPDATE])
+ * on every rank: the launch's final workgroup writes this rank's partial row
+ * into every inbox (xGMI stores), polls its own until all world rows of the
+ * step arrived, merges them in rank order and (fused) updates the nominal — no
+ * collective call or second launch per step.  Every rank must run the same
+ * sequence of exchange launches.  A peer that never arrives ends the poll after
+ * ~1 s with a timeout that mppi_sync reports. */
+int mppi_exchange_handle(mppi_ctx *ctx, int world, void *handle_out);
+int mppi_exchange_attach(mppi_ctx *ctx, int rank, int world, const void *handles);
 
 /* D2H (synchronising) reads of the last step's results. */
 int mppi_get_weighted_noise(mppi_ctx *ctx, double *w_eps_host /* [T][2] */);
@@ -184,6 +206,10 @@ int mppi_chain_set_step_inputs(mppi_chain_ctx *ctx, const double *x0, const doub
 int mppi_chain_rollout(mppi_chain_ctx *ctx, const float *noise_dev, double *S_dev, double *partial_dev,
                        unsigned flags);
 int mppi_chain_merge_partials(mppi_chain_ctx *ctx, const double *partials_dev, int n, unsigned flags);
+/* In-launch exchange for the chain (as mppi_exchange_handle / _attach; rows of
+ * 2 + nT values). */
+int mppi_chain_exchange_handle(mppi_chain_ctx *ctx, int world, void *handle_out);
+int mppi_chain_exchange_attach(mppi_chain_ctx *ctx, int rank, int world, const void *handles);
 int mppi_chain_get_weighted_noise(mppi_chain_ctx *ctx, double *w_eps_host);
 int mppi_chain_get_nominal(mppi_chain_ctx *ctx, double *u_host);
 /* control.py:129-145 analogue: out_dev[K][T][2n] fp32 (q, dq) */

@@ -19,14 +19,19 @@ MPPI_E_ARG = -1
 MPPI_E_HIP = -2
 MPPI_E_SINGULAR = -3
 MPPI_FLAG_FUSED_UPDATE = 1
+MPPI_FLAG_EXCHANGE = 2
+MPPI_IPC_HANDLE_BYTES = 64
+MPPI_MAX_WORLD = 8
 
 # every symbol the header declares (tests check the library exports all of them)
 EXPORTS = (
     "mppi_ctx_create", "mppi_ctx_destroy", "mppi_last_error", "mppi_set_stream", "mppi_ctx_info", "mppi_ctx_handoff",
-    "mppi_set_step_inputs", "mppi_rollout", "mppi_merge_partials", "mppi_get_weighted_noise",
+    "mppi_set_step_inputs", "mppi_rollout", "mppi_merge_partials", "mppi_exchange_handle", "mppi_exchange_attach",
+    "mppi_get_weighted_noise",
     "mppi_get_nominal", "mppi_rollout_traj", "mppi_noise_philox", "mppi_sync", "mppi_debug_set_buffer",
     "mppi_chain_ctx_create", "mppi_chain_ctx_destroy", "mppi_chain_set_stream", "mppi_chain_ctx_info",
-    "mppi_chain_set_step_inputs", "mppi_chain_rollout", "mppi_chain_merge_partials",
+    "mppi_chain_set_step_inputs", "mppi_chain_rollout", "mppi_chain_merge_partials", "mppi_chain_exchange_handle",
+    "mppi_chain_exchange_attach",
     "mppi_chain_get_weighted_noise", "mppi_chain_get_nominal", "mppi_chain_rollout_traj",
     "mppi_chain_noise_philox", "mppi_chain_sync", "mppi_chain_debug_set_buffer",
 )
@@ -88,6 +93,8 @@ def open_library(path: str):
         "mppi_set_step_inputs": ([vp, dp, dp, C.c_int, dp], C.c_int),
         "mppi_rollout": ([vp, fp, vp, vp, C.c_uint], C.c_int),
         "mppi_merge_partials": ([vp, vp, C.c_int, C.c_uint], C.c_int),
+        "mppi_exchange_handle": ([vp, C.c_int, vp], C.c_int),
+        "mppi_exchange_attach": ([vp, C.c_int, C.c_int, vp], C.c_int),
         "mppi_get_weighted_noise": ([vp, dp], C.c_int),
         "mppi_get_nominal": ([vp, dp], C.c_int),
         "mppi_rollout_traj": ([vp, dp, fp, C.c_int, fp], C.c_int),
@@ -101,6 +108,8 @@ def open_library(path: str):
         "mppi_chain_set_step_inputs": ([vp, dp, dp, C.c_int, dp], C.c_int),
         "mppi_chain_rollout": ([vp, fp, vp, vp, C.c_uint], C.c_int),
         "mppi_chain_merge_partials": ([vp, vp, C.c_int, C.c_uint], C.c_int),
+        "mppi_chain_exchange_handle": ([vp, C.c_int, vp], C.c_int),
+        "mppi_chain_exchange_attach": ([vp, C.c_int, C.c_int, vp], C.c_int),
         "mppi_chain_get_weighted_noise": ([vp, dp], C.c_int),
         "mppi_chain_get_nominal": ([vp, dp], C.c_int),
         "mppi_chain_rollout_traj": ([vp, dp, fp, C.c_int, fp], C.c_int),

@@ -55,6 +55,7 @@ struct alignas(16) ChainStep {
 constexpr int kCDyn = 72;
 struct ChainConst {
     int K_local, T, k_offset, k_exploit, nblocks, acquire, n, cu_off;   // cu_off: per-CU tickets in counters[]
+    int fair, pad0;   // fair: > 1 workgroup per CU (fair_priority)
     alignas(8) float dyn[kCDyn];   // packed dynamics / cost constants (layout: kOff* below)
     double lambda, inv_lambda, gamma;
     double sig_inv[kCMax * kCMax];
@@ -336,7 +337,7 @@ __global__ __launch_bounds__(kCT) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
     const ChainConst c, const ChainStep* __restrict__ st, const float* __restrict__ dyn,
     const float* __restrict__ noise, double* __restrict__ S_out, double* __restrict__ slab, double* __restrict__ gslab,
     unsigned* __restrict__ counters, double* __restrict__ partial_out, double* __restrict__ w_eps_out,
-    ChainStep* __restrict__ nxt, unsigned flags, unsigned* __restrict__ epoch, unsigned* __restrict__ tmo,
+    ChainStep* __restrict__ nxt, unsigned flags, const XDesc xd, unsigned* __restrict__ epoch, unsigned* __restrict__ tmo,
     unsigned long long* __restrict__ dbg) {
     static_assert(N <= kCMax && N >= 2, "links");
     __shared__ float4 s_win[kSlots];
@@ -350,7 +351,7 @@ __global__ __launch_bounds__(kCT) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
 
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const int k_raw = blockIdx.x * kCT + tid;
-    draw_cu_ticket(counters + c.cu_off, &s_parity);
+    if (c.fair) draw_cu_ticket(counters + c.cu_off, &s_parity);
     const bool valid = k_raw < c.K_local;
     const int k = valid ? k_raw : c.K_local - 1;
     const float exf = (c.k_offset + k) < c.k_exploit ? 1.f : 0.f;  // control.py:98-101
@@ -433,9 +434,9 @@ __global__ __launch_bounds__(kCT) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
         }
     };
     int t = 0;
-    const unsigned parity = __builtin_amdgcn_readfirstlane(s_parity);
+    const unsigned parity = c.fair ? __builtin_amdgcn_readfirstlane(s_parity) : 2u;
     for (; t + 4 <= T; t += 4) {
-        fair_priority(parity);
+        if (parity < 2u) fair_priority(parity);
         unroll_seq([&](auto i_c) { step(t + decltype(i_c)::value, i_c); }, std::make_integer_sequence<int, 4>{});
     }
     unroll_seq([&](auto i_c) {
@@ -571,6 +572,7 @@ __global__ __launch_bounds__(kCT) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
     }
     STAMP(11, NOW());
     STAMP(6, (unsigned long long)sm.nrel);
+    if (flags & MPPI_FLAG_EXCHANGE) exchange_merge<kCT, kCMaxCh>(xd, geo, c.inv_lambda, sm, w_eps_out, tmo);
     if (flags & MPPI_FLAG_FUSED_UPDATE) chain_update_block<N>(nxt, c, sm, u_cur);
     STAMP(7, NOW());
 }
@@ -682,6 +684,13 @@ struct mppi_chain_ctx {
     unsigned* h_tmo = nullptr;
     unsigned* d_tmo = nullptr;
     unsigned long long* d_dbg = nullptr;
+    // node-level exchange (mppi_chain_exchange_*), as in mppi_ctx
+    XDesc xd{};
+    void* d_inbox = nullptr;
+    double* d_xrow = nullptr;
+    unsigned* d_xepoch = nullptr;
+    int xworld_alloc = 0;
+    void* xopened[kMaxWorld] = {};
 };
 
 namespace {
@@ -692,7 +701,7 @@ template <int N, bool P>
 void launch_rollout(mppi_chain_ctx* c, const ChainStep* cur, const float* noise, double* S, double* part, ChainStep* nxt,
                     unsigned flags) {
     hipLaunchKernelGGL((chain_rollout_kernel<N, P>), dim3(c->nblocks), dim3(kCT), 0, c->stream, c->kc, cur, c->d_dyn, noise, S,
-                       c->d_slab, c->d_gslab, c->d_counter, part, c->d_weps, nxt, flags, c->d_epoch, c->d_tmo,
+                       c->d_slab, c->d_gslab, c->d_counter, part, c->d_weps, nxt, flags, c->xd, c->d_epoch, c->d_tmo,
                        c->d_dbg);
 }
 
@@ -832,6 +841,7 @@ int mppi_chain_ctx_create(const mppi_chain_config* cfg, int device, void* stream
     const size_t cu_off = (((size_t)(ngroups + 2) * sizeof(unsigned) + 255) & ~(size_t)255) / sizeof(unsigned);
     const size_t ctr_bytes = (cu_off + kCuSlots) * sizeof(unsigned);
     c->kc.cu_off = (int)cu_off;
+    c->kc.fair = c->nblocks > ncu ? 1 : 0;
     float chol[kCMax * kCMax] = {};
     for (int i = 0; i < n; ++i)
         for (int j = 0; j <= i; ++j) chol[i * kCMax + j] = (float)Lc[i][j];
@@ -875,6 +885,11 @@ void mppi_chain_ctx_destroy(mppi_chain_ctx* c) {
     (void)hipFree(c->d_base);
     (void)hipFree(c->d_chol);
     (void)hipFree(c->d_dyn);
+    for (void* p : c->xopened)
+        if (p) (void)hipIpcCloseMemHandle(p);
+    (void)hipFree(c->d_inbox);
+    (void)hipFree(c->d_xrow);
+    (void)hipFree(c->d_xepoch);
     if (c->h_step) (void)hipHostFree(c->h_step);
     if (c->h_buf) (void)hipHostFree(c->h_buf);
     if (c->h_base) (void)hipHostFree(c->h_base);
@@ -950,6 +965,11 @@ int mppi_chain_rollout(mppi_chain_ctx* c, const float* noise_dev, double* S_dev,
     if (!c || !noise_dev) return fail(MPPI_E_ARG, "null argument");
     if ((flags & MPPI_FLAG_FUSED_UPDATE) && c->cfg.T < 5)
         return fail(MPPI_E_ARG, "device median filter needs T >= 5 (use the host update)");
+    if (flags & MPPI_FLAG_EXCHANGE) {
+        if (c->xd.world < 1) return fail(MPPI_E_ARG, "MPPI_FLAG_EXCHANGE before mppi_chain_exchange_attach");
+        if (partial_dev) return fail(MPPI_E_ARG, "MPPI_FLAG_EXCHANGE merges on device: no partial_out");
+        partial_dev = c->d_xrow;
+    }
     const ChainStep* cur = c->d_step + c->cur;
     ChainStep* nxt = c->d_step + (c->cur ^ 1);
 #define MPPI_L(N)                                                                       \
@@ -960,6 +980,53 @@ int mppi_chain_rollout(mppi_chain_ctx* c, const float* noise_dev, double* S_dev,
     const hipError_t e = hipGetLastError();
     if (e != hipSuccess) return fail(MPPI_E_HIP, std::string("chain_rollout_kernel: ") + hipGetErrorString(e));
     if (flags & MPPI_FLAG_FUSED_UPDATE) c->cur ^= 1;
+    return MPPI_OK;
+}
+
+int mppi_chain_exchange_handle(mppi_chain_ctx* c, int world, void* handle_out) {
+    if (!c || !handle_out || world < 1 || world > kMaxWorld) return fail(MPPI_E_ARG, "bad argument");
+    if (c->d_inbox && c->xworld_alloc != world) return fail(MPPI_E_ARG, "inbox already sized for another world");
+    const int stride = 2 + c->cfg.T * c->n;
+    if (!c->d_inbox) {
+        const size_t bytes = (size_t)2 * world * stride * 16;
+        hipError_t e;
+        if ((e = hipSetDevice(c->device)) != hipSuccess ||
+            (e = hipExtMallocWithFlags(&c->d_inbox, bytes, hipDeviceMallocUncached)) != hipSuccess ||
+            (e = hipMemset(c->d_inbox, 0, bytes)) != hipSuccess ||
+            (e = hipMalloc(&c->d_xrow, stride * sizeof(double))) != hipSuccess ||
+            (e = hipMalloc(&c->d_xepoch, 256)) != hipSuccess || (e = hipMemset(c->d_xepoch, 0, 256)) != hipSuccess ||
+            (e = hipDeviceSynchronize()) != hipSuccess)
+            return fail(MPPI_E_HIP, std::string("exchange inbox: ") + hipGetErrorString(e));
+        c->xworld_alloc = world;
+        c->xd.bytes = (int)bytes;
+    }
+    const hipError_t e = hipIpcGetMemHandle(static_cast<hipIpcMemHandle_t*>(handle_out), c->d_inbox);
+    if (e != hipSuccess) return fail(MPPI_E_HIP, std::string("hipIpcGetMemHandle: ") + hipGetErrorString(e));
+    return MPPI_OK;
+}
+
+int mppi_chain_exchange_attach(mppi_chain_ctx* c, int rank, int world, const void* handles) {
+    if (!c || !handles || world < 1 || rank < 0 || rank >= world) return fail(MPPI_E_ARG, "bad argument");
+    if (!c->d_inbox || c->xworld_alloc != world) return fail(MPPI_E_ARG, "call mppi_chain_exchange_handle(world) first");
+    if (c->xd.world) return fail(MPPI_E_ARG, "already attached");
+    hipError_t e = hipSetDevice(c->device);
+    if (e != hipSuccess) return fail(MPPI_E_HIP, std::string("hipSetDevice: ") + hipGetErrorString(e));
+    const hipIpcMemHandle_t* h = static_cast<const hipIpcMemHandle_t*>(handles);
+    for (int p = 0; p < world; ++p) {
+        if (p == rank) {
+            c->xd.peer[p] = c->d_inbox;
+            continue;
+        }
+        void* ptr = nullptr;
+        if ((e = hipIpcOpenMemHandle(&ptr, h[p], hipIpcMemLazyEnablePeerAccess)) != hipSuccess)
+            return fail(MPPI_E_HIP, std::string("hipIpcOpenMemHandle: ") + hipGetErrorString(e));
+        c->xopened[p] = ptr;
+        c->xd.peer[p] = ptr;
+    }
+    c->xd.row = c->d_xrow;
+    c->xd.epoch = c->d_xepoch;
+    c->xd.rank = rank;
+    c->xd.world = world;
     return MPPI_OK;
 }
 

@@ -755,6 +755,54 @@ __device__ __forceinline__ float2 box_muller(unsigned a, unsigned b) {
 
 }  // namespace mppi
 
+namespace mppi {
+
+// ------------------------------------------------------ node-level exchange
+// Multi-GPU (one process per GPU, one node) without a collective call per step:
+// the launch's final workgroup writes this rank's merged row {rho, eta, N} as
+// tagged granules into slot [parity][rank] of EVERY rank's inbox (IPC-mapped
+// device memory; remote ranks over xGMI, system-scope stores), then polls its
+// own inbox until the world rows of this step carry the tag and merges them in
+// rank order with the same granule merge as inside a launch.  The pattern is
+// RCCL's LL protocol (flagged stores into a peer's buffer); the inbox is
+// uncached device memory, so a poll never reads a stale L2 line.  Tags come
+// from a per-rank exchange epoch advanced once per exchange launch: every rank
+// runs the same launches, so the epochs agree.  Two parity halves: a rank can
+// write step n + 1 while a slower peer still reads step n, never step n + 2
+// (it needs that peer's step n + 1 row first).
+constexpr int kMaxWorld = MPPI_MAX_WORLD;
+struct XDesc {
+    const void* peer[kMaxWorld];   // inbox base of every rank (own rank: local memory)
+    double* row;                   // this rank's merged row, written by the launch's final merge
+    unsigned* epoch;               // this rank's exchange epoch
+    int rank, world, bytes;        // bytes: inbox size (2 x world rows of `stride` granules)
+};
+__device__ __forceinline__ void st_gran_sys(__amdgpu_buffer_rsrc_t r, int idx, double v, unsigned tag) {
+    const unsigned long long b = (unsigned long long)__double_as_longlong(v);
+    const u32x4 x = {(unsigned)b, tag, (unsigned)(b >> 32), tag};
+    __builtin_amdgcn_raw_buffer_store_b128(x, r, idx * 16, 0, kSC1 | 1);   // sc0 sc1: system scope
+}
+
+// Called by the final workgroup after its merge wrote x.row (put_final ends with
+// a barrier, so the row is visible to the whole workgroup).
+template <int NT, int MAXCH, class SM>
+__device__ __forceinline__ void exchange_merge(const XDesc& x, const RowGeo& geo, double inv_lambda, SM& sm,
+                                               double* w_eps_out, unsigned* tmo) {
+    // the previous exchange launch's final store; kernel boundaries order it
+    const unsigned tag = (unsigned)__builtin_amdgcn_readfirstlane((int)*x.epoch) + 1u;
+    const int par = (int)(tag & 1u), stride = geo.stride;
+    for (int idx = threadIdx.x; idx < stride; idx += NT) {
+        const double v = x.row[idx];
+        for (int p = 0; p < x.world; ++p)
+            st_gran_sys(rows_rsrc(x.peer[p], x.bytes), (par * x.world + x.rank) * stride + idx, v, tag);
+    }
+    merge_rows_block<NT, MAXCH, true, true>(rows_rsrc(x.peer[x.rank], x.bytes), par * x.world, x.world, geo,
+                                            inv_lambda, sm, nullptr, 0, nullptr, w_eps_out, tag, tmo);
+    if (threadIdx.x == 0) *x.epoch = tag;
+}
+
+}  // namespace mppi
+
 // Issue fairness between workgroups that share a CU.  The SIMD arbiter serves
 // the oldest ready wave first, so of two co-resident rollout waves the younger
 // one only fills the older one's issue gaps and then finishes alone at the

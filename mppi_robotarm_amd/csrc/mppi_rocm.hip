@@ -158,7 +158,7 @@ __global__ __launch_bounds__(NT) void rollout_kernel(
     const KConst c, const DevStep* __restrict__ st, const float2* __restrict__ noise,
     double* __restrict__ S_out, double* __restrict__ slab, double* __restrict__ gslab,
     unsigned* __restrict__ counters, double* __restrict__ partial_out, double* __restrict__ w_eps_out,
-    DevStep* __restrict__ nxt, unsigned flags, unsigned* __restrict__ epoch, unsigned* __restrict__ tmo,
+    DevStep* __restrict__ nxt, unsigned flags, const XDesc xd, unsigned* __restrict__ epoch, unsigned* __restrict__ tmo,
     unsigned long long* __restrict__ dbg) {
     __shared__ float4 s_win[kSlots];
     __shared__ float s_redf[NT / 64];
@@ -405,6 +405,7 @@ __global__ __launch_bounds__(NT) void rollout_kernel(
     }
     STAMP(11, NOW());
     STAMP(6, (unsigned long long)sm.nrel);
+    if (flags & MPPI_FLAG_EXCHANGE) exchange_merge<NT, 1>(xd, geo, c.inv_lambda, sm, w_eps_out, tmo);
     if (flags & MPPI_FLAG_FUSED_UPDATE) nominal_update_block<NT>(st, nxt, c, sm, u_cur);
     STAMP(7, NOW());
 }
@@ -500,6 +501,13 @@ struct mppi_ctx {
     float2* h_base = nullptr;   // pinned
     double sig_inv[4];
     unsigned long long* d_dbg = nullptr;  // diagnostic stamp buffer (MPPI_STAMPS builds)
+    // node-level exchange (mppi_exchange_*): inbox, this rank's row, epoch, peer mappings
+    XDesc xd{};
+    void* d_inbox = nullptr;
+    double* d_xrow = nullptr;
+    unsigned* d_xepoch = nullptr;
+    int xworld_alloc = 0;
+    void* xopened[kMaxWorld] = {};
 };
 
 namespace mppi_host {
@@ -692,6 +700,11 @@ void mppi_ctx_destroy(mppi_ctx* c) {
     (void)hipFree(c->d_gslab);
     (void)hipFree(c->d_weps);
     (void)hipFree(c->d_base);
+    for (void* p : c->xopened)
+        if (p) (void)hipIpcCloseMemHandle(p);
+    (void)hipFree(c->d_inbox);
+    (void)hipFree(c->d_xrow);
+    (void)hipFree(c->d_xepoch);
     if (c->h_step) (void)hipHostFree(c->h_step);
     if (c->h_buf) (void)hipHostFree(c->h_buf);
     if (c->h_base) (void)hipHostFree(c->h_base);
@@ -764,12 +777,17 @@ int mppi_rollout(mppi_ctx* c, const float* noise_dev, double* S_dev, double* par
     if (!c || !noise_dev) return fail(MPPI_E_ARG, "null argument");
     if ((flags & MPPI_FLAG_FUSED_UPDATE) && c->cfg.T < 5)
         return fail(MPPI_E_ARG, "device median filter needs T >= 5 (use the host update)");
+    if (flags & MPPI_FLAG_EXCHANGE) {
+        if (c->xd.world < 1) return fail(MPPI_E_ARG, "MPPI_FLAG_EXCHANGE before mppi_exchange_attach");
+        if (partial_dev) return fail(MPPI_E_ARG, "MPPI_FLAG_EXCHANGE merges on device: no partial_out");
+        partial_dev = c->d_xrow;
+    }
     const DevStep* cur = c->d_step + c->cur;
     DevStep* nxt = c->d_step + (c->cur ^ 1);
     const float2* nz = reinterpret_cast<const float2*>(noise_dev);
 #define MPPI_LAUNCH2(L, NTH, P)                                                                                \
     hipLaunchKernelGGL((rollout_kernel<L, NTH, P>), dim3(c->nblocks), dim3(NTH), 0, c->stream, c->kc, cur, nz, \
-                       S_dev, c->d_slab, c->d_gslab, c->d_counter, partial_dev, c->d_weps, nxt, flags, c->d_epoch, \
+                       S_dev, c->d_slab, c->d_gslab, c->d_counter, partial_dev, c->d_weps, nxt, flags, c->xd, c->d_epoch, \
                        c->d_tmo, c->d_dbg)
 #define MPPI_LAUNCH(L, NTH)               \
     do {                                  \
@@ -790,6 +808,49 @@ int mppi_rollout(mppi_ctx* c, const float* noise_dev, double* S_dev, double* par
     const int rc = launch_check("rollout_kernel");
     if (rc == MPPI_OK && (flags & MPPI_FLAG_FUSED_UPDATE)) c->cur ^= 1;
     return rc;
+}
+
+int mppi_exchange_handle(mppi_ctx* c, int world, void* handle_out) {
+    if (!c || !handle_out || world < 1 || world > kMaxWorld) return fail(MPPI_E_ARG, "bad argument");
+    if (c->d_inbox && c->xworld_alloc != world) return fail(MPPI_E_ARG, "inbox already sized for another world");
+    const int stride = 2 + 2 * c->cfg.T;
+    if (!c->d_inbox) {
+        const size_t bytes = (size_t)2 * world * stride * 16;
+        HIP_TRY(hipSetDevice(c->device));
+        HIP_TRY(hipExtMallocWithFlags(&c->d_inbox, bytes, hipDeviceMallocUncached));
+        HIP_TRY(hipMemset(c->d_inbox, 0, bytes));
+        HIP_TRY(hipMalloc(&c->d_xrow, stride * sizeof(double)));
+        HIP_TRY(hipMalloc(&c->d_xepoch, 256));
+        HIP_TRY(hipMemset(c->d_xepoch, 0, 256));
+        HIP_TRY(hipDeviceSynchronize());
+        c->xworld_alloc = world;
+        c->xd.bytes = (int)bytes;
+    }
+    HIP_TRY(hipIpcGetMemHandle(static_cast<hipIpcMemHandle_t*>(handle_out), c->d_inbox));
+    return MPPI_OK;
+}
+
+int mppi_exchange_attach(mppi_ctx* c, int rank, int world, const void* handles) {
+    if (!c || !handles || world < 1 || rank < 0 || rank >= world) return fail(MPPI_E_ARG, "bad argument");
+    if (!c->d_inbox || c->xworld_alloc != world) return fail(MPPI_E_ARG, "call mppi_exchange_handle(world) first");
+    if (c->xd.world) return fail(MPPI_E_ARG, "already attached");
+    HIP_TRY(hipSetDevice(c->device));
+    const hipIpcMemHandle_t* h = static_cast<const hipIpcMemHandle_t*>(handles);
+    for (int p = 0; p < world; ++p) {
+        if (p == rank) {
+            c->xd.peer[p] = c->d_inbox;
+            continue;
+        }
+        void* ptr = nullptr;
+        HIP_TRY(hipIpcOpenMemHandle(&ptr, h[p], hipIpcMemLazyEnablePeerAccess));
+        c->xopened[p] = ptr;
+        c->xd.peer[p] = ptr;
+    }
+    c->xd.row = c->d_xrow;
+    c->xd.epoch = c->d_xepoch;
+    c->xd.rank = rank;
+    c->xd.world = world;
+    return MPPI_OK;
 }
 
 int mppi_merge_partials(mppi_ctx* c, const double* partials_dev, int n, unsigned flags) {

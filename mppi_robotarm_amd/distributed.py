@@ -46,3 +46,52 @@ def exchange_partials(partial: torch.Tensor, gathered: torch.Tensor, group=None)
         return gathered
     dist.all_gather_into_tensor(gathered, partial, group=group)
     return gathered
+
+
+def attach_exchange(engine, group=None) -> bool:
+    """Set up the in-launch exchange (include/mppi_rocm.h mppi_exchange_*): every
+    rank exports its inbox's IPC handle, the handles are all-gathered over the
+    group once, and every rank maps its peers' inboxes.  Afterwards
+    ``engine.rollout(noise, exchange=True, fused_update=True)`` finishes a whole
+    multi-GPU control step in one launch per rank.
+
+    Collective-safe: every rank joins every collective whatever fails locally,
+    and all ranks return the same answer (False: use exchange_partials)."""
+    world, rank = dist.get_world_size(group), dist.get_rank(group)
+    try:
+        h = engine.exchange_handle(world)
+    except Exception:  # noqa: BLE001 - reported to every rank below
+        h = None
+    handles = [None] * world
+    dist.all_gather_object(handles, h, group=group)
+    ok = all(x is not None for x in handles)
+    if ok:
+        try:
+            engine.exchange_attach(rank, world, handles)
+        except Exception:  # noqa: BLE001
+            ok = False
+    return _all_ranks(ok, group)
+
+
+def check_exchange(engine, noise, partial, gathered, group=None) -> bool:
+    """One step both ways from the same state (no update): the in-launch exchange
+    must reproduce all-gather + device merge (1e-9) without a hand-off timeout.
+    Every rank gets the same verdict."""
+    import numpy as np
+    engine.rollout(noise, partial_out=partial)
+    exchange_partials(partial, gathered, group)
+    engine.merge(gathered, dist.get_world_size(group))
+    w_ref = engine.weighted_noise()
+    try:
+        engine.rollout(noise, exchange=True)
+        engine.synchronize()          # raises on a hand-off timeout
+        ok = bool(np.allclose(engine.weighted_noise(), w_ref, rtol=1e-9, atol=1e-12))
+    except Exception:  # noqa: BLE001
+        ok = False
+    return _all_ranks(ok, group)
+
+
+def _all_ranks(ok: bool, group=None) -> bool:
+    flags = [None] * dist.get_world_size(group)
+    dist.all_gather_object(flags, bool(ok), group=group)
+    return all(flags)

@@ -119,8 +119,24 @@ class RolloutEngine:
                 "mppi_set_step_inputs")
         self._keep = (x0, win, uu)  # keep host arrays alive until the async copy ran
 
+    def exchange_handle(self, world: int) -> bytes:
+        """Allocate this rank's exchange inbox for `world` ranks; its IPC handle (64 B)."""
+        buf = C.create_string_buffer(N.MPPI_IPC_HANDLE_BYTES)
+        N.check(self._lib.mppi_exchange_handle(self._ctx, int(world), buf), "mppi_exchange_handle")
+        return buf.raw
+
+    def exchange_attach(self, rank: int, world: int, handles) -> None:
+        """Map every rank's inbox (handles in rank order); then rollout(..., exchange=True)."""
+        blob = b"".join(bytes(h) for h in handles)
+        if len(blob) != world * N.MPPI_IPC_HANDLE_BYTES:
+            raise ValueError("one 64-byte handle per rank")
+        N.check(self._lib.mppi_exchange_attach(self._ctx, int(rank), int(world), C.create_string_buffer(blob, len(blob))),
+                "mppi_exchange_attach")
+        self.exchange_world = int(world)
+
     def rollout(self, noise: torch.Tensor, S_out: torch.Tensor | None = None,
-                partial_out: torch.Tensor | None = None, fused_update: bool = False) -> None:
+                partial_out: torch.Tensor | None = None, fused_update: bool = False, exchange: bool = False) -> None:
+        """control.py:81-118 for this shard; `exchange`: also exchange and merge the ranks' rows in the launch."""
         self._sync_stream()
         self._check_noise(noise)
         if S_out is not None:
@@ -130,7 +146,8 @@ class RolloutEngine:
         N.check(self._lib.mppi_rollout(self._ctx, C.c_void_p(noise.data_ptr()),
                                        C.c_void_p(S_out.data_ptr()) if S_out is not None else None,
                                        C.c_void_p(partial_out.data_ptr()) if partial_out is not None else None,
-                                       N.MPPI_FLAG_FUSED_UPDATE if fused_update else 0),
+                                       (N.MPPI_FLAG_FUSED_UPDATE if fused_update else 0)
+                                       | (N.MPPI_FLAG_EXCHANGE if exchange else 0)),
                 "mppi_rollout")
 
     def merge(self, partials: torch.Tensor, n: int, fused_update: bool = False) -> None:

@@ -167,3 +167,48 @@ def test_chain_sharded_exchange_matches_unsharded(tmp_path, K, T):
     w, ref = coracle.chain_weighted_noise(S, eps, CHAIN_LAM)
     assert 1.0 / np.sum(w ** 2) > 3            # several samples carry weight
     np.testing.assert_allclose(r0, ref, rtol=1e-10, atol=1e-12)
+
+
+class _FakeEngine:
+    """Stands in for an engine in the exchange set-up (no GPU): rank `bad` fails at `where`."""
+
+    def __init__(self, rank, bad, where):
+        self.rank, self.bad, self.where, self.attached = rank, bad, where, None
+
+    def exchange_handle(self, world):
+        if self.rank == self.bad and self.where == "handle":
+            raise RuntimeError("no inbox")
+        return bytes([self.rank]) * 64
+
+    def exchange_attach(self, rank, world, handles):
+        if self.rank == self.bad and self.where == "attach":
+            raise RuntimeError("cannot map")
+        self.attached = [h[0] for h in handles]
+
+
+def _attach_worker(rank, world, port, bad, where, out_path):
+    import sys
+    sys.path.insert(0, ROOT)
+    from mppi_robotarm_amd.distributed import attach_exchange
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        eng = _FakeEngine(rank, bad, where)
+        ok = attach_exchange(eng)
+        np.save(f"{out_path}.{rank}.npy", np.array([int(ok)] + (eng.attached or [-1] * world)))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("bad,where", [(-1, ""), (1, "handle"), (0, "attach")])
+def test_attach_exchange_is_collective_safe(tmp_path, bad, where):
+    """A rank that cannot export or map inboxes makes EVERY rank fall back (same
+    verdict everywhere, no rank left waiting in a collective)."""
+    world = 2
+    out = str(tmp_path / "att")
+    mp.start_processes(_attach_worker, args=(world, _free_port(), bad, where, out), nprocs=world, join=True,
+                       start_method="spawn")
+    r = [np.load(f"{out}.{k}.npy") for k in range(world)]
+    assert r[0][0] == r[1][0] == (1 if bad < 0 else 0)
+    if bad < 0:
+        assert r[0][1:].tolist() == r[1][1:].tolist() == [0, 1]   # handles in rank order
