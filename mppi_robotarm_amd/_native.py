@@ -118,6 +118,8 @@ def open_library(path: str):
         "mppi_chain_debug_set_buffer": ([vp, vp], C.c_int),
     }
     for name, (args, res) in sig.items():
+        if not hasattr(L, name):   # an older diagnostic build (tools/ab.py); load() checks the product's exports
+            continue
         fn = getattr(L, name)
         fn.argtypes = args
         fn.restype = res
@@ -128,7 +130,11 @@ def load():
     """Load libmppi_rocm.so (raises OSError if it is missing — no fallback)."""
     global _lib
     if _lib is None:
-        _lib = open_library(LIB_PATH)
+        L = open_library(LIB_PATH)
+        missing = [n for n in EXPORTS if not hasattr(L, n)]
+        if missing:
+            raise OSError(f"{LIB_PATH} is stale (missing {', '.join(missing)}): rebuild it")
+        _lib = L
     return _lib
 
 
