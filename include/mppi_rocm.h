@@ -157,6 +157,14 @@ int mppi_sync(mppi_ctx *ctx);
  * timeline (16 uint64 per workgroup) to dbg_dev; product builds ignore it. */
 int mppi_debug_set_buffer(mppi_ctx *ctx, void *dbg_dev);
 
+/* Tests: the nearest window slot of n end-effector points pts_dev[n][2] (fp32
+ * device), once through the window-search candidate table and once by the full
+ * 30-slot scan, into out_dev[n][2] (int32 device).  The two must agree bit for
+ * bit (control.py:200-232 as the device evaluates it).  The table is opt-in:
+ * MPPI_SEARCH=table in the environment at mppi_ctx_create (lanes_per_sample 1);
+ * MPPI_E_ARG otherwise. */
+int mppi_debug_search(mppi_ctx *ctx, const float *pts_dev, int n, int *out_dev);
+
 /* ------------------------------------------------------------------------
  * n-link planar chain (BASELINE config 5: "7-DoF arm dynamics (extended
  * sys_params.py), K=131072 T=128, xydq_circle.txt reference").  The reference

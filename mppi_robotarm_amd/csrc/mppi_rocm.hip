@@ -51,7 +51,7 @@ struct alignas(16) DevStep {
     float4 win[kSlots];   // rx, ry, rdq1, rdq2 of window slot j (lookup after argmin)
     float4 key[kSlots];   // rx', ry', c' = rx'^2 + ry'^2 (centred), 0; pads c' = 1e30
     float4 x0;            // q1, q2, dq1, dq2
-    float4 ctr;           // window centre (cx, cy), W, unused
+    float4 ctr;           // window centre (cx, cy), W, sscale of the candidate table (mppi_device.h)
     float4 ua[kMaxT];     // u0, u1, a0, a1 (a = (gamma u_t)^T Sigma^-1), fp32
     double u[kMaxT][2];   // nominal control sequence, fp64 (device closed loop)
 };
@@ -144,6 +144,14 @@ __device__ __forceinline__ float2 noise_ld(const float2* p) { return *p; }
 #endif
 
 constexpr int kPF = 4;  // noise rows in flight per lane
+// Blocked horizon loop for the full scan too (MPPI_BLOCKED builds): the
+// dynamics of kPF steps, then their searches, then one batch of LDS lookups.
+// Measured 0.9 % slower than step by step (tools/ab.py), so off by default.
+#ifdef MPPI_BLOCKED
+constexpr bool kBlockSteps = true;
+#else
+constexpr bool kBlockSteps = false;
+#endif
 
 // POLL: the partial rows travel as tagged granules (see st_gran) to consumer
 // workgroups that poll for them — the highest-numbered workgroup of each group
@@ -153,14 +161,21 @@ constexpr int kPF = 4;  // noise rows in flight per lane
 // when the grid is at most one workgroup per CU); correctness does not depend
 // on placement or order, every value is tag-checked.  Otherwise (!POLL) the
 // last workgroup to arrive on a counter merges (arrive_last).
-template <int LPS, int NT, bool POLL>
+// TAB (LPS = 1): the window search goes through the candidate table (TabSearch,
+// built per window by search_table_kernel), resolving each block of kPF steps
+// after their dynamics; results are bit-identical to the full scan.
+template <int LPS, int NT, bool POLL, bool TAB>
 __global__ __launch_bounds__(NT) void rollout_kernel(
-    const KConst c, const DevStep* __restrict__ st, const float2* __restrict__ noise,
+    const KConst c, const DevStep* __restrict__ st, const uint4* __restrict__ tab, const float2* __restrict__ noise,
     double* __restrict__ S_out, double* __restrict__ slab, double* __restrict__ gslab,
     unsigned* __restrict__ counters, double* __restrict__ partial_out, double* __restrict__ w_eps_out,
     DevStep* __restrict__ nxt, unsigned flags, const XDesc xd, unsigned* __restrict__ epoch, unsigned* __restrict__ tmo,
     unsigned long long* __restrict__ dbg) {
+    static_assert(!TAB || LPS == 1, "table search is per lane");
     __shared__ float4 s_win[kSlots];
+    __shared__ __attribute__((aligned(16))) unsigned char s_tab[TAB ? kTabBytes : 16];
+    __shared__ float4 s_rows[TAB ? kKeyRows : 1];
+    __shared__ KeyPair s_kp[TAB ? kKeyPairs : 1];
     __shared__ float s_redf[NT / 64];
     __shared__ int s_cnt[NT / 64];
     __shared__ int s_k[NT];
@@ -186,7 +201,17 @@ __global__ __launch_bounds__(NT) void rollout_kernel(
     const double u_cur = ((flags & MPPI_FLAG_FUSED_UPDATE) && tid < 2 * T) ? st->u[tid >> 1][tid & 1] : 0.0;
     if (tid < kSlots) s_win[tid] = st->win[tid];
     Search<LPS> sr;
-    sr.load(st->key, st->ctr, tid & (LPS - 1));
+    TabSearch ts;
+    if constexpr (TAB) {
+        for (int i = tid; i < kTabVec; i += NT) reinterpret_cast<uint4*>(s_tab)[i] = tab[i];
+        if (tid < kKeyRows) s_rows[tid] = tid < kSlots ? st->key[tid] : make_float4(0.f, 0.f, kPadKey, 0.f);
+        SearchLDS<false>::fill(s_kp, st->key, tid);
+        const float4 ctr = st->ctr;
+        ts = TabSearch{s_tab, s_rows, s_kp, ctr.x, ctr.y, ctr.w};
+        sr.sub = 0;
+    } else {
+        sr.load(st->key, st->ctr, tid & (LPS - 1));
+    }
     const float4 x0 = st->x0;
     ArmState x;
     x.q1 = x0.x;
@@ -235,23 +260,81 @@ __global__ __launch_bounds__(NT) void rollout_kernel(
         const float g = fmaf(ua.z, v1, ua.w * v2);  // (gamma u^T Sigma^-1) v, control.py:106
         S4 += weighted_sq(ex, ey, e1, e2, c.sw) + g;
     };
+    // TAB: the dynamics of steps t..t+n-1 first, then their n window searches
+    // together (independent of each other: the lookups' LDS latencies overlap),
+    // then the costs in step order (the same fp32 sums as step()).
+    auto block = [&](int t, auto n_c) {
+        constexpr int n = decltype(n_c)::value;
+        float px[n], py[n], d1[n], d2[n], gc[n];
+        unroll_seq([&](auto s_c) {
+            constexpr int s = decltype(s_c)::value;
+            const float2 e = ring[s];
+            const float4 ua = uring[s];
+            const int tl = t + s + kPF < T ? t + s + kPF : T - 1;
+            ring[s] = noise_ld(np + (size_t)tl * K);
+            PIN_LOADS();
+            const float v1 = fmaf(exf, ua.x, e.x);
+            const float v2 = fmaf(exf, ua.y, e.y);
+            dyn_step(x, v1, v2, c);
+            px[s] = fmaf(c.fk1, x.c1, c.fk2 * x.c12);
+            py[s] = fmaf(c.fk1, x.s1, c.fk2 * x.s12);
+            d1[s] = x.dq1;
+            d2[s] = x.dq2;
+            gc[s] = fmaf(ua.z, v1, ua.w * v2);
+        }, std::make_integer_sequence<int, n>{});
+        unsigned jn[n];
+        if constexpr (TAB) {
+            ts.nearest<n>(px, py, jn);
+        } else {
+#pragma unroll
+            for (int s = 0; s < n; ++s) jn[s] = sr.nearest(px[s], py[s]);
+        }
+#pragma unroll
+        for (int s = 0; s < n; ++s) {
+            const float4 r = s_win[jn[s]];
+            ex = px[s] - r.x;
+            ey = py[s] - r.y;
+            e1 = d1[s] - r.z;
+            e2 = d2[s] - r.w;
+            S4 += weighted_sq(ex, ey, e1, e2, c.sw) + gc[s];
+        }
+        // scalar prefetches after the block's LDS lookups (see step())
+        PIN_LOADS();
+        unroll_seq([&](auto s_c) {
+            constexpr int s = decltype(s_c)::value;
+            uring[s] = const_ld4(cua + 4 * (t + s + kPF < T ? t + s + kPF : T - 1));
+        }, std::make_integer_sequence<int, n>{});
+        PIN_LOADS();
+    };
     using I0 = std::integral_constant<int, 0>;
     using I1 = std::integral_constant<int, 1>;
     using I2 = std::integral_constant<int, 2>;
     using I3 = std::integral_constant<int, 3>;
     static_assert(kPF == 4, "unrolled for a 4-deep ring");
     int t = 0;
-    for (; t + kPF <= T; t += kPF) {
-        step(t, I0{});
-        step(t + 1, I1{});
-        step(t + 2, I2{});
-        step(t + 3, I3{});
-        S += (double)S4;
-        S4 = 0.f;
+    if constexpr (TAB || kBlockSteps) {
+        for (; t + kPF <= T; t += kPF) {
+            block(t, std::integral_constant<int, kPF>{});
+            S += (double)S4;
+            S4 = 0.f;
+        }
+        const int rem = T - t;  // slots 0..rem-1, t % kPF == 0
+        if (rem == 1) block(t, I1{});
+        else if (rem == 2) block(t, I2{});
+        else if (rem == 3) block(t, I3{});
+    } else {
+        for (; t + kPF <= T; t += kPF) {
+            step(t, I0{});
+            step(t + 1, I1{});
+            step(t + 2, I2{});
+            step(t + 3, I3{});
+            S += (double)S4;
+            S4 = 0.f;
+        }
+        if (t < T) step(t, I0{});          // remainder: t % kPF == 0, 1, 2 in order
+        if (t + 1 < T) step(t + 1, I1{});
+        if (t + 2 < T) step(t + 2, I2{});
     }
-    if (t < T) step(t, I0{});          // remainder: t % kPF == 0, 1, 2 in order
-    if (t + 1 < T) step(t + 1, I1{});
-    if (t + 2 < T) step(t + 2, I2{});
     S += (double)S4;
     S += (double)weighted_sq(ex, ey, e1, e2, c.tw);  // terminal cost, control.py:109
 
@@ -454,6 +537,38 @@ __global__ __launch_bounds__(kThreads) void traj_kernel(const KConst c, const De
     }
 }
 
+// Candidate table of the window search (mppi_device.h, build_tab_cell): one
+// thread per (cell, slot), from the step block's fp32 keys as the rollouts read them.
+__global__ __launch_bounds__(256) void search_table_kernel(const DevStep* __restrict__ st, unsigned char* __restrict__ tab) {
+    const float4 ctr = st->ctr;
+    build_tab_cell(st->key, (int)ctr.z, ctr.w, tab);
+}
+
+// Diagnostics / tests: the table search and the full scan of the same points
+// (pts[n] = (px, py)); out[2i] = table result, out[2i + 1] = full scan.
+__global__ __launch_bounds__(256) void search_check_kernel(const DevStep* __restrict__ st, const uint4* __restrict__ tab,
+                                                           const float2* __restrict__ pts, int n, int* __restrict__ out) {
+    __shared__ __attribute__((aligned(16))) unsigned char s_tab[kTabBytes];
+    __shared__ float4 s_rows[kKeyRows];
+    __shared__ KeyPair s_kp[kKeyPairs];
+    const int tid = threadIdx.x;
+    for (int i = tid; i < kTabVec; i += 256) reinterpret_cast<uint4*>(s_tab)[i] = tab[i];
+    if (tid < kKeyRows) s_rows[tid] = tid < kSlots ? st->key[tid] : make_float4(0.f, 0.f, kPadKey, 0.f);
+    SearchLDS<false>::fill(s_kp, st->key, tid);
+    __syncthreads();
+    const float4 ctr = st->ctr;
+    const TabSearch ts{s_tab, s_rows, s_kp, ctr.x, ctr.y, ctr.w};
+    const int i = blockIdx.x * 256 + tid;
+    const float2 p = pts[min(i, n - 1)];
+    unsigned j;
+    ts.nearest<1>(&p.x, &p.y, &j);
+    const unsigned jf = ts.scan_all(p.x - ctr.x, p.y - ctr.y);
+    if (i < n) {
+        out[2 * i] = (int)j;
+        out[2 * i + 1] = (int)jf;
+    }
+}
+
 // Philox4x32-10 + Box-Muller (mppi_device.h); eps = L z, L = chol(Sigma).
 __global__ __launch_bounds__(kThreads) void philox_noise_kernel(int K_local, int T, long long k_offset,
                                                                 unsigned long long seed,
@@ -486,6 +601,8 @@ struct mppi_ctx {
     KConst kc;
     DevStep* d_step = nullptr;  // [2] ping-pong
     int cur = 0;
+    uint4* d_tab = nullptr;     // window-search candidate table (built per window)
+    bool use_tab = false;       // LPS = 1 and MPPI_SEARCH=table
     DevStep* h_step = nullptr;  // pinned staging
     hipEvent_t staged = nullptr;
     double* d_slab = nullptr;
@@ -539,7 +656,7 @@ int launch_check(const char* what) {
 
 template <int L, int N>
 int occupancy(int* per_cu) {
-    return (int)hipOccupancyMaxActiveBlocksPerMultiprocessor(per_cu, (const void*)rollout_kernel<L, N, true>, N, 0);
+    return (int)hipOccupancyMaxActiveBlocksPerMultiprocessor(per_cu, (const void*)rollout_kernel<L, N, true, L == 1>, N, 0);
 }
 
 int check_timeout(mppi_ctx* c) {
@@ -592,6 +709,11 @@ int mppi_ctx_create(const mppi_config* cfg, int device, void* stream, mppi_ctx**
         return fail(MPPI_E_ARG, "lanes_per_sample must be 0, 1, 2 or 4");
     }
     c->lps = lps;
+    // window search: the full 30-slot scan (default), or MPPI_SEARCH=table for the
+    // candidate table (LPS = 1; bit-identical; faster only while the samples stay
+    // away from the window — DESIGN §3, "Tried and measured")
+    const char* sv = getenv("MPPI_SEARCH");
+    c->use_tab = lps == 1 && sv && !strcmp(sv, "table");
     // 512-thread workgroups when the grid fills every CU with one of them (8 waves:
     // two per SIMD); 256 otherwise.  MPPI_BLOCK=256|512 overrides (diagnostics).
     const long long lanes = (long long)cfg->K_local * lps;
@@ -665,6 +787,8 @@ int mppi_ctx_create(const mppi_config* cfg, int device, void* stream, mppi_ctx**
     const size_t gslab = (size_t)ngroups * (2 + 2 * cfg->T) * val;
     const size_t ctr_bytes = ((size_t)(ngroups + 2) * sizeof(unsigned) + 255) & ~(size_t)255;
     if ((e = hipMalloc(&c->d_step, 2 * sizeof(DevStep))) != hipSuccess ||
+        (e = hipMalloc(&c->d_tab, kTabBytes)) != hipSuccess ||
+        (e = hipMemset(c->d_tab, 0xFF, kTabBytes)) != hipSuccess ||
         (e = hipMalloc(&c->d_slab, slab)) != hipSuccess ||
         (e = hipMalloc(&c->d_gslab, gslab)) != hipSuccess ||
         (e = hipMalloc(&c->d_counter, ctr_bytes)) != hipSuccess ||
@@ -695,6 +819,7 @@ void mppi_ctx_destroy(mppi_ctx* c) {
     if (c->stream) (void)hipStreamSynchronize(c->stream);
     (void)hipDeviceSynchronize();
     (void)hipFree(c->d_step);
+    (void)hipFree(c->d_tab);
     (void)hipFree(c->d_slab);
     (void)hipFree(c->d_counter);
     (void)hipFree(c->d_gslab);
@@ -751,7 +876,11 @@ int mppi_set_step_inputs(mppi_ctx* c, const double* x0, const double* window, in
         }
     }
     h->x0 = make_float4((float)x0[0], (float)x0[1], (float)x0[2], (float)x0[3]);
-    h->ctr = make_float4((float)cx, (float)cy, (float)W, 0.f);
+    // candidate table scale: sigma bins over [0, 2 / R_w), R_w = max |r'_j| of the fp32 keys
+    double R2 = 0.0;
+    for (int j = 0; j < W; ++j) R2 = fmax(R2, (double)h->key[j].z);
+    const float sscale = R2 > 0.0 && isfinite(R2) ? (float)(kTabSig * 0.5 * sqrt(R2)) : 0.f;
+    h->ctr = make_float4((float)cx, (float)cy, (float)W, sscale);
     size_t bytes = offsetof(DevStep, ua);
     if (u) {
         const KConst& k = c->kc;
@@ -770,6 +899,12 @@ int mppi_set_step_inputs(mppi_ctx* c, const double* x0, const double* window, in
     HIP_TRY(hipMemcpyAsync(c->d_step + (c->cur ^ 1), h, offsetof(DevStep, ua), hipMemcpyHostToDevice, c->stream));
     HIP_TRY(hipMemcpyAsync(c->d_step + c->cur, h, bytes, hipMemcpyHostToDevice, c->stream));
     HIP_TRY(hipEventRecord(c->staged, c->stream));
+    if (c->use_tab) {
+        // one thread per (cell, slot); stream-ordered after the copies above
+        hipLaunchKernelGGL(search_table_kernel, dim3(kTabBytes * 32 / 256), dim3(256), 0, c->stream, c->d_step + c->cur,
+                           reinterpret_cast<unsigned char*>(c->d_tab));
+        return launch_check("search_table_kernel");
+    }
     return MPPI_OK;
 }
 
@@ -785,26 +920,38 @@ int mppi_rollout(mppi_ctx* c, const float* noise_dev, double* S_dev, double* par
     const DevStep* cur = c->d_step + c->cur;
     DevStep* nxt = c->d_step + (c->cur ^ 1);
     const float2* nz = reinterpret_cast<const float2*>(noise_dev);
-#define MPPI_LAUNCH2(L, NTH, P)                                                                                \
-    hipLaunchKernelGGL((rollout_kernel<L, NTH, P>), dim3(c->nblocks), dim3(NTH), 0, c->stream, c->kc, cur, nz, \
+#define MPPI_LAUNCH3(L, NTH, P, TB)                                                                             \
+    hipLaunchKernelGGL((rollout_kernel<L, NTH, P, TB>), dim3(c->nblocks), dim3(NTH), 0, c->stream, c->kc, cur, c->d_tab, nz, \
                        S_dev, c->d_slab, c->d_gslab, c->d_counter, partial_dev, c->d_weps, nxt, flags, c->xd, c->d_epoch, \
                        c->d_tmo, c->d_dbg)
+#define MPPI_LAUNCH2(L, NTH, P)                  \
+    do {                                        \
+        if (c->use_tab) MPPI_LAUNCH3(L, NTH, P, true); \
+        else MPPI_LAUNCH3(L, NTH, P, false);    \
+    } while (0)
 #define MPPI_LAUNCH(L, NTH)               \
     do {                                  \
         if (c->poll) MPPI_LAUNCH2(L, NTH, true);  \
         else MPPI_LAUNCH2(L, NTH, false); \
     } while (0)
+#define MPPI_LAUNCH_NT(L, NTH, P)         \
+    do {                                  \
+        if (P) MPPI_LAUNCH3(L, NTH, true, false);  \
+        else MPPI_LAUNCH3(L, NTH, false, false);   \
+    } while (0)
     if (c->nt == 512) {
         if (c->lps == 1) MPPI_LAUNCH(1, 512);
-        else if (c->lps == 2) MPPI_LAUNCH(2, 512);
-        else MPPI_LAUNCH(4, 512);
+        else if (c->lps == 2) MPPI_LAUNCH_NT(2, 512, c->poll);
+        else MPPI_LAUNCH_NT(4, 512, c->poll);
     } else {
         if (c->lps == 1) MPPI_LAUNCH(1, 256);
-        else if (c->lps == 2) MPPI_LAUNCH(2, 256);
-        else MPPI_LAUNCH(4, 256);
+        else if (c->lps == 2) MPPI_LAUNCH_NT(2, 256, c->poll);
+        else MPPI_LAUNCH_NT(4, 256, c->poll);
     }
+#undef MPPI_LAUNCH_NT
 #undef MPPI_LAUNCH
 #undef MPPI_LAUNCH2
+#undef MPPI_LAUNCH3
     const int rc = launch_check("rollout_kernel");
     if (rc == MPPI_OK && (flags & MPPI_FLAG_FUSED_UPDATE)) c->cur ^= 1;
     return rc;
@@ -933,6 +1080,14 @@ int mppi_debug_set_buffer(mppi_ctx* c, void* dbg_dev) {
     if (!c) return fail(MPPI_E_ARG, "null context");
     c->d_dbg = (unsigned long long*)dbg_dev;
     return MPPI_OK;
+}
+
+int mppi_debug_search(mppi_ctx* c, const float* pts_dev, int n, int* out_dev) {
+    if (!c || !pts_dev || !out_dev || n < 1) return fail(MPPI_E_ARG, "bad argument");
+    if (!c->use_tab) return fail(MPPI_E_ARG, "context does not use the candidate table (MPPI_SEARCH=table, LPS 1)");
+    hipLaunchKernelGGL(search_check_kernel, dim3((n + 255) / 256), dim3(256), 0, c->stream, c->d_step + c->cur, c->d_tab,
+                       reinterpret_cast<const float2*>(pts_dev), n, out_dev);
+    return launch_check("search_check_kernel");
 }
 
 int mppi_sync(mppi_ctx* c) {

@@ -196,6 +196,17 @@ class RolloutEngine:
                                             C.c_void_p(out.data_ptr())), "mppi_noise_philox")
         return out
 
+    def search_check(self, points) -> np.ndarray:
+        """Tests: nearest window slot of end-effector points (n, 2) through the
+        candidate table and by the full scan -> (n, 2) int32 (must agree)."""
+        self._sync_stream()
+        pts = torch.as_tensor(np.ascontiguousarray(points, dtype=np.float32).reshape(-1, 2), device=self.device)
+        out = torch.empty((pts.shape[0], 2), dtype=torch.int32, device=self.device)
+        N.check(self._lib.mppi_debug_search(self._ctx, C.c_void_p(pts.data_ptr()), int(pts.shape[0]),
+                                            C.c_void_p(out.data_ptr())), "mppi_debug_search")
+        self.synchronize()
+        return out.cpu().numpy()
+
     def synchronize(self) -> None:
         N.check(self._lib.mppi_sync(self._ctx), "mppi_sync")
 

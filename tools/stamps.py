@@ -37,6 +37,9 @@ else:
     eng.set_step_inputs(X0_RUNPY, path[:30], np.array([[10.0, -2.0]] * T))
     set_dbg = eng._lib.mppi_debug_set_buffer
 noise = [eng.philox_noise(1234, i) for i in range(4)]
+for i in range(int(os.environ.get("WARM", "0"))):   # converge the device loop first (bench.py's regime)
+    eng.rollout(noise[i % 4], fused_update=True)
+torch.cuda.synchronize()
 dbg = torch.zeros(eng.blocks * 16, dtype=torch.int64, device="cuda")
 N.check(set_dbg(eng._ctx, N.C.c_void_p(dbg.data_ptr())), "dbg")
 print(f"K={K} T={T} lps={eng.lanes_per_sample} blocks={eng.blocks} lambda={lam} lib={os.path.basename(lib)}")
