@@ -486,6 +486,11 @@ __global__ __launch_bounds__(kCT) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
         if constexpr (POLL) st_gran(slab_r, idx, v, tag);
         else st_wt(slab_r, idx, v);
     };
+    // rho_b and eta_b leave first (see rollout_kernel in mppi_rocm.hip)
+    if (tid == 0) {
+        publish(blockIdx.x * stride, rho_b);
+        publish(blockIdx.x * stride + 1, eta_b);
+    }
     nl = __builtin_amdgcn_readfirstlane(nl);
     if (nl <= kSparseMax) {
         // column (t, d) = t N + d of the noise is the row noise[col K : col K + K]
@@ -528,10 +533,6 @@ __global__ __launch_bounds__(kCT) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
                 if (lane == 0 && cb + r < nval) publish(blockIdx.x * stride + 2 + cb + r, a);
             }
         }
-    }
-    if (tid == 0) {
-        publish(blockIdx.x * stride, rho_b);
-        publish(blockIdx.x * stride + 1, eta_b);
     }
     STAMP(2, NOW());
     STAMP(5, (unsigned long long)nl);

@@ -195,11 +195,19 @@ __global__ __launch_bounds__(NT) void rollout_kernel(
     STAMP(8, (unsigned long long)__builtin_amdgcn_s_getreg(0xF804));   // HW_ID
     STAMP(9, (unsigned long long)__builtin_amdgcn_s_getreg(0xF814));   // XCC_ID
 #endif
+    // The first noise rows go out first: they depend on nothing and come from
+    // HBM, so every other prologue load (step block, keys) overlaps them.
+    const float2* np = noise + k;
+    float2 ring[kPF];   // noise rows eps[t][k] in flight
+#pragma unroll
+    for (int j = 0; j < kPF; ++j) ring[j] = noise_ld(np + (size_t)(j < T ? j : T - 1) * K);
     // this launch's granule tag (device epoch + 1), fetched now so its latency is hidden
     const unsigned tag_v = POLL ? __hip_atomic_load(epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) + 1u : 0u;
     // nominal element for the fused update, fetched now so its latency is hidden
     const double u_cur = ((flags & MPPI_FLAG_FUSED_UPDATE) && tid < 2 * T) ? st->u[tid >> 1][tid & 1] : 0.0;
-    if (tid < kSlots) s_win[tid] = st->win[tid];
+    // window row for the LDS copy: loaded unconditionally (a load inside the
+    // tid < kSlots branch would be waited for right there), stored before the barrier
+    const float4 wrow = st->win[tid & (kSlots - 1)];
     Search<LPS> sr;
     TabSearch ts;
     if constexpr (TAB) {
@@ -220,16 +228,11 @@ __global__ __launch_bounds__(NT) void rollout_kernel(
     x.dq2 = x0.w;
     sincos_f32(x.q1, &x.s1, &x.c1);
     sincos_f32(x.q1 + x.q2, &x.s12, &x.c12);
-    const float2* np = noise + k;
     cfloat* cua = (cfloat*)(st->ua);
-    float2 ring[kPF];   // noise rows eps[t][k] in flight
     float4 uring[kPF];  // per-step constants (u_t, a_t), uniform
 #pragma unroll
-    for (int j = 0; j < kPF; ++j) {
-        const int tj = j < T ? j : T - 1;
-        ring[j] = noise_ld(np + (size_t)tj * K);
-        uring[j] = const_ld4(cua + 4 * tj);
-    }
+    for (int j = 0; j < kPF; ++j) uring[j] = const_ld4(cua + 4 * (j < T ? j : T - 1));
+    if (tid < kSlots) s_win[tid] = wrow;
     __syncthreads();
 
     // Horizon loop (control.py:95-109): v = u + eps -> _F -> end effector ->
@@ -323,6 +326,7 @@ __global__ __launch_bounds__(NT) void rollout_kernel(
         else if (rem == 2) block(t, I2{});
         else if (rem == 3) block(t, I3{});
     } else {
+        STAMP(12, NOW());
         for (; t + kPF <= T; t += kPF) {
             step(t, I0{});
             step(t + 1, I1{});
@@ -330,6 +334,10 @@ __global__ __launch_bounds__(NT) void rollout_kernel(
             step(t + 3, I3{});
             S += (double)S4;
             S4 = 0.f;
+#ifdef MPPI_STAMPS
+            if (t == 0) STAMP(13, NOW());
+            if (t + kPF == T / 2) STAMP(14, NOW());
+#endif
         }
         if (t < T) step(t, I0{});          // remainder: t % kPF == 0, 1, 2 in order
         if (t + 1 < T) step(t + 1, I1{});
@@ -380,6 +388,12 @@ __global__ __launch_bounds__(NT) void rollout_kernel(
         if constexpr (POLL) st_gran(slab_r, idx, v, tag);
         else st_wt(slab_r, idx, v);
     };
+    // rho_b and eta_b leave first: a poll merger learns the global minimum and
+    // which rows carry weight before the slowest workgroup's gather is done
+    if (tid == 0) {
+        publish(blockIdx.x * stride, rho_b);
+        publish(blockIdx.x * stride + 1, eta_b);
+    }
     nl = __builtin_amdgcn_readfirstlane(nl);
     if (nl <= kSparseMax) {
         // few weighted samples (the usual case: S spread >> lambda): column
@@ -440,10 +454,6 @@ __global__ __launch_bounds__(NT) void rollout_kernel(
                 }
             }
         }
-    }
-    if (tid == 0) {
-        publish(blockIdx.x * stride, rho_b);
-        publish(blockIdx.x * stride + 1, eta_b);
     }
     STAMP(2, NOW());
     STAMP(5, (unsigned long long)nl);

@@ -66,6 +66,12 @@ for i in range(steps):
           f"grp-arrive {us(d[last, 3]):5.1f} grp-merge {us(d[last, 10]):5.1f} fin-arrive {us(d[last, 4]):5.1f} "
           f"fin-merge {us(d[last, 11]):5.1f} update {us(d[last, 7]):5.1f} | nl med {np.median(d[:, 5]):.0f} max {d[:, 5].max()} "
           f"| rows {d[last, 6]}")
+    if d[:, 12].any():   # loop stamps: prologue, first 4 steps, per-step rate over the second half
+        pro = (d[:, 12] - d[:, 0]) / 100.0
+        b0 = (d[:, 13] - d[:, 12]) / 100.0
+        rate = (d[:, 1] - d[:, 14]) / 100.0 / (T - T // 2) * 1e3
+        print(f"         prologue med {np.median(pro):.2f} max {pro.max():.2f} us | first 4 steps med {np.median(b0):.2f} us"
+              f" | second-half ns/step med {np.median(rate):.0f} max {rate.max():.0f}")
 if os.environ.get("DUMP"):   # the last step: rollout time of the older / younger workgroup sharing a CU
     order = np.argsort(d[:, 0])
     first = {}
