@@ -539,19 +539,19 @@ __global__ __launch_bounds__(kCT) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
     const int g = blockIdx.x / kGroup;
     const int gsz = min(kGroup, nrows - g * kGroup);
     if constexpr (POLL) {
-        if ((int)blockIdx.x != g * kGroup + gsz - 1) return;
+        if ((int)blockIdx.x != g * kGroup) return;
         STAMP(3, NOW());
         if (ngroups == 1) {
             merge_rows_block<kCT, kCMaxCh, true, true>(slab_r, 0, gsz, geo, c.inv_lambda, sm, nullptr, 0, partial_out,
                                                        w_eps_out, tag, tmo);
-        } else if ((int)blockIdx.x == nrows - 1 && nrows <= kDirectRows &&
+        } else if (blockIdx.x == 0 && nrows <= kDirectRows &&
                    direct_merge<kCT, kCMaxCh, true>(slab_r, nrows, geo, c.inv_lambda, sm, partial_out, w_eps_out, tag,
                                                     tmo)) {
         } else {
             merge_rows_block<kCT, kCMaxCh, false, true>(slab_r, g * kGroup, gsz, geo, c.inv_lambda, sm, &gslab_r, g,
                                                         nullptr, nullptr, tag, tmo);
             STAMP(10, NOW());
-            if ((int)blockIdx.x != nrows - 1) return;
+            if (blockIdx.x != 0) return;
             STAMP(4, NOW());
             merge_rows_block<kCT, kCMaxCh, true, true>(gslab_r, 0, ngroups, geo, c.inv_lambda, sm, nullptr, 0,
                                                        partial_out, w_eps_out, tag, tmo);

@@ -154,8 +154,8 @@ constexpr bool kBlockSteps = false;
 #endif
 
 // POLL: the partial rows travel as tagged granules (see st_gran) to consumer
-// workgroups that poll for them — the highest-numbered workgroup of each group
-// of kGroup merges its group, workgroup nblocks - 1 merges the groups — so no
+// workgroups that poll for them — the first workgroup of each group of kGroup
+// merges its group, workgroup 0 merges the groups — so no
 // workgroup drains its stores or waits on a counter, and the merges overlap the
 // stragglers.  Needs every workgroup resident at once (the host enables it
 // when the grid is at most one workgroup per CU); correctness does not depend
@@ -394,6 +394,7 @@ __global__ __launch_bounds__(NT) void rollout_kernel(
         publish(blockIdx.x * stride, rho_b);
         publish(blockIdx.x * stride + 1, eta_b);
     }
+    STAMP(15, NOW());
     nl = __builtin_amdgcn_readfirstlane(nl);
     if (nl <= kSparseMax) {
         // few weighted samples (the usual case: S spread >> lambda): column
@@ -460,20 +461,21 @@ __global__ __launch_bounds__(NT) void rollout_kernel(
     const int g = blockIdx.x / kGroup;
     const int gsz = min(kGroup, nrows - g * kGroup);
     if constexpr (POLL) {
-        // ---- level 1: the group's highest-numbered workgroup polls and merges its rows
-        if ((int)blockIdx.x != g * kGroup + gsz - 1) return;
+        // ---- level 1: the group's first workgroup polls and merges its rows (the first
+        // dispatched are the first done, so the merger is waiting when the last row lands)
+        if ((int)blockIdx.x != g * kGroup) return;
         STAMP(3, NOW());
         if (ngroups == 1) {
             merge_rows_block<NT, 1, true, true>(slab_r, 0, gsz, geo, c.inv_lambda, sm, nullptr, 0, partial_out, w_eps_out, tag, tmo);
-        } else if ((int)blockIdx.x == nrows - 1 && nrows <= kDirectRows &&
+        } else if (blockIdx.x == 0 && nrows <= kDirectRows &&
                    direct_merge<NT, 1, true>(slab_r, nrows, geo, c.inv_lambda, sm, partial_out, w_eps_out, tag, tmo)) {
             // few weighted rows: finished straight from the workgroup rows
         } else {
             merge_rows_block<NT, 1, false, true>(slab_r, g * kGroup, gsz, geo, c.inv_lambda, sm, &gslab_r, g, nullptr, nullptr, tag,
                                                  tmo);
             STAMP(10, NOW());
-            // ---- level 2: the last workgroup polls and merges the group rows
-            if ((int)blockIdx.x != nrows - 1) return;
+            // ---- level 2: workgroup 0 polls and merges the group rows
+            if (blockIdx.x != 0) return;
             STAMP(4, NOW());
             merge_rows_block<NT, 1, true, true>(gslab_r, 0, ngroups, geo, c.inv_lambda, sm, nullptr, 0, partial_out,
                                                 w_eps_out, tag, tmo);

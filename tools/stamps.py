@@ -66,6 +66,9 @@ for i in range(steps):
           f"grp-arrive {us(d[last, 3]):5.1f} grp-merge {us(d[last, 10]):5.1f} fin-arrive {us(d[last, 4]):5.1f} "
           f"fin-merge {us(d[last, 11]):5.1f} update {us(d[last, 7]):5.1f} | nl med {np.median(d[:, 5]):.0f} max {d[:, 5].max()} "
           f"| rows {d[last, 6]}")
+    if d[:, 15].any():
+        print(f"         last rho published {us(d[:, 15].max()):5.1f} (loop end of that wg {us(d[np.argmax(d[:, 15]), 1]):5.1f})"
+              f" -> final merge done {us(d[last, 11]):5.1f}")
     if d[:, 12].any():   # loop stamps: prologue, first 4 steps, per-step rate over the second half
         pro = (d[:, 12] - d[:, 0]) / 100.0
         b0 = (d[:, 13] - d[:, 12]) / 100.0
