@@ -24,6 +24,16 @@
 
 namespace mppi {
 
+// Diagnostic builds only (-DMPPI_STAMPS, a separate .so): per-workgroup
+// timeline in s_memrealtime ticks (100 MHz) + counters.  Never in the product.
+#ifdef MPPI_STAMPS
+#define STAMP(slot, val) do { if (dbg && threadIdx.x == 0) dbg[(size_t)blockIdx.x * 16 + (slot)] = (val); } while (0)
+#define NOW() __builtin_amdgcn_s_memrealtime()
+#else
+#define STAMP(slot, val) do { (void)dbg; } while (0)
+#define NOW() 0ull
+#endif
+
 constexpr int kMaxT = MPPI_MAX_T;
 
 constexpr int kSlots = 32;             // window slots (>= MPPI_SEARCH_LEN), index fits 5 bits
@@ -760,7 +770,7 @@ __device__ __forceinline__ void merge_rows_block(__amdgpu_buffer_rsrc_t rows, in
 template <int NT, int MAXCH, bool GRAN, class SM>
 __device__ __forceinline__ bool direct_merge(__amdgpu_buffer_rsrc_t rows, int n, const RowGeo& geo,
                                              double inv_lambda, SM& sm, double* out_row, double* w_eps_out,
-                                             unsigned tag, unsigned* tmo) {
+                                             unsigned tag, unsigned* tmo, unsigned long long* dbg = nullptr) {
     constexpr int P = kDirectRows / 64;
     constexpr int LB = 16;                      // loads per batch per thread
     constexpr int RB = LB / MAXCH;              // rows per load batch
@@ -827,6 +837,7 @@ __device__ __forceinline__ bool direct_merge(__amdgpu_buffer_rsrc_t rows, int n,
         if ((row >> 6) == j) sk = sj;
     }
     const bool mine = lane < nrel;
+    STAMP(13, NOW());
     // phase 2: eta and the (row, column chunk) entries of the weighted rows
     double acc[MAXCH], eta = 0.0, eta_k = 0.0;
 #pragma unroll
@@ -871,6 +882,7 @@ __device__ __forceinline__ bool direct_merge(__amdgpu_buffer_rsrc_t rows, int n,
             }
         }
     }
+    STAMP(14, NOW());
     put_final<NT, MAXCH>(rho, acc, eta, nrel, geo, sm, out_row, w_eps_out);
     return true;
 }
@@ -1027,12 +1039,3 @@ __device__ __forceinline__ void fair_priority(unsigned parity) {
         __builtin_amdgcn_s_setprio(0);
 }
 
-// Diagnostic builds only (-DMPPI_STAMPS, a separate .so): per-workgroup
-// timeline in s_memrealtime ticks (100 MHz) + counters.  Never in the product.
-#ifdef MPPI_STAMPS
-#define STAMP(slot, val) do { if (dbg && threadIdx.x == 0) dbg[(size_t)blockIdx.x * 16 + (slot)] = (val); } while (0)
-#define NOW() __builtin_amdgcn_s_memrealtime()
-#else
-#define STAMP(slot, val) do { (void)dbg; } while (0)
-#define NOW() 0ull
-#endif

@@ -468,7 +468,7 @@ __global__ __launch_bounds__(NT) void rollout_kernel(
         if (ngroups == 1) {
             merge_rows_block<NT, 1, true, true>(slab_r, 0, gsz, geo, c.inv_lambda, sm, nullptr, 0, partial_out, w_eps_out, tag, tmo);
         } else if (blockIdx.x == 0 && nrows <= kDirectRows &&
-                   direct_merge<NT, 1, true>(slab_r, nrows, geo, c.inv_lambda, sm, partial_out, w_eps_out, tag, tmo)) {
+                   direct_merge<NT, 1, true>(slab_r, nrows, geo, c.inv_lambda, sm, partial_out, w_eps_out, tag, tmo, dbg)) {
             // few weighted rows: finished straight from the workgroup rows
         } else {
             merge_rows_block<NT, 1, false, true>(slab_r, g * kGroup, gsz, geo, c.inv_lambda, sm, &gslab_r, g, nullptr, nullptr, tag,

@@ -66,6 +66,8 @@ for i in range(steps):
           f"grp-arrive {us(d[last, 3]):5.1f} grp-merge {us(d[last, 10]):5.1f} fin-arrive {us(d[last, 4]):5.1f} "
           f"fin-merge {us(d[last, 11]):5.1f} update {us(d[last, 7]):5.1f} | nl med {np.median(d[:, 5]):.0f} max {d[:, 5].max()} "
           f"| rows {d[last, 6]}")
+    if d[last, 13] and d[last, 14] and d[last, 13] > d[last, 3]:
+        print(f"         merger: rho seen {us(d[last, 13]):5.1f}, weighted rows loaded {us(d[last, 14]):5.1f}")
     if d[:, 15].any():
         print(f"         last rho published {us(d[:, 15].max()):5.1f} (loop end of that wg {us(d[np.argmax(d[:, 15]), 1]):5.1f})"
               f" -> final merge done {us(d[last, 11]):5.1f}")
