@@ -264,6 +264,7 @@ def main():
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
         elapsed, kern_ms = float(tt[0]), float(tt[1])
     args.steps = steps
+    eng.synchronize()   # raises if an in-launch hand-off timed out anywhere in the run (results invalid)
     u_final = eng.nominal()
     assert np.all(np.isfinite(u_final)), "non-finite nominal control"
 
