@@ -555,6 +555,7 @@ struct MergeScratch {
     double red[kMaxWaves];
     double weps[MAXV];
     double unew[MAXV];
+    double rho[kDirectRows];  // direct merge: the rows' rho, polled by wave 0
     int nrel;
 };
 
@@ -779,21 +780,28 @@ __device__ __forceinline__ bool direct_merge(__amdgpu_buffer_rsrc_t rows, int n,
     // phase 1: rho of row lane + 64 j in slot j
     double rho_l[P];
     if constexpr (GRAN) {
-        u32x4 gr[P];
-        for (unsigned spins = 0;; ++spins) {
-            asm volatile("" ::: "memory");
-            bool ok = true;
+        // ONE wave polls (a hop's latency sits in the polling CU's memory queue:
+        // MI355X guide, polling-cost / handoff-1to1) and hands the values over in LDS
+        if (tid < 64) {
+            u32x4 gr[P];
+            for (unsigned spins = 0;; ++spins) {
+                asm volatile("" ::: "memory");
+                bool ok = true;
 #pragma unroll
-            for (int j = 0; j < P; ++j) {
-                const int r = lane + 64 * j;
-                gr[j] = ld_gran(rows, r < n ? r * stride : kOffRange);
-                ok = ok && (r >= n || gran_ok(gr[j], tag));
+                for (int j = 0; j < P; ++j) {
+                    const int r = lane + 64 * j;
+                    gr[j] = ld_gran(rows, r < n ? r * stride : kOffRange);
+                    ok = ok && (r >= n || gran_ok(gr[j], tag));
+                }
+                if (__all(ok)) break;
+                MPPI_SPIN_OR_GIVE_UP(spins, tmo, lane);
             }
-            if (__all(ok)) break;
-            MPPI_SPIN_OR_GIVE_UP(spins, tmo, lane);
-        }
 #pragma unroll
-        for (int j = 0; j < P; ++j) rho_l[j] = lane + 64 * j < n ? gran_val(gr[j]) : INFINITY;
+            for (int j = 0; j < P; ++j) sm.rho[lane + 64 * j] = lane + 64 * j < n ? gran_val(gr[j]) : INFINITY;
+        }
+        __syncthreads();
+#pragma unroll
+        for (int j = 0; j < P; ++j) rho_l[j] = sm.rho[lane + 64 * j];
     } else {
 #pragma unroll
         for (int j = 0; j < P; ++j) {
