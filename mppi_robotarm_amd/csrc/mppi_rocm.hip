@@ -105,24 +105,33 @@ using Scratch = MergeScratch<2 * kMaxT>;
 // Median filter (scipy.ndimage.median_filter(size=10, mode='reflect'),
 // control.py:319-327, window [t-5, t+4], valid for T >= 5), u += w_eps
 // (control.py:126), shift (control.py:148-149) and the fp32 per-step constants
-// of the next launch.  u_cur: this thread's cur->u[t][d] (t = tid/2, d = tid%2),
-// read at kernel entry.
+// of the next launch.  Thread 2t + d produces the shifted element u_next[t][d]
+// = u[src][d] + median(src, d) with src = min(t + 1, T - 1) straight from the
+// filtered w_eps in sm.weps (no second barrier); u_src = cur->u[src][d], read
+// at kernel entry (nominal_src).  The pair (t, 0), (t, 1) meets through DPP.
+__device__ __forceinline__ double nominal_src(const DevStep* st, int tid, int T) {
+    const int t = tid >> 1, src = t + 1 < T ? t + 1 : T - 1;
+    return tid < 2 * T ? st->u[src][tid & 1] : 0.0;
+}
+
 template <int NT>
-__device__ void nominal_update_block(const DevStep* cur, DevStep* nxt, const KConst& c, Scratch& sm,
-                                     double u_cur) {
+__device__ void nominal_update_block(DevStep* nxt, const KConst& c, Scratch& sm, double u_src) {
     const int tid = threadIdx.x;
     const int T = c.T;
-    if (tid < 2 * T) sm.unew[tid] = u_cur + median_at(sm, tid >> 1, tid & 1, T, 2);
-    __syncthreads();
-    if (tid < T) {
-        const int src = tid + 1 < T ? tid + 1 : T - 1;
-        const double u0 = sm.unew[2 * src], u1 = sm.unew[2 * src + 1];
-        nxt->u[tid][0] = u0;
-        nxt->u[tid][1] = u1;
-        const double g0 = c.gamma * u0, g1 = c.gamma * u1;
-        const double a0 = g0 * c.sig_inv[0] + g1 * c.sig_inv[2];
-        const double a1 = g0 * c.sig_inv[1] + g1 * c.sig_inv[3];
-        nxt->ua[tid] = make_float4((float)u0, (float)u1, (float)a0, (float)a1);
+    if (tid >= ((2 * T + 63) & ~63)) return;   // whole waves: the DPP pairs stay complete
+    const int t = tid >> 1, d = tid & 1;
+    const int src = t + 1 < T ? t + 1 : T - 1;
+    const double un = tid < 2 * T ? u_src + median_at(sm, src, d, T, 2) : 0.0;
+    const double other = dpp_f64<0xB1>(un);   // quad_perm [1,0,3,2]: the partner element
+    if (tid < 2 * T) {
+        nxt->u[t][d] = un;
+        if (d == 0) {
+            const double u0 = un, u1 = other;
+            const double g0 = c.gamma * u0, g1 = c.gamma * u1;
+            const double a0 = g0 * c.sig_inv[0] + g1 * c.sig_inv[2];
+            const double a1 = g0 * c.sig_inv[1] + g1 * c.sig_inv[3];
+            nxt->ua[t] = make_float4((float)u0, (float)u1, (float)a0, (float)a1);
+        }
     }
     // win / key / x0 / ctr are written to both ping-pong blocks by
     // mppi_set_step_inputs, so only the nominal moves here.
@@ -204,7 +213,7 @@ __global__ __launch_bounds__(NT) void rollout_kernel(
     // this launch's granule tag (device epoch + 1), fetched now so its latency is hidden
     const unsigned tag_v = POLL ? __hip_atomic_load(epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) + 1u : 0u;
     // nominal element for the fused update, fetched now so its latency is hidden
-    const double u_cur = ((flags & MPPI_FLAG_FUSED_UPDATE) && tid < 2 * T) ? st->u[tid >> 1][tid & 1] : 0.0;
+    const double u_cur = (flags & MPPI_FLAG_FUSED_UPDATE) ? nominal_src(st, tid, T) : 0.0;
     // window row for the LDS copy: loaded unconditionally (a load inside the
     // tid < kSlots branch would be waited for right there), stored before the barrier
     const float4 wrow = st->win[tid & (kSlots - 1)];
@@ -501,7 +510,7 @@ __global__ __launch_bounds__(NT) void rollout_kernel(
     STAMP(11, NOW());
     STAMP(6, (unsigned long long)sm.nrel);
     if (flags & MPPI_FLAG_EXCHANGE) exchange_merge<NT, 1>(xd, geo, c.inv_lambda, sm, w_eps_out, tmo);
-    if (flags & MPPI_FLAG_FUSED_UPDATE) nominal_update_block<NT>(st, nxt, c, sm, u_cur);
+    if (flags & MPPI_FLAG_FUSED_UPDATE) nominal_update_block<NT>(nxt, c, sm, u_cur);
     STAMP(7, NOW());
 }
 
@@ -511,11 +520,11 @@ __global__ __launch_bounds__(NT) void merge_kernel(const KConst c, const double*
                                                    const DevStep* cur, DevStep* nxt, unsigned flags) {
     __shared__ Scratch sm;
     const int tid = threadIdx.x;
-    const double u_cur = ((flags & MPPI_FLAG_FUSED_UPDATE) && tid < 2 * c.T) ? cur->u[tid >> 1][tid & 1] : 0.0;
+    const double u_cur = (flags & MPPI_FLAG_FUSED_UPDATE) ? nominal_src(cur, tid, c.T) : 0.0;
     const __amdgpu_buffer_rsrc_t r = rows_rsrc(parts, n * (2 + 2 * c.T) * 8);
     merge_rows_block<NT, 1, true, false>(r, 0, n, RowGeo(2 * c.T), c.inv_lambda, sm, nullptr, 0, nullptr, w_eps_out,
                                          0u, nullptr);
-    if (flags & MPPI_FLAG_FUSED_UPDATE) nominal_update_block<NT>(cur, nxt, c, sm, u_cur);
+    if (flags & MPPI_FLAG_FUSED_UPDATE) nominal_update_block<NT>(nxt, c, sm, u_cur);
 }
 
 // Trajectory re-roll (control.py:129-145): control(t) = base[(t-1) mod T] (+ eps).
