@@ -496,14 +496,7 @@ __global__ __launch_bounds__(kCT) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
         // column (t, d) = t N + d of the noise is the row noise[col K : col K + K]
         for (int col = tid; col < nval; col += kCT) {
             const float* base = noise + (size_t)col * K;
-            float e[kSparseMax];
-#pragma unroll
-            for (int l = 0; l < kSparseMax; ++l) e[l] = base[nl > 0 ? s_k[min(l, nl - 1)] : 0];
-            double acc = 0.0;
-#pragma unroll
-            for (int l = 0; l < kSparseMax; ++l)
-                if (l < nl) acc = fma((double)s_e[l], (double)e[l], acc);
-            publish(blockIdx.x * stride + 2 + col, acc);
+            publish(blockIdx.x * stride + 2 + col, gather_col(base, 1, s_k, s_e, nl));
         }
     } else {
         constexpr int PER = kCT / 64;

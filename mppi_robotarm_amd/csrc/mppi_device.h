@@ -484,6 +484,33 @@ struct TabSearch {
     }
 };
 
+// Epilogue gather of one noise column for the workgroup's listed samples:
+// sum_l w_l eps[k_l] in ascending l (fp64 fma), the NL loads of the column
+// issued together.  NL is a compile-time bucket >= nl, so a workgroup with one
+// weighted sample issues one load per column, not kSparseMax.
+template <int NL>
+__device__ __forceinline__ double gather_col_n(const float* base, int kstride, const int* s_k, const float* s_e,
+                                               int nl) {
+    float e[NL];
+#pragma unroll
+    for (int l = 0; l < NL; ++l) e[l] = base[(size_t)(nl > 0 ? s_k[min(l, nl - 1)] : 0) * kstride];
+    double acc = 0.0;
+#pragma unroll
+    for (int l = 0; l < NL; ++l)
+        if (l < nl) acc = fma((double)s_e[l], (double)e[l], acc);
+    return acc;
+}
+// nl: wave-uniform, <= kSparseMax
+__device__ __forceinline__ double gather_col(const float* base, int kstride, const int* s_k, const float* s_e,
+                                             int nl) {
+    static_assert(kSparseMax == 16, "buckets");
+    if (nl <= 1) return gather_col_n<1>(base, kstride, s_k, s_e, nl);
+    if (nl <= 2) return gather_col_n<2>(base, kstride, s_k, s_e, nl);
+    if (nl <= 4) return gather_col_n<4>(base, kstride, s_k, s_e, nl);
+    if (nl <= 8) return gather_col_n<8>(base, kstride, s_k, s_e, nl);
+    return gather_col_n<16>(base, kstride, s_k, s_e, nl);
+}
+
 // stage / terminal cost terms (control.py:185-198, weights x 10000 folded in)
 __device__ __forceinline__ float weighted_sq(float ex, float ey, float e1, float e2, const float* w) {
     return fmaf(w[0], ex * ex, fmaf(w[1], ey * ey, fmaf(w[2], e1 * e1, w[3] * e2 * e2)));

@@ -412,14 +412,7 @@ __global__ __launch_bounds__(NT) void rollout_kernel(
         const float* nf = reinterpret_cast<const float*>(noise);
         for (int col = tid; col < 2 * T; col += NT) {
             const float* base = nf + (size_t)(col >> 1) * K * 2 + (col & 1);
-            float e[kSparseMax];
-#pragma unroll
-            for (int l = 0; l < kSparseMax; ++l) e[l] = base[(size_t)(nl > 0 ? s_k[min(l, nl - 1)] : 0) * 2];
-            double acc = 0.0;
-#pragma unroll
-            for (int l = 0; l < kSparseMax; ++l)
-                if (l < nl) acc = fma((double)s_e[l], (double)e[l], acc);
-            publish(blockIdx.x * stride + 2 + col, acc);
+            publish(blockIdx.x * stride + 2 + col, gather_col(base, 2, s_k, s_e, nl));
         }
     } else {
         // dense weights: each wave takes whole rows eps[t][k0 : k0 + NS] (coalesced),
