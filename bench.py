@@ -121,6 +121,20 @@ def cpu_baseline_c5(args, window, x0, u, K, T):
                       f"restatement oracle/chain_oracle.c, OpenMP, {el:.1f} s"}
 
 
+def dropin_latency(K, T, device, ticks=60):
+    """SURVEY §8(d)'s control-step latency: the wall time of the drop-in's
+    calc_control_input (host work + device noise + the fused rollout launch +
+    the host update of control.py:120-152), median over a closed loop of
+    run.py's driver (mppi_robotarm_amd.harness) at the bench's K and T."""
+    from mppi_robotarm_amd.harness import run_closed_loop
+    path = np.load(os.path.join(ROOT, "tests", "golden", "paths.npz"))["xydq_circle"][:, :4]
+    rec = run_closed_loop(path, ticks=ticks, number_of_samples_K=K, horizon_step_T=T, noise="device", seed=0,
+                          verbose=False, visualze_sampled_trajs=False, device=device)
+    rec["controller"].close()
+    lat = rec["latency_s"][2:] * 1e3
+    return float(np.median(lat)), float(np.percentile(lat, 90))
+
+
 def main():
     args = parse()
     c5 = args.workload == "c5"
@@ -291,7 +305,8 @@ def main():
             "warmup": args.warmup, "settle_ms": args.settle_ms,
             "ms_per_step": ms_per_step,
             "rollouts_per_s": K_total * args.steps / elapsed,
-            "control_step_latency_ms": ms_per_step,
+            "control_step_latency_ms": None,   # filled below (N = 1, c3): the drop-in's calc_control_input
+            "device_step_ms": ms_per_step,
             "kernel_ms": kern_ms,
             "higher_is_better": True,
             "scaling": "strong" if c5 else "weak",
@@ -313,6 +328,13 @@ def main():
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": achieved / HBM_PEAK_GBS, "traffic": traffic},
         }
+        if world == 1 and not c5:
+            med, p90 = dropin_latency(K, T, local_rank)
+            out["control_step_latency_ms"] = med
+            out["control_step_latency_p90_ms"] = p90
+            out["control_step_latency_def"] = ("median wall time of MPPIControllerForPathTracking.calc_control_input "
+                                               "(drop-in, noise='device', host update included) in run.py's closed "
+                                               "loop at this K, T; ms_per_step is the device-resident loop")
         if world == 1 and args.cpu_seconds > 0:
             out["cpu_baseline"] = (cpu_baseline_c5(args, window, x0, u, K, T) if c5
                                    else cpu_baseline(args, window, x0, u))

@@ -141,6 +141,18 @@ int mppi_get_nominal(mppi_ctx *ctx, double *u_host /* [T][2] */);
 int mppi_rollout_traj(mppi_ctx *ctx, const double *base_u, const float *noise_dev, int K,
                       float *out_dev);
 
+/* The optimal trajectory of control.py:129-134 (the updated controls u_new
+ * before the shift of :148-149, off-by-one u_new[t-1]) after a launch with
+ * MPPI_FLAG_FUSED_UPDATE: fp32 states out_dev[T][4] of one re-roll from x0,
+ * the controls taken from the update itself (no host round trip).
+ * MPPI_E_ARG before the first fused update. */
+int mppi_optimal_traj(mppi_ctx *ctx, float *out_dev);
+
+/* One synchronising read-back of a fused control step: the shifted nominal
+ * u[T][2] fp64 (the new self.u_prev, control.py:148-149) into u_host and, if
+ * traj_dev is not NULL, the fp32 [T][4] trajectory it holds into traj_host. */
+int mppi_get_step_outputs(mppi_ctx *ctx, double *u_host, const float *traj_dev, float *traj_host);
+
 /* Counter-based Philox4x32-10 Gaussian noise with covariance Sigma (replaces
  * np.random.multivariate_normal, control.py:163, for device-resident runs; not
  * bit-equal to NumPy).  Values depend only on (seed, step, t, global k), so a

@@ -28,7 +28,8 @@ EXPORTS = (
     "mppi_ctx_create", "mppi_ctx_destroy", "mppi_last_error", "mppi_set_stream", "mppi_ctx_info", "mppi_ctx_handoff",
     "mppi_set_step_inputs", "mppi_rollout", "mppi_merge_partials", "mppi_exchange_handle", "mppi_exchange_attach",
     "mppi_get_weighted_noise",
-    "mppi_get_nominal", "mppi_rollout_traj", "mppi_noise_philox", "mppi_sync", "mppi_debug_set_buffer",
+    "mppi_get_nominal", "mppi_rollout_traj", "mppi_optimal_traj", "mppi_get_step_outputs", "mppi_noise_philox",
+    "mppi_sync", "mppi_debug_set_buffer",
     "mppi_debug_search",
     "mppi_chain_ctx_create", "mppi_chain_ctx_destroy", "mppi_chain_set_stream", "mppi_chain_ctx_info",
     "mppi_chain_set_step_inputs", "mppi_chain_rollout", "mppi_chain_merge_partials", "mppi_chain_exchange_handle",
@@ -99,6 +100,8 @@ def open_library(path: str):
         "mppi_get_weighted_noise": ([vp, dp], C.c_int),
         "mppi_get_nominal": ([vp, dp], C.c_int),
         "mppi_rollout_traj": ([vp, dp, fp, C.c_int, fp], C.c_int),
+        "mppi_optimal_traj": ([vp, fp], C.c_int),
+        "mppi_get_step_outputs": ([vp, dp, fp, fp], C.c_int),
         "mppi_noise_philox": ([vp, C.c_ulonglong, C.c_ulonglong, fp], C.c_int),
         "mppi_sync": ([vp], C.c_int),
         "mppi_debug_set_buffer": ([vp, vp], C.c_int),

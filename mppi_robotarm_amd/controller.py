@@ -8,19 +8,27 @@ spelling), same ``calc_control_input(observed_x)`` contract (control.py:67-152):
       noise draw ``np.random.multivariate_normal`` on the legacy global RNG
       (control.py:154-164, same stream as the reference),
       ``np.linalg.inv(Sigma)`` (``LinAlgError`` as at control.py:106),
-      median filter via ``scipy.ndimage.median_filter`` (control.py:319-327),
-      ``u += w_eps`` in place, shift, and the aliasing return
-      (``u0`` is a view of the shifted ``u_prev``; ``u_seq is self.u_prev``);
+      and the aliasing return (``u0`` is a view of the shifted ``u_prev``;
+      ``u_seq is self.u_prev``);
   * device, HIP (O(K*T) work): rollouts, costs, soft-min weights, weighted
     noise sum (control.py:81-118) and the trajectory re-rolls
-    (control.py:129-145).
+    (control.py:129-145);
+  * the update of control.py:120-149 (median filter, ``u += w_eps``, shift):
+    for T >= 5 inside the rollout launch (fused update: the median of 10 is a
+    selection and the add is the same fp64 add, so the values equal the host
+    path's), then one read-back of the shifted nominal and the optimal
+    trajectory; with T < 5, or ``host_update=True``, on the host through
+    ``scipy.ndimage.median_filter`` (control.py:319-327) as the reference does.
+    With device noise the next step's noise is generated at the end of a call,
+    off the next call's critical path.
 
 Extra keyword arguments (all optional): ``device``, ``verbose`` (the three
 progress prints of control.py:227-229, on by default like the reference),
 ``noise`` ("numpy" = reference RNG stream, or "device" = on-device Philox),
-``seed`` (device noise), ``lanes_per_sample``, ``arm`` (ArmParams) and
+``seed`` (device noise), ``lanes_per_sample``, ``arm`` (ArmParams),
 ``process_group`` (shard the samples over the ranks of a torch.distributed
-group; one RCCL all-gather of the per-device partials per step).
+group; one RCCL all-gather of the per-device partials per step) and
+``host_update`` (force the host update path).
 """
 from __future__ import annotations
 
@@ -60,6 +68,7 @@ class MPPIControllerForPathTracking:
             lanes_per_sample: int = 0,
             arm: ArmParams | None = None,
             process_group=None,
+            host_update: bool = False,
     ) -> None:
         self.dim_x = 4
         self.dim_u = 2
@@ -92,6 +101,8 @@ class MPPIControllerForPathTracking:
         self._device = device
         self._engine = None
         self._step_count = 0
+        self._noise_ready = None       # (seed, step) of the device noise already in the buffer
+        self.host_update = bool(host_update) or self.T < 5   # the device median needs T >= 5
         self.keep_costs = False        # set True to keep per-sample S (self.last_S)
         self.last_S = None
 
@@ -114,6 +125,7 @@ class MPPIControllerForPathTracking:
             self._noise_dev = self._engine.new_noise()
             self._partial = self._engine.new_partial()
             self._S_dev = torch.empty(K_local, dtype=torch.float64, device=self._engine.device)
+            self._traj_dev = torch.empty((self.T, self.dim_x), dtype=torch.float32, device=self._engine.device)
             if world > 1:
                 self._gathered = torch.empty(world * self._engine.partial_len, dtype=torch.float64,
                                              device=self._engine.device)
@@ -141,13 +153,15 @@ class MPPIControllerForPathTracking:
         if epsilon is not None:
             lo = eng.k_offset
             eng.upload_noise(epsilon[lo:lo + eng.K_local], out=self._noise_dev)
-        else:
+        elif self._noise_ready != (self.seed, self._step_count):
             eng.philox_noise(self.seed, self._step_count, out=self._noise_dev)
         self._step_count += 1
 
         window = self.ref_path[self.prev_waypoints_idx:(self.prev_waypoints_idx + SEARCH_IDX_LEN)]
         eng.set_step_inputs(np.asarray(x0, dtype=np.float64), window, u)
         world, _ = self._shard()
+        if not self.host_update:
+            return self._fused_step(eng, u, world)
         if world == 1:
             eng.rollout(self._noise_dev, S_out=self._S_dev if self.keep_costs else None)
         else:
@@ -179,7 +193,49 @@ class MPPIControllerForPathTracking:
 
         self.u_prev[:-1] = u[1:]
         self.u_prev[-1] = u[-1]
+        self._prefetch_noise(eng)
         return u[0], u, optimal_traj, sampled_traj_list
+
+    def _fused_step(self, eng: RolloutEngine, u: np.ndarray, world: int):
+        """control.py:81-152 with the update inside the launch: rollouts + merge +
+        median filter + u += w_eps + shift on device, the optimal trajectory from the
+        updated controls, one read-back.  u is self.u_prev (updated in place)."""
+        S_out = self._S_dev if self.keep_costs else None
+        u_before = u.copy() if self.visualze_sampled_trajs else None
+        if world == 1:
+            eng.rollout(self._noise_dev, S_out=S_out, fused_update=True)
+        else:
+            eng.rollout(self._noise_dev, S_out=S_out, partial_out=self._partial)
+            exchange_partials(self._partial, self._gathered, self.process_group)
+            eng.merge(self._gathered, world, fused_update=True)
+        traj = eng.optimal_traj(out=self._traj_dev) if self.visualize_optimal_traj else None
+        sampled_traj_list = np.zeros((self.K, self.T, self.dim_x))
+        tr = None
+        if self.visualze_sampled_trajs:
+            tr = eng.trajectories(base_u=u_before, noise=self._noise_dev)   # pre-update u, v[k, t-1]
+        self._prefetch_noise(eng)
+        u_new, traj_host = eng.step_outputs(traj)
+        if self.keep_costs:
+            self.last_S = self._S_dev.cpu().numpy()
+        if tr is not None:
+            if world > 1:
+                import torch.distributed as dist
+                parts = [None] * world
+                dist.all_gather_object(parts, (eng.k_offset, tr.cpu().numpy()), group=self.process_group)
+                for off, arr in parts:
+                    sampled_traj_list[off:off + arr.shape[0]] = arr
+            else:
+                sampled_traj_list[:] = tr.double().cpu().numpy()
+        u[:] = u_new                                       # the shifted nominal, in place (aliasing kept)
+        optimal_traj = traj_host.astype(np.float64) if traj is not None else np.zeros((self.T, self.dim_x))
+        return u[0], u, optimal_traj, sampled_traj_list
+
+    def _prefetch_noise(self, eng: RolloutEngine) -> None:
+        """Device noise: draw the next step's noise now (stream-ordered after every
+        reader of this step's), so the next call does not wait for it."""
+        if self.noise_source == "device":
+            eng.philox_noise(self.seed, self._step_count, out=self._noise_dev)
+            self._noise_ready = (self.seed, self._step_count)
 
     # ------------------------------------------------------------ host helpers (reference semantics)
     @staticmethod

@@ -113,9 +113,17 @@ __device__ __forceinline__ double nominal_src(const DevStep* st, int tid, int T)
     const int t = tid >> 1, src = t + 1 < T ? t + 1 : T - 1;
     return tid < 2 * T ? st->u[src][tid & 1] : 0.0;
 }
+// cur->u[0][d] for threads 0 and 1 (the element the shift drops), else 0
+__device__ __forceinline__ double nominal_first(const DevStep* st, int tid) {
+    return tid < 2 ? st->u[0][tid] : 0.0;
+}
 
+// upd (nullable): the updated, not yet shifted controls u_new[t] in fp32, the
+// base of the optimal trajectory (control.py:129-134, mppi_optimal_traj):
+// u_new[t + 1] is this thread's shifted element, u_new[0] one more median.
 template <int NT>
-__device__ void nominal_update_block(DevStep* nxt, const KConst& c, Scratch& sm, double u_src) {
+__device__ void nominal_update_block(DevStep* nxt, const KConst& c, Scratch& sm, double u_src, double u_first,
+                                     float* upd) {
     const int tid = threadIdx.x;
     const int T = c.T;
     if (tid >= ((2 * T + 63) & ~63)) return;   // whole waves: the DPP pairs stay complete
@@ -123,6 +131,10 @@ __device__ void nominal_update_block(DevStep* nxt, const KConst& c, Scratch& sm,
     const int src = t + 1 < T ? t + 1 : T - 1;
     const double un = tid < 2 * T ? u_src + median_at(sm, src, d, T, 2) : 0.0;
     const double other = dpp_f64<0xB1>(un);   // quad_perm [1,0,3,2]: the partner element
+    if (upd && tid < 2 * T) {
+        if (t + 1 < T) upd[2 * (t + 1) + d] = (float)un;
+        if (t == 0) upd[d] = (float)(u_first + median_at(sm, 0, d, T, 2));
+    }
     if (tid < 2 * T) {
         nxt->u[t][d] = un;
         if (d == 0) {
@@ -179,7 +191,7 @@ __global__ __launch_bounds__(NT) void rollout_kernel(
     double* __restrict__ S_out, double* __restrict__ slab, double* __restrict__ gslab,
     unsigned* __restrict__ counters, double* __restrict__ partial_out, double* __restrict__ w_eps_out,
     DevStep* __restrict__ nxt, unsigned flags, const XDesc xd, unsigned* __restrict__ epoch, unsigned* __restrict__ tmo,
-    unsigned long long* __restrict__ dbg) {
+    float* __restrict__ upd, unsigned long long* __restrict__ dbg) {
     static_assert(!TAB || LPS == 1, "table search is per lane");
     __shared__ float4 s_win[kSlots];
     __shared__ __attribute__((aligned(16))) unsigned char s_tab[TAB ? kTabBytes : 16];
@@ -214,6 +226,7 @@ __global__ __launch_bounds__(NT) void rollout_kernel(
     const unsigned tag_v = POLL ? __hip_atomic_load(epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) + 1u : 0u;
     // nominal element for the fused update, fetched now so its latency is hidden
     const double u_cur = (flags & MPPI_FLAG_FUSED_UPDATE) ? nominal_src(st, tid, T) : 0.0;
+    const double u_first = (flags & MPPI_FLAG_FUSED_UPDATE) ? nominal_first(st, tid) : 0.0;
     // window row for the LDS copy: loaded unconditionally (a load inside the
     // tid < kSlots branch would be waited for right there), stored before the barrier
     const float4 wrow = st->win[tid & (kSlots - 1)];
@@ -503,21 +516,22 @@ __global__ __launch_bounds__(NT) void rollout_kernel(
     STAMP(11, NOW());
     STAMP(6, (unsigned long long)sm.nrel);
     if (flags & MPPI_FLAG_EXCHANGE) exchange_merge<NT, 1>(xd, geo, c.inv_lambda, sm, w_eps_out, tmo);
-    if (flags & MPPI_FLAG_FUSED_UPDATE) nominal_update_block<NT>(nxt, c, sm, u_cur);
+    if (flags & MPPI_FLAG_FUSED_UPDATE) nominal_update_block<NT>(nxt, c, sm, u_cur, u_first, upd);
     STAMP(7, NOW());
 }
 
 // Merge of the all-gathered per-device rows (multi-GPU), plus the fused update.
 template <int NT>
 __global__ __launch_bounds__(NT) void merge_kernel(const KConst c, const double* parts, int n, double* w_eps_out,
-                                                   const DevStep* cur, DevStep* nxt, unsigned flags) {
+                                                   const DevStep* cur, DevStep* nxt, unsigned flags, float* upd) {
     __shared__ Scratch sm;
     const int tid = threadIdx.x;
     const double u_cur = (flags & MPPI_FLAG_FUSED_UPDATE) ? nominal_src(cur, tid, c.T) : 0.0;
+    const double u_first = (flags & MPPI_FLAG_FUSED_UPDATE) ? nominal_first(cur, tid) : 0.0;
     const __amdgpu_buffer_rsrc_t r = rows_rsrc(parts, n * (2 + 2 * c.T) * 8);
     merge_rows_block<NT, 1, true, false>(r, 0, n, RowGeo(2 * c.T), c.inv_lambda, sm, nullptr, 0, nullptr, w_eps_out,
                                          0u, nullptr);
-    if (flags & MPPI_FLAG_FUSED_UPDATE) nominal_update_block<NT>(nxt, c, sm, u_cur);
+    if (flags & MPPI_FLAG_FUSED_UPDATE) nominal_update_block<NT>(nxt, c, sm, u_cur, u_first, upd);
 }
 
 // Trajectory re-roll (control.py:129-145): control(t) = base[(t-1) mod T] (+ eps).
@@ -630,6 +644,9 @@ struct mppi_ctx {
     double* h_buf = nullptr;    // pinned D2H staging, 2 * kMaxT doubles
     float2* d_base = nullptr;   // traj base controls
     float2* h_base = nullptr;   // pinned
+    float2* d_upd = nullptr;    // updated, unshifted controls of the last fused update (optimal trajectory)
+    bool upd_valid = false;
+    double* h_out = nullptr;    // pinned: nominal (2T fp64) + optimal trajectory (4T fp32) of mppi_get_step_outputs
     double sig_inv[4];
     unsigned long long* d_dbg = nullptr;  // diagnostic stamp buffer (MPPI_STAMPS builds)
     // node-level exchange (mppi_exchange_*): inbox, this rank's row, epoch, peer mappings
@@ -808,6 +825,9 @@ int mppi_ctx_create(const mppi_config* cfg, int device, void* stream, mppi_ctx**
         (e = hipMalloc(&c->d_counter, ctr_bytes)) != hipSuccess ||
         (e = hipMalloc(&c->d_weps, 2 * kMaxT * sizeof(double))) != hipSuccess ||
         (e = hipMalloc(&c->d_base, kMaxT * sizeof(float2))) != hipSuccess ||
+        (e = hipMalloc(&c->d_upd, kMaxT * sizeof(float2))) != hipSuccess ||
+        (e = hipHostMalloc(&c->h_out, 2 * kMaxT * sizeof(double) + 4 * kMaxT * sizeof(float), hipHostMallocDefault)) !=
+            hipSuccess ||
         (e = hipHostMalloc(&c->h_step, sizeof(DevStep), hipHostMallocDefault)) != hipSuccess ||
         (e = hipHostMalloc(&c->h_buf, 2 * kMaxT * sizeof(double), hipHostMallocDefault)) != hipSuccess ||
         (e = hipHostMalloc(&c->h_base, kMaxT * sizeof(float2), hipHostMallocDefault)) != hipSuccess ||
@@ -839,6 +859,8 @@ void mppi_ctx_destroy(mppi_ctx* c) {
     (void)hipFree(c->d_gslab);
     (void)hipFree(c->d_weps);
     (void)hipFree(c->d_base);
+    (void)hipFree(c->d_upd);
+    if (c->h_out) (void)hipHostFree(c->h_out);
     for (void* p : c->xopened)
         if (p) (void)hipIpcCloseMemHandle(p);
     (void)hipFree(c->d_inbox);
@@ -937,7 +959,7 @@ int mppi_rollout(mppi_ctx* c, const float* noise_dev, double* S_dev, double* par
 #define MPPI_LAUNCH3(L, NTH, P, TB)                                                                             \
     hipLaunchKernelGGL((rollout_kernel<L, NTH, P, TB>), dim3(c->nblocks), dim3(NTH), 0, c->stream, c->kc, cur, c->d_tab, nz, \
                        S_dev, c->d_slab, c->d_gslab, c->d_counter, partial_dev, c->d_weps, nxt, flags, c->xd, c->d_epoch, \
-                       c->d_tmo, c->d_dbg)
+                       c->d_tmo, reinterpret_cast<float*>(c->d_upd), c->d_dbg)
 #define MPPI_LAUNCH2(L, NTH, P)                  \
     do {                                        \
         if (c->use_tab) MPPI_LAUNCH3(L, NTH, P, true); \
@@ -967,7 +989,10 @@ int mppi_rollout(mppi_ctx* c, const float* noise_dev, double* S_dev, double* par
 #undef MPPI_LAUNCH2
 #undef MPPI_LAUNCH3
     const int rc = launch_check("rollout_kernel");
-    if (rc == MPPI_OK && (flags & MPPI_FLAG_FUSED_UPDATE)) c->cur ^= 1;
+    if (rc == MPPI_OK && (flags & MPPI_FLAG_FUSED_UPDATE)) {
+        c->cur ^= 1;
+        c->upd_valid = true;
+    }
     return rc;
 }
 
@@ -1023,12 +1048,15 @@ int mppi_merge_partials(mppi_ctx* c, const double* partials_dev, int n, unsigned
     // one workgroup, one thread per merged column (2T + 1 <= 256 up to T = 127)
     if (2 * c->cfg.T + 1 <= 256)
         hipLaunchKernelGGL(merge_kernel<256>, dim3(1), dim3(256), 0, c->stream, c->kc, partials_dev, n, c->d_weps,
-                           cur, nxt, flags);
+                           cur, nxt, flags, reinterpret_cast<float*>(c->d_upd));
     else
         hipLaunchKernelGGL(merge_kernel<512>, dim3(1), dim3(512), 0, c->stream, c->kc, partials_dev, n, c->d_weps,
-                           cur, nxt, flags);
+                           cur, nxt, flags, reinterpret_cast<float*>(c->d_upd));
     const int rc = launch_check("merge_kernel");
-    if (rc == MPPI_OK && (flags & MPPI_FLAG_FUSED_UPDATE)) c->cur ^= 1;
+    if (rc == MPPI_OK && (flags & MPPI_FLAG_FUSED_UPDATE)) {
+        c->cur ^= 1;
+        c->upd_valid = true;
+    }
     return rc;
 }
 
@@ -1071,6 +1099,29 @@ int mppi_rollout_traj(mppi_ctx* c, const double* base_u, const float* noise_dev,
     hipLaunchKernelGGL(traj_kernel, dim3(blocks), dim3(kThreads), 0, c->stream, c->kc, cur, base,
                        reinterpret_cast<const float2*>(noise_dev), K, reinterpret_cast<float4*>(out_dev));
     return launch_check("traj_kernel");
+}
+
+int mppi_optimal_traj(mppi_ctx* c, float* out_dev) {
+    if (!c || !out_dev) return fail(MPPI_E_ARG, "null argument");
+    if (!c->upd_valid) return fail(MPPI_E_ARG, "mppi_optimal_traj needs a preceding MPPI_FLAG_FUSED_UPDATE launch");
+    // x0 and the window are in both ping-pong blocks, so the current one serves
+    hipLaunchKernelGGL(traj_kernel, dim3(1), dim3(kThreads), 0, c->stream, c->kc, c->d_step + c->cur, c->d_upd,
+                       (const float2*)nullptr, 1, reinterpret_cast<float4*>(out_dev));
+    return launch_check("traj_kernel");
+}
+
+int mppi_get_step_outputs(mppi_ctx* c, double* u_host, const float* traj_dev, float* traj_host) {
+    if (!c || !u_host || (traj_dev && !traj_host)) return fail(MPPI_E_ARG, "bad argument");
+    const int T = c->cfg.T;
+    const size_t ub = 2 * (size_t)T * sizeof(double), tb = 4 * (size_t)T * sizeof(float);
+    float* h_traj = reinterpret_cast<float*>(c->h_out + 2 * kMaxT);
+    HIP_TRY(hipMemcpyAsync(c->h_out, (const char*)(c->d_step + c->cur) + offsetof(DevStep, u), ub,
+                           hipMemcpyDeviceToHost, c->stream));
+    if (traj_dev) HIP_TRY(hipMemcpyAsync(h_traj, traj_dev, tb, hipMemcpyDeviceToHost, c->stream));
+    HIP_TRY(hipStreamSynchronize(c->stream));
+    memcpy(u_host, c->h_out, ub);
+    if (traj_dev) memcpy(traj_host, h_traj, tb);
+    return check_timeout(c);
 }
 
 int mppi_noise_philox(mppi_ctx* c, unsigned long long seed, unsigned long long step, float* out_dev) {

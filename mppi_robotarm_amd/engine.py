@@ -188,6 +188,26 @@ class RolloutEngine:
         self._keep_traj = bu
         return out
 
+    def optimal_traj(self, out: torch.Tensor | None = None) -> torch.Tensor:
+        """(T, 4) fp32 optimal trajectory (control.py:129-134) from the controls of the
+        last fused update, before their shift (mppi_optimal_traj)."""
+        self._sync_stream()
+        out = torch.empty((self.T, 4), dtype=torch.float32, device=self.device) if out is None else out
+        N.check(self._lib.mppi_optimal_traj(self._ctx, C.c_void_p(out.data_ptr())), "mppi_optimal_traj")
+        return out
+
+    def step_outputs(self, traj: torch.Tensor | None = None):
+        """One synchronising read-back after a fused step: the shifted nominal (T, 2) fp64
+        and, if given, the (T, 4) fp32 trajectory tensor as a host array (else None)."""
+        self._sync_stream()
+        u = np.zeros((self.T, 2))
+        tr = np.zeros((self.T, 4), dtype=np.float32) if traj is not None else None
+        N.check(self._lib.mppi_get_step_outputs(self._ctx, _dptr(u),
+                                                C.c_void_p(traj.data_ptr()) if traj is not None else None,
+                                                tr.ctypes.data_as(C.c_void_p) if tr is not None else None),
+                "mppi_get_step_outputs")
+        return u, tr
+
     def philox_noise(self, seed: int, step: int = 0, out: torch.Tensor | None = None) -> torch.Tensor:
         self._sync_stream()
         out = self.new_noise() if out is None else out

@@ -396,3 +396,39 @@ def test_free_running_closed_loop_tracks_reference(paths):
     # from the reference's recorded states (fp32-rounded draws) after these 25 ticks
     np.testing.assert_allclose(np.array(seen), ref, atol=5e-2)
     ctrl.close()
+
+
+@pytest.mark.parametrize("name", ["runpy_k100_t30", "dense_k256_t24", "end_k64_t16", "expl_k128_t20"])
+def test_fused_dropin_equals_host_update_path(name, paths):
+    """The default drop-in (update inside the launch, optimal trajectory from the
+    update, one read-back) against host_update=True (scipy median on the host, as
+    the reference): identical u, u0 aliasing, trajectories and S."""
+    g = load_step(name)
+    eps = g["eps"].astype(np.float64)
+    outs = []
+    for host in (False, True):
+        c = _ctrl(g, paths, host_update=host)
+        c.keep_costs = True
+        c._calc_epsilon = lambda *a, **k: eps
+        u_prev = c.u_prev
+        u0, u_seq, opt, samp = c.calc_control_input(g["x0"])
+        assert u_seq is u_prev and np.shares_memory(u0, u_prev)
+        outs.append((u_seq.copy(), float(u0[0]), opt.copy(), samp.copy(), c.last_S.copy()))
+        c.close()
+    (ua, u0a, oa, sa, Sa), (ub, u0b, ob, sb, Sb) = outs
+    assert np.array_equal(ua, ub) and u0a == u0b
+    assert np.array_equal(oa, ob) and np.array_equal(sa, sb) and np.array_equal(Sa, Sb)
+
+
+def test_fused_dropin_device_noise_loop_equals_host_update(paths):
+    """A closed loop with device noise (next step's noise drawn at the end of each
+    call): the fused path and the host-update path give the same trajectory."""
+    from mppi_robotarm_amd.harness import run_closed_loop
+    recs = []
+    for host in (False, True):
+        rec = run_closed_loop(paths["xydq_circle"][:, :4], ticks=12, number_of_samples_K=4096, horizon_step_T=32,
+                              noise="device", seed=5, verbose=False, visualze_sampled_trajs=False, device=0,
+                              host_update=host)
+        recs.append((rec["u"].copy(), rec["q"].copy()))
+        rec["controller"].close()
+    assert np.array_equal(recs[0][0], recs[1][0]) and np.array_equal(recs[0][1], recs[1][1])
