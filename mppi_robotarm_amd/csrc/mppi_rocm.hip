@@ -173,6 +173,13 @@ constexpr bool kBlockSteps = true;
 #else
 constexpr bool kBlockSteps = false;
 #endif
+// Deferred cost (default): each step's waypoint row is consumed after the next
+// step's dynamics (see dstep); MPPI_STEP_COST builds keep step() (diagnostics).
+#ifdef MPPI_STEP_COST
+constexpr bool kDeferCost = false;
+#else
+constexpr bool kDeferCost = true;
+#endif
 
 // POLL: the partial rows travel as tagged granules (see st_gran) to consumer
 // workgroups that poll for them — the first workgroup of each group of kGroup
@@ -194,6 +201,7 @@ __global__ __launch_bounds__(NT) void rollout_kernel(
     float* __restrict__ upd, unsigned long long* __restrict__ dbg) {
     static_assert(!TAB || LPS == 1, "table search is per lane");
     __shared__ float4 s_win[kSlots];
+    __shared__ float4 s_ua[kDeferCost ? kMaxT : 1];   // per-step constants (u_t, a_t), kDeferCost
     __shared__ __attribute__((aligned(16))) unsigned char s_tab[TAB ? kTabBytes : 16];
     __shared__ float4 s_rows[TAB ? kKeyRows : 1];
     __shared__ KeyPair s_kp[TAB ? kKeyPairs : 1];
@@ -252,10 +260,18 @@ __global__ __launch_bounds__(NT) void rollout_kernel(
     sincos_f32(x.q1 + x.q2, &x.s12, &x.c12);
     cfloat* cua = (cfloat*)(st->ua);
     float4 uring[kPF];  // per-step constants (u_t, a_t), uniform
+    if constexpr (kDeferCost) {
+        for (int i = tid; i < T; i += NT) s_ua[i] = st->ua[i];
+    } else {
 #pragma unroll
-    for (int j = 0; j < kPF; ++j) uring[j] = const_ld4(cua + 4 * (j < T ? j : T - 1));
+        for (int j = 0; j < kPF; ++j) uring[j] = const_ld4(cua + 4 * (j < T ? j : T - 1));
+    }
     if (tid < kSlots) s_win[tid] = wrow;
     __syncthreads();
+    if constexpr (kDeferCost) {
+#pragma unroll
+        for (int j = 0; j < kPF; ++j) uring[j] = s_ua[j < T ? j : T - 1];
+    }
 
     // Horizon loop (control.py:95-109): v = u + eps -> _F -> end effector ->
     // nearest waypoint -> stage cost + control cost, S in fp64.
@@ -277,13 +293,59 @@ __global__ __launch_bounds__(NT) void rollout_kernel(
         dyn_step(x, v1, v2, c);
         const float px = fmaf(c.fk1, x.c1, c.fk2 * x.c12);  // control.py:178-179
         const float py = fmaf(c.fk1, x.s1, c.fk2 * x.s12);
+#if defined(MPPI_ABL_NOSEARCH)   // diagnostic ablations (wrong results): no window scan / no LDS row lookup
+        const float4 r = s_win[(__float_as_uint(px) ^ __float_as_uint(py)) & 31u];
+#elif defined(MPPI_ABL_NOLOOKUP)
+        const unsigned jj = sr.nearest(px, py);
+        const float4 r = make_float4((float)jj * 1e-3f, 0.f, (float)jj, 0.f);
+#else
         const float4 r = s_win[sr.nearest(px, py)];
+#endif
         ex = px - r.x;
         ey = py - r.y;
         e1 = x.dq1 - r.z;
         e2 = x.dq2 - r.w;
         const float g = fmaf(ua.z, v1, ua.w * v2);  // (gamma u^T Sigma^-1) v, control.py:106
         S4 += weighted_sq(ex, ey, e1, e2, c.sw) + g;
+    };
+    // kDeferCost: the LDS row of step t's nearest waypoint is consumed one step
+    // later, after step t + 1's dynamics, so the lookup's latency is hidden; the
+    // per-step constants come from LDS (no scalar load shares lgkmcnt with the
+    // lookup).  The costs are added in step order and folded every kPF steps as
+    // in step() (same sums).
+    float4 pr = make_float4(0.f, 0.f, 0.f, 0.f);
+    float ppx = 0.f, ppy = 0.f, pd1 = 0.f, pd2 = 0.f, pg = 0.f;
+    auto add_pending = [&]() {
+        ex = ppx - pr.x;
+        ey = ppy - pr.y;
+        e1 = pd1 - pr.z;
+        e2 = pd2 - pr.w;
+        S4 += weighted_sq(ex, ey, e1, e2, c.sw) + pg;
+    };
+    auto dstep = [&](int t, auto slot_c) {
+        constexpr int slot = decltype(slot_c)::value;
+        const float2 e = ring[slot];
+        const float4 ua = uring[slot];
+        const int tl = t + kPF < T ? t + kPF : T - 1;
+        ring[slot] = noise_ld(np + (size_t)tl * K);
+        uring[slot] = s_ua[tl];
+        PIN_LOADS();
+        const float v1 = fmaf(exf, ua.x, e.x);  // u[t] + eps (exploit) or eps, control.py:99-101
+        const float v2 = fmaf(exf, ua.y, e.y);
+        dyn_step(x, v1, v2, c);
+        if (t > 0) {
+            add_pending();   // step t - 1
+            if (slot == 0) {
+                S += (double)S4;
+                S4 = 0.f;
+            }
+        }
+        ppx = fmaf(c.fk1, x.c1, c.fk2 * x.c12);  // control.py:178-179
+        ppy = fmaf(c.fk1, x.s1, c.fk2 * x.s12);
+        pd1 = x.dq1;
+        pd2 = x.dq2;
+        pg = fmaf(ua.z, v1, ua.w * v2);  // (gamma u^T Sigma^-1) v, control.py:106
+        pr = s_win[sr.nearest(ppx, ppy)];
     };
     // TAB: the dynamics of steps t..t+n-1 first, then their n window searches
     // together (independent of each other: the lookups' LDS latencies overlap),
@@ -347,6 +409,22 @@ __global__ __launch_bounds__(NT) void rollout_kernel(
         if (rem == 1) block(t, I1{});
         else if (rem == 2) block(t, I2{});
         else if (rem == 3) block(t, I3{});
+    } else if constexpr (kDeferCost) {
+        STAMP(12, NOW());
+        for (; t + kPF <= T; t += kPF) {
+            dstep(t, I0{});
+            dstep(t + 1, I1{});
+            dstep(t + 2, I2{});
+            dstep(t + 3, I3{});
+#ifdef MPPI_STAMPS
+            if (t == 0) STAMP(13, NOW());
+            if (t + kPF == T / 2) STAMP(14, NOW());
+#endif
+        }
+        if (t < T) dstep(t, I0{});          // remainder: t % kPF == 0, 1, 2 in order
+        if (t + 1 < T) dstep(t + 1, I1{});
+        if (t + 2 < T) dstep(t + 2, I2{});
+        add_pending();                       // step T - 1
     } else {
         STAMP(12, NOW());
         for (; t + kPF <= T; t += kPF) {
