@@ -45,6 +45,34 @@ from mppi_robotarm_amd.params import ArmParams, X0_RUNPY  # noqa: E402
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md, chip-level parameters)
 BYTES_PER_STATE_STEP = 8  # fp32 eps[t][k][0:2] read once
 C5_BYTES_PER_STATE_STEP = 28  # fp32 eps[t][0:7][k] read once ("C5 (du=7): 28 B/state-step")
+# VALU issue roofline (SURVEY §8d asks for it beside the HBM one).  MI355X_MICROARCH.md: 256 CUs x 4 SIMD-32,
+# 2.4 GHz max clock; a SIMD issues one wave64 VALU instruction per 2 cycles, one wave alone one per 4 cycles
+# (row 'vector-instruction ISSUE cost'; transcendentals 8).
+SIMDS = 1024
+CLOCK_HZ = 2.4e9
+SIMD_ISSUE_CYC = 2.0
+LONE_WAVE_ISSUE_CYC = 4.0
+
+
+def valu_roofline(tj, kern_ms):
+    """VALU issue roofline of the rollout launch from the PMC count in the traffic json (SQ_INSTS_VALU, whole
+    device, per launch; tools/traffic_summary.py) and this run's kernel time."""
+    n = tj.get("valu_insts_per_launch") if tj else None
+    waves = tj.get("waves_per_launch") if tj else None
+    if not n or not waves:
+        return None
+    cycles = kern_ms * 1e-3 * CLOCK_HZ
+    per_simd = n / SIMDS   # wave-instructions each SIMD issues (waves are spread evenly, <= 1 workgroup per CU)
+    waves_per_simd = waves / SIMDS
+    achieved = per_simd / cycles   # wave-instructions per SIMD-cycle
+    out = {"bound": "valu-issue", "achieved": achieved, "peak": 1.0 / SIMD_ISSUE_CYC,
+           "unit": "wave-instr/SIMD/cycle", "frac": achieved * SIMD_ISSUE_CYC,
+           "waves_per_simd": waves_per_simd, "valu_insts_per_launch": n,
+           "source": "SQ_INSTS_VALU (" + str(tj.get("source", "")).split("; ")[-1] + "), live kernel time, 2.4 GHz"}
+    if waves_per_simd <= 1.0:
+        # a lone wave cannot use the SIMD's full rate: its own ceiling is one instruction per 4 cycles
+        out["frac_one_wave_ceiling"] = achieved * LONE_WAVE_ISSUE_CYC
+    return out
 
 
 def parse():
@@ -288,11 +316,13 @@ def main():
         alg_bytes = (C5_BYTES_PER_STATE_STEP if c5 else BYTES_PER_STATE_STEP) * K * T
         achieved = alg_bytes / (kern_ms * 1e-3) / 1e9
         traffic = None
+        valu = None
         if os.path.exists(args.traffic_json):
             try:
                 tj = json.load(open(args.traffic_json))
                 if tj.get("K") == K and tj.get("T") == T and tj.get("workload", "c3") == args.workload:
                     traffic = tj.get("hbm_bytes_per_launch")
+                    valu = valu_roofline(tj, kern_ms)
             except Exception:
                 traffic = None
         out = {
@@ -327,6 +357,7 @@ def main():
                                                                else ", back-to-back launches")},
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": achieved / HBM_PEAK_GBS, "traffic": traffic},
+            "valu_roofline": valu,
         }
         if world == 1 and not c5:
             med, p90 = dropin_latency(K, T, local_rank)

@@ -147,3 +147,20 @@ def test_harness_plant_matches_reference_loop():
         assert np.array_equal(np.concatenate([q, dq]), nxt)
     x1, y1, x2, y2 = forward_kinematics(np.array([0.3, -0.4]))
     assert np.allclose([x2, y2], [np.cos(0.3) + np.cos(-0.1), np.sin(0.3) + np.sin(-0.1)])
+
+
+def test_bench_valu_roofline_from_committed_counters():
+    """bench.py's VALU issue roofline from the committed PMC summary: one wave per SIMD at c3,
+    two at c5; fractions of the SIMD's issue rate in (0, 1]."""
+    import json
+    import os
+    import bench
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    for name, kern_ms, wps in (("traffic.json", 0.0293, 1.0), ("traffic_c5.json", 0.250, 2.0)):
+        tj = json.load(open(os.path.join(root, "profiles", name)))
+        v = bench.valu_roofline(tj, kern_ms)
+        assert v["waves_per_simd"] == wps and 0.0 < v["frac"] <= 1.0
+        assert v["frac"] == pytest.approx(tj["valu_insts_per_launch"] / bench.SIMDS * bench.SIMD_ISSUE_CYC
+                                          / (kern_ms * 1e-3 * bench.CLOCK_HZ))
+        assert ("frac_one_wave_ceiling" in v) == (wps == 1.0)
+    assert bench.valu_roofline({}, 0.03) is None

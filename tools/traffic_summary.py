@@ -11,7 +11,7 @@ bytes, WRITE_SIZE at 1.0x) and writes:
   profiles/TAG/kernel_stats.csv      rocprofv3 --kernel-trace --stats summary
   profiles/TAG/pmc_*.csv             the counter CSVs (one per pass)
   profiles/TAG/sq_counters.json      SQ issue / wait summary
-  profiles/traffic.json              HBM bytes per rollout launch (read by bench.py)
+  profiles/traffic.json              HBM bytes and VALU instructions per rollout launch (read by bench.py)
 """
 import csv
 import json
@@ -80,11 +80,15 @@ def main():
         "rocprof_avg_kernel_ns": avg_ns,
         "source": f"rocprofv3 --pmc FETCH_SIZE / --pmc WRITE_SIZE (separate passes), bench.py; {os.path.basename(dst)}",
     }
+    sqf = os.path.join(src, "sq", "p_counter_collection.csv")
+    sq = {k: float(np.median(v)) for k, v in counters(sqf, kpat).items()} if os.path.exists(sqf) else {}
+    if "SQ_INSTS_VALU" in sq:
+        # whole-device VALU wave-instructions per launch (bench.py's "valu" roofline)
+        out["valu_insts_per_launch"] = sq["SQ_INSTS_VALU"]
+        out["waves_per_launch"] = sq.get("SQ_WAVES")
     name = "traffic_c5.json" if workload == "c5" else "traffic.json"
     json.dump(out, open(os.path.join(os.path.dirname(dst.rstrip('/')), name), "w"), indent=1)
-    sqf = os.path.join(src, "sq", "p_counter_collection.csv")
-    if os.path.exists(sqf):
-        sq = {k: float(np.median(v)) for k, v in counters(sqf, kpat).items()}
+    if sq:
         gr = {}
         grf = os.path.join(src, "grbm", "p_counter_collection.csv")
         if os.path.exists(grf):
