@@ -38,8 +38,14 @@ constexpr int kCMax = MPPI_CHAIN_MAX_DOF;   // links
 constexpr int kCT = 256;                    // threads per workgroup, one lane per sample
 constexpr int kCMaxCh = 4;                  // column chunks of a partial row: T N + 1 <= 4 x 256 ... (N <= 7)
 constexpr int kCMaxVals = kMaxT * kCMax;    // T N values per row, at most
-constexpr int kCPF = 2;                     // noise steps in flight per lane (N rows each)
-constexpr int kCPU = 2;                     // per-step constant rows in flight
+#ifndef MPPI_CHAIN_CPF
+#define MPPI_CHAIN_CPF 2
+#endif
+#ifndef MPPI_CHAIN_CPU
+#define MPPI_CHAIN_CPU 2
+#endif
+constexpr int kCPF = MPPI_CHAIN_CPF;        // noise steps in flight per lane (N rows each)
+constexpr int kCPU = MPPI_CHAIN_CPU;        // per-step constant rows in flight
 
 // Device-resident per-step parameter block (ping-pong pair in the context).
 struct alignas(16) ChainStep {
@@ -381,10 +387,19 @@ __global__ __launch_bounds__(kCT) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
     // last step read row T - 1 again (never used)
     // (uniform row base + a 32-bit lane byte offset: the saddr form of global_load)
     const unsigned kb = (unsigned)k * 4u;
+#ifdef MPPI_CHAIN_NOISE_BUFFER
+    // row offset in the buffer instruction's scalar soffset: no 64-bit VALU address per load
+    const __amdgpu_buffer_rsrc_t nrs = rows_rsrc(noise, T * N * K * 4);
+    auto nrow = [&](int t, int d) {
+        const int so = __builtin_amdgcn_readfirstlane((min(t, T - 1) * N + d) * K * 4);
+        return __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(nrs, (int)kb, so, 0));
+    };
+#else
     auto nrow = [&](int t, int d) {
         const char* row = (const char*)(noise + ((size_t)min(t, T - 1) * N + d) * K);
         return *(const float*)(row + kb);
     };
+#endif
     cfloat* cua = (cfloat*)(&st->ua[0][0]);
     float ring[kCPF][N];
     float uring[kCPU][2 * N];

@@ -242,6 +242,100 @@ struct Search {
     }
 };
 
+// The same search (LPS = 1) with the keys of a whole wave from the matrix core.
+// The 32 slots x 64 samples of keys are a product  [c' ry' rx' 0] x [1 ay ax 0]^T,
+// two chained v_mfma_f32_32x32x2_f32 per half-wave of samples:
+//   D = mfma(A2 = (rx', 0), B2 = (ax, 0), mfma(A1 = (c', ry'), B1 = (1, ay), 0)),
+// which is bit-identical to Search's fma(ax, rx', fma(ay, ry', c')) (each MFMA
+// rounds its 2-term dot product plus accumulator once; c' * 1 and 0 * b are
+// exact; checked on 8.4 M keys by tools/mfma_probe.hip, and end to end by the
+// parity tests).  Operand lane l holds A[i = l % 32][k = l / 32] and
+// B[k = l / 32][j = l % 32]; result register r of lane l is D[slot][j] with
+//   slot = 8 (r / 4) + 4 (l / 32) + r % 4,   j = l % 32,
+// so each lane ends with 16 of the 32 keys of one sample of each half: sample
+// l % 32 (half 0) and 32 + l % 32 (half 1).  It packs the slot index into them
+// as Search does, takes the two 16-key minima, and one v_permlane32_swap hands
+// each half's minimum to the sample's own lane.  The wave's VALU work per step
+// drops from 15 v_pk_fma (30 keys) to the operand set-up (one swap, four
+// bitwise selects); the 4 MFMAs run on the matrix pipe in two dependent pairs,
+// spread over the kernel's steps (rollout_kernel's mstep).
+// Every lane of the wave must execute issue() and reduce() (full EXEC).
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+
+__device__ __forceinline__ void permlane32_swap(float& a, float& b) {
+    // lanes 32..63 of a trade places with lanes 0..31 of b (probed: tools/mfma_probe.hip)
+    const auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(a), __float_as_uint(b), false, false);
+    a = __uint_as_float(r[0]);
+    b = __uint_as_float(r[1]);
+}
+
+struct SearchMFMA {
+    float a1, a2;            // A operands: (c', ry') and (rx', 0) of slot lane % 32
+    unsigned mlo, mhi, one;  // lane selects: ~0 on lanes 0..31 / 32..63, 1.0f bits on lanes 0..31
+    unsigned hi4;            // 4 on lanes 32..63 (slot offset of the lane's result rows)
+    float cx, cy;
+    float b2_0, b2_1;        // second-stage B operands of the keys in flight
+    f32x16 d0[2], d1[2];     // keys of half 0 / half 1, double-buffered by step parity
+
+    __device__ __forceinline__ void load(const float4* key, float4 ctr, int lane) {
+        const bool hi = lane >= 32;
+        const float4 kk = key[lane & 31];
+        a1 = hi ? kk.y : kk.z;
+        a2 = hi ? 0.f : kk.x;
+        // opaque lane masks: as known selects the compiler would turn them into v_cndmask
+        unsigned m;
+        asm volatile("v_mov_b32 %0, %1" : "=v"(m) : "v"(hi ? 0u : ~0u));
+        mlo = m;
+        mhi = ~m;
+        one = m & 0x3f800000u;
+        hi4 = ~m & 4u;
+        cx = ctr.x;
+        cy = ctr.y;
+    }
+
+    // Stage 1 (after the step's kinematics): B operands of this lane's sample at
+    // (px, py) — the same ax, ay as Search::nearest — and the first MFMA pair,
+    // fma(ay, ry', c') per key.  Selects are bitwise, so a non-finite lane cannot
+    // leak into another sample's keys.
+    template <int P>
+    __device__ __forceinline__ void issue1(float px, float py) {
+        const float ax = -2.f * (px - cx), ay = -2.f * (py - cy);
+        const float b1_1 = __uint_as_float((__float_as_uint(ay) & mhi) | one);
+        b2_0 = __uint_as_float(__float_as_uint(ax) & mlo);
+        float x = ax, y = ay;
+        permlane32_swap(x, y);   // x = [ax 0..31 | ay 0..31], y = [ax 32..63 | ay 32..63]
+        const float b1_0 = __uint_as_float((__float_as_uint(x) & mhi) | one);
+        b2_1 = __uint_as_float(__float_as_uint(y) & mlo);
+        const f32x16 z = {};
+        d0[P] = __builtin_amdgcn_mfma_f32_32x32x2f32(a1, b1_0, z, 0, 0, 0);
+        d1[P] = __builtin_amdgcn_mfma_f32_32x32x2f32(a1, b1_1, z, 0, 0, 0);
+    }
+    // Stage 2 (a stretch of independent work later: in-order issue would stall
+    // on the first pair's result): + ax rx' per key.
+    template <int P>
+    __device__ __forceinline__ void issue2() {
+        d0[P] = __builtin_amdgcn_mfma_f32_32x32x2f32(a2, b2_0, d0[P], 0, 0, 0);
+        d1[P] = __builtin_amdgcn_mfma_f32_32x32x2f32(a2, b2_1, d1[P], 0, 0, 0);
+    }
+
+    __device__ __forceinline__ float pk(float key, int r) const {
+        return __uint_as_float((__float_as_uint(key) & ~31u) | ((unsigned)(8 * (r >> 2) + (r & 3)) + hi4));
+    }
+    __device__ __forceinline__ float min16(const f32x16& d) const {
+        float b = min3_raw(pk(d[0], 0), pk(d[1], 1), pk(d[2], 2));
+#pragma unroll
+        for (int r = 3; r < 15; r += 2) b = min3_raw(b, pk(d[r], r), pk(d[r + 1], r + 1));
+        return min_raw(b, pk(d[15], 15));
+    }
+    // Stage 3: nearest slot of buffer P's keys (same packed argmin as Search::nearest)
+    template <int P>
+    __device__ __forceinline__ unsigned reduce() const {
+        float b0 = min16(d0[P]), b1 = min16(d1[P]);
+        permlane32_swap(b0, b1);   // lane < 32: b1 = half 0's other 16; lane >= 32: b0 = half 1's other 16
+        return __float_as_uint(min_raw(b0, b1)) & 31u;
+    }
+};
+
 // The same search with the window keys in LDS instead of registers: the keys
 // are uniform across the workgroup, so every read is a broadcast ds_read_b128
 // (two per two slots: {rx'0, rx'1, ry'0, ry'1}, {c'0, c'1, -, -}).  Costs one

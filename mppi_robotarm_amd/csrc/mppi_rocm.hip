@@ -180,6 +180,17 @@ constexpr bool kDeferCost = false;
 #else
 constexpr bool kDeferCost = true;
 #endif
+// Window keys from the matrix core (SearchMFMA, LPS = 1 full scan; opt-in
+// MPPI_MFMA_SEARCH builds, bit-identical): measured +14% at K = 65536 T = 64
+// against the VALU scan (dstep).  FP32 MFMA runs at the FP32 vector rate on the
+// same SIMD (MI355X guide: 64 FLOP/clk/SIMD either way), and the 32 x 32 x 2
+// shape computes 2x the needed products (zero K half, padded slots), so the
+// matrix core buys no issue slots here; kept for the record.
+#ifdef MPPI_MFMA_SEARCH
+constexpr bool kMfmaSearch = kDeferCost;
+#else
+constexpr bool kMfmaSearch = false;
+#endif
 
 // POLL: the partial rows travel as tagged granules (see st_gran) to consumer
 // workgroups that poll for them — the first workgroup of each group of kGroup
@@ -238,9 +249,14 @@ __global__ __launch_bounds__(NT) void rollout_kernel(
     // window row for the LDS copy: loaded unconditionally (a load inside the
     // tid < kSlots branch would be waited for right there), stored before the barrier
     const float4 wrow = st->win[tid & (kSlots - 1)];
+    constexpr bool MF = kMfmaSearch && LPS == 1 && !TAB && !kBlockSteps;
     Search<LPS> sr;
+    SearchMFMA ms;
     TabSearch ts;
-    if constexpr (TAB) {
+    if constexpr (MF) {
+        ms.load(st->key, st->ctr, lane);
+        sr.sub = 0;
+    } else if constexpr (TAB) {
         for (int i = tid; i < kTabVec; i += NT) reinterpret_cast<uint4*>(s_tab)[i] = tab[i];
         if (tid < kKeyRows) s_rows[tid] = tid < kSlots ? st->key[tid] : make_float4(0.f, 0.f, kPadKey, 0.f);
         SearchLDS<false>::fill(s_kp, st->key, tid);
@@ -347,6 +363,55 @@ __global__ __launch_bounds__(NT) void rollout_kernel(
         pg = fmaf(ua.z, v1, ua.w * v2);  // (gamma u^T Sigma^-1) v, control.py:106
         pr = s_win[sr.nearest(ppx, ppy)];
     };
+    // MF: a three-stage pipeline over the steps, so that no instruction waits on
+    // the matrix core (issue is in order) and every cost is still added in step
+    // order:  step t:  [first MFMA pair of step t - 1 is done] second pair of
+    // step t - 1 -> dynamics t -> kinematics t, first pair of step t -> cost of
+    // step t - 2 (row looked up during step t - 1) -> reduce step t - 1's keys
+    // and look its row up.  Pending records: q = step t - 1, pp = step t - 2.
+    // Costs are folded after every step = 3 mod 4, as in step() / dstep().
+    float qx1 = 0.f, qy1 = 0.f, qd1 = 0.f, qe1 = 0.f, qg1 = 0.f;
+    // (h1, h2: steps t - 1 / t - 2 exist; compile-time, the first two steps are peeled)
+    auto mstep = [&](int t, auto slot_c, auto h1_c, auto h2_c) {
+        constexpr int slot = decltype(slot_c)::value;
+        constexpr int P = slot & 1, Q = P ^ 1;   // key buffers of steps t and t - 1
+        constexpr bool h1 = decltype(h1_c)::value, h2 = decltype(h2_c)::value;
+        const float2 e = ring[slot];
+        const float4 ua = uring[slot];
+        const int tl = t + kPF < T ? t + kPF : T - 1;
+        ring[slot] = noise_ld(np + (size_t)tl * K);
+        uring[slot] = s_ua[tl];
+        PIN_LOADS();
+        if constexpr (h1) ms.template issue2<Q>();
+        __builtin_amdgcn_sched_barrier(0);
+        const float v1 = fmaf(exf, ua.x, e.x);  // u[t] + eps (exploit) or eps, control.py:99-101
+        const float v2 = fmaf(exf, ua.y, e.y);
+        dyn_step(x, v1, v2, c);
+        const float nx = fmaf(c.fk1, x.c1, c.fk2 * x.c12);  // control.py:178-179
+        const float ny = fmaf(c.fk1, x.s1, c.fk2 * x.s12);
+        ms.template issue1<P>(nx, ny);
+        __builtin_amdgcn_sched_barrier(0);
+        if constexpr (h2) {
+            add_pending();   // step t - 2
+            if (slot == 1) {
+                S += (double)S4;
+                S4 = 0.f;
+            }
+        }
+        if constexpr (h1) {
+            pr = s_win[ms.template reduce<Q>()];   // step t - 1's row
+            ppx = qx1;
+            ppy = qy1;
+            pd1 = qd1;
+            pd2 = qe1;
+            pg = qg1;
+        }
+        qx1 = nx;
+        qy1 = ny;
+        qd1 = x.dq1;
+        qe1 = x.dq2;
+        qg1 = fmaf(ua.z, v1, ua.w * v2);  // (gamma u^T Sigma^-1) v, control.py:106
+    };
     // TAB: the dynamics of steps t..t+n-1 first, then their n window searches
     // together (independent of each other: the lookups' LDS latencies overlap),
     // then the costs in step order (the same fp32 sums as step()).
@@ -409,6 +474,45 @@ __global__ __launch_bounds__(NT) void rollout_kernel(
         if (rem == 1) block(t, I1{});
         else if (rem == 2) block(t, I2{});
         else if (rem == 3) block(t, I3{});
+    } else if constexpr (MF) {
+        STAMP(12, NOW());
+        using BF = std::false_type;
+        using BT = std::true_type;
+        mstep(0, I0{}, BF{}, BF{});
+        if (T > 1) mstep(1, I1{}, BT{}, BF{});
+        for (t = 2; t + kPF <= T; t += kPF) {   // slots 2, 3, 0, 1
+            mstep(t, I2{}, BT{}, BT{});
+            mstep(t + 1, I3{}, BT{}, BT{});
+            mstep(t + 2, I0{}, BT{}, BT{});
+            mstep(t + 3, I1{}, BT{}, BT{});
+#ifdef MPPI_STAMPS
+            if (t == 2) STAMP(13, NOW());
+            if (t + kPF == T / 2 + 2) STAMP(14, NOW());
+#endif
+        }
+        if (t < T) mstep(t, I2{}, BT{}, BT{});          // remainder: t % kPF == 2, 3, 0 in order
+        if (t + 1 < T) mstep(t + 1, I3{}, BT{}, BT{});
+        if (t + 2 < T) mstep(t + 2, I0{}, BT{}, BT{});
+        if (T >= 2) {
+            add_pending();                   // step T - 2
+            if ((T - 2) % kPF == kPF - 1) {
+                S += (double)S4;
+                S4 = 0.f;
+            }
+        }
+        if ((T - 1) & 1) {                   // step T - 1: its second MFMA pair, then its row
+            ms.template issue2<1>();
+            pr = s_win[ms.template reduce<1>()];
+        } else {
+            ms.template issue2<0>();
+            pr = s_win[ms.template reduce<0>()];
+        }
+        ppx = qx1;
+        ppy = qy1;
+        pd1 = qd1;
+        pd2 = qe1;
+        pg = qg1;
+        add_pending();
     } else if constexpr (kDeferCost) {
         STAMP(12, NOW());
         for (; t + kPF <= T; t += kPF) {

@@ -10,6 +10,7 @@ Prints, per build, the median / min per-launch time (HIP events around each
 batch on the launching stream) and each build's ratio to the first.
 """
 import ctypes as C
+import hashlib
 import os
 import sys
 
@@ -57,7 +58,11 @@ def chain_runs(libs, K, T, lam):
         def batch(n, eng=eng, noise=noise):
             for i in range(n):
                 eng.rollout(noise[i % len(noise)], fused_update=True)
-        runs.append((p, batch, eng.close, []))
+        def close(eng=eng, p=p):   # same launch sequence in every build: the nominals must match
+            u = eng.nominal()
+            print(f"    {os.path.basename(p)}: nominal sha1 {hashlib.sha1(u.tobytes()).hexdigest()[:12]}")
+            eng.close()
+        runs.append((p, batch, close, []))
     return runs
 
 
