@@ -432,3 +432,55 @@ def test_fused_dropin_device_noise_loop_equals_host_update(paths):
         recs.append((rec["u"].copy(), rec["q"].copy()))
         rec["controller"].close()
     assert np.array_equal(recs[0][0], recs[1][0]) and np.array_equal(recs[0][1], recs[1][1])
+
+
+@pytest.mark.parametrize("K,T,lam", [(1, 1, 100.0), (2, 2, 100.0), (63, 3, 100.0), (65, 4, 3.0e6), (257, 1, 3.0e6),
+                                     (1000, 5, 100.0)])
+def test_tiny_and_ragged_sizes_against_c_oracle(K, T, lam, paths):
+    """Edge sizes: one sample, one step, K not a multiple of the wave or workgroup (partial waves, idle
+    lanes), the shortest horizons; S and the weighted noise against the C fp64 oracle."""
+    eng = _engine(K, T, param_lambda=lam)
+    win = _window(paths)
+    u = np.array([[10.0, -2.0]] * T) + np.random.default_rng(K + T).normal(0, 0.5, (T, 2))
+    eng.set_step_inputs(X0, win, u)
+    noise = eng.philox_noise(7, 1)
+    S_dev = torch.empty(K, dtype=torch.float64, device="cuda")
+    eng.rollout(noise, S_out=S_dev)
+    w_eps = eng.weighted_noise()
+    S = S_dev.cpu().numpy()
+    eps_tk = noise.cpu().numpy()
+    ref_S = coracle.rollout_costs(X0, u, eps_tk, win, 0.006, lam, 0.98, np.eye(2) * 20.0,
+                                  RUNPY["stage_cost_weight"], RUNPY["terminal_cost_weight"], O.ArmParams(),
+                                  layout="TK")
+    assert float(np.max(np.abs(S - ref_S) / np.abs(ref_S))) < S_TOL
+    assert int(np.argmin(S)) == int(np.argmin(ref_S))
+    _, ref_weps = coracle.weighted_noise(ref_S, eps_tk, lam, layout="TK")
+    assert _urel(w_eps, ref_weps) < U_TOL
+    eng.close()
+
+
+@pytest.mark.parametrize("K,T", [(1, 1), (5, 2), (64, 3), (100, 4), (130, 5)])
+def test_dropin_short_horizons_match_oracle_controller(K, T, paths):
+    """The drop-in at horizons below the median window (T < 5: host update through SciPy's reflect
+    padding; T = 5: the fused device update) against the fp64 oracle controller, three closed-loop ticks
+    on the same NumPy noise, including the aliasing of the returns."""
+    from mppi_robotarm_amd.controller import MPPIControllerForPathTracking
+    kw = dict(delta_t=0.006, ref_path=paths["xydq_circle"], horizon_step_T=T, number_of_samples_K=K,
+              visualize_optimal_traj=True, **RUNPY)
+    c = MPPIControllerForPathTracking(verbose=False, **kw)
+    o = O.OracleController(**kw)
+    x = X0.copy()
+    rng = np.random.default_rng(K * 10 + T)
+    for tick in range(3):
+        eps = rng.multivariate_normal(np.zeros(2), RUNPY["sigma"], (K, T)).astype(np.float32).astype(np.float64)
+        c._calc_epsilon = lambda *a, e=eps, **k: e
+        u_prev = c.u_prev
+        u0, u_seq, opt, _ = c.calc_control_input(x)
+        r0, r_seq, r_opt, _ = o.calc_control_input(x, epsilon=eps)
+        assert _urel(u_seq, r_seq) < U_TOL, tick
+        assert _urel(np.asarray(u0), np.asarray(r0)) < U_TOL, tick
+        assert u_seq is u_prev and np.shares_memory(u0, u_prev)
+        assert c.prev_waypoints_idx == o.prev_waypoints_idx
+        np.testing.assert_allclose(opt, r_opt, rtol=1e-4, atol=1e-4)
+        x = r_opt[-1].copy()
+    c.close()
