@@ -45,7 +45,10 @@ constexpr int kGroup = 16;             // workgroups per first-level merge group
 // (which has s = 1 and eta >= 1): far below the fp64 resolution of the result.
 constexpr double kMergeFloor = 5.421010862427522e-20;  // 2^-64
 constexpr int kDirectRows = 256;       // workgroup rows the direct merge scans (4 per lane)
-constexpr int kDirectMax = 16;         // weighted rows it merges; more go through the group rows
+#ifndef MPPI_DIRECT_MAX
+#define MPPI_DIRECT_MAX 16
+#endif
+constexpr int kDirectMax = MPPI_DIRECT_MAX;  // weighted rows it merges; more go through the group rows
 constexpr int kSparseMax = 16;         // weighted samples per workgroup handled by the epilogue gather
 
 // ------------------------------------------------------------------ helpers
