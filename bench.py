@@ -120,10 +120,35 @@ def cpu_baseline(args, window, x0, u):
         el = time.perf_counter() - t0
         if el >= args.cpu_seconds:
             break
-    return {"value": K * T * n / el, "unit": "state-steps/s", "cores": coracle.max_threads(),
-            "kind": "port",
-            "sample": f"{n} full steps of K={K} T={T} (rollout+cost+softmin+weighted noise), "
-                      f"C fp64 restatement oracle/mppi_oracle.c, OpenMP, {el:.1f} s"}
+    out = {"value": K * T * n / el, "unit": "state-steps/s", "cores": coracle.max_threads(),
+           "kind": "port",
+           "sample": f"{n} full steps of K={K} T={T} (rollout+cost+softmin+weighted noise), "
+                     f"C fp64 restatement oracle/mppi_oracle.c, OpenMP, {el:.1f} s",
+           "os_cpu_count": os.cpu_count(), "OMP_NUM_THREADS": os.environ.get("OMP_NUM_THREADS")}
+    out["numpy_fp64_1thread"] = numpy_baseline(eps, window, x0, u, lam, max(1.0, args.cpu_seconds / 4))
+    return out
+
+
+def numpy_baseline(eps, window, x0, u, lam, seconds):
+    """the vectorised fp64 NumPy restatement (oracle/mppi_oracle.py), one thread, on the first
+    4096 samples of the same workload (whole steps: rollout + cost + weights + weighted noise)."""
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import mppi_oracle as O  # checker / baseline only
+    sub = np.ascontiguousarray(eps[:4096])
+    Ks, T = sub.shape[0], sub.shape[1]
+    t0 = time.perf_counter()
+    n = 0
+    while True:
+        S = O.rollout_costs(x0, u, sub, window, 0, 0.006, lam, 0.98, np.eye(2) * 20.0,
+                            np.array([0.5, 0.5, 5.0, 5.0]), np.array([5.0, 5.0, 50.0, 50.0]))
+        O.weighted_noise(O.compute_weights(S, lam), sub)
+        n += 1
+        el = time.perf_counter() - t0
+        if el >= seconds:
+            break
+    return {"value": Ks * T * n / el, "unit": "state-steps/s", "cores": 1,
+            "sample": f"{n} full steps of K={Ks} T={T} (first {Ks} samples of the workload), "
+                      f"oracle/mppi_oracle.py NumPy fp64, {el:.1f} s"}
 
 
 def cpu_baseline_c5(args, window, x0, u, K, T):

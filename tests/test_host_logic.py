@@ -164,3 +164,12 @@ def test_bench_valu_roofline_from_committed_counters():
                                           / (kern_ms * 1e-3 * bench.CLOCK_HZ))
         assert ("frac_one_wave_ceiling" in v) == (wps == 1.0)
     assert bench.valu_roofline({}, 0.03) is None
+
+
+def test_bench_numpy_baseline_runs(paths):
+    """bench.py's single-thread NumPy fp64 baseline on a tiny sample."""
+    import bench
+    eps = (np.random.default_rng(0).standard_normal((64, 4, 2)) * math.sqrt(20.0)).astype(np.float32)
+    out = bench.numpy_baseline(eps, paths["xydq_circle"][:30], np.array([1.15, -1.27, 0.0, 0.0]),
+                               np.array([[10.0, -2.0]] * 4), 100.0, 0.0)
+    assert out["value"] > 0 and out["cores"] == 1 and "K=64 T=4" in out["sample"]
