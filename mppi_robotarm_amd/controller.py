@@ -213,7 +213,6 @@ class MPPIControllerForPathTracking:
         tr = None
         if self.visualze_sampled_trajs:
             tr = eng.trajectories(base_u=u_before, noise=self._noise_dev)   # pre-update u, v[k, t-1]
-        self._prefetch_noise(eng)
         u_new, traj_host = eng.step_outputs(traj)
         if self.keep_costs:
             self.last_S = self._S_dev.cpu().numpy()
@@ -226,6 +225,9 @@ class MPPIControllerForPathTracking:
                     sampled_traj_list[off:off + arr.shape[0]] = arr
             else:
                 sampled_traj_list[:] = tr.double().cpu().numpy()
+        # next step's noise after the last read-back: the draw overlaps the caller's
+        # work between ticks instead of sitting in front of this call's synchronise
+        self._prefetch_noise(eng)
         u[:] = u_new                                       # the shifted nominal, in place (aliasing kept)
         optimal_traj = traj_host.astype(np.float64) if traj is not None else np.zeros((self.T, self.dim_x))
         return u[0], u, optimal_traj, sampled_traj_list

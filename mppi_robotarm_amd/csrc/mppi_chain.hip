@@ -641,10 +641,10 @@ __global__ __launch_bounds__(kCT) void chain_traj_kernel(const ChainConst c, con
 __global__ __launch_bounds__(kCT) void chain_philox_kernel(int K_local, int T, int n, long long k_offset,
                                                            unsigned long long seed, unsigned long long step,
                                                            const float* __restrict__ Lch, float* __restrict__ out) {
-    const long long idx = (long long)blockIdx.x * kCT + threadIdx.x;
-    if (idx >= (long long)K_local * T) return;
-    const int k = (int)(idx % K_local);
-    const int t = (int)(idx / K_local);
+    // grid (ceil(K_local / kCT), T): no 64-bit divide per thread
+    const int k = (int)blockIdx.x * kCT + (int)threadIdx.x;
+    if (k >= K_local) return;
+    const int t = (int)blockIdx.y;
     const unsigned long long kg = (unsigned long long)(k_offset + k);
     const uint2 key = make_uint2((unsigned)seed, (unsigned)(seed >> 32) ^ (unsigned)(step >> 32));
     float z[kCMax];
@@ -1109,9 +1109,8 @@ int mppi_chain_rollout_traj(mppi_chain_ctx* c, const double* base_u, const float
 
 int mppi_chain_noise_philox(mppi_chain_ctx* c, unsigned long long seed, unsigned long long step, float* out_dev) {
     if (!c || !out_dev) return fail(MPPI_E_ARG, "null argument");
-    const long long nth = (long long)c->cfg.K_local * c->cfg.T;
-    const int blocks = (int)((nth + kCT - 1) / kCT);
-    hipLaunchKernelGGL(chain_philox_kernel, dim3(blocks), dim3(kCT), 0, c->stream, c->cfg.K_local, c->cfg.T, c->n,
+    const dim3 grid((unsigned)((c->cfg.K_local + kCT - 1) / kCT), (unsigned)c->cfg.T);
+    hipLaunchKernelGGL(chain_philox_kernel, grid, dim3(kCT), 0, c->stream, c->cfg.K_local, c->cfg.T, c->n,
                        (long long)c->cfg.k_offset, seed, step, c->d_chol, out_dev);
     const hipError_t e = hipGetLastError();
     if (e != hipSuccess) return fail(MPPI_E_HIP, std::string("chain_philox_kernel: ") + hipGetErrorString(e));

@@ -805,15 +805,15 @@ __global__ __launch_bounds__(256) void search_check_kernel(const DevStep* __rest
 }
 
 // Philox4x32-10 + Box-Muller (mppi_device.h); eps = L z, L = chol(Sigma).
+// Grid (ceil(K_local / kThreads), ceil(T / 2)): blockIdx.y is the step pair, so
+// no 64-bit divide per thread (it was ~half the kernel's instructions).
 __global__ __launch_bounds__(kThreads) void philox_noise_kernel(int K_local, int T, long long k_offset,
                                                                 unsigned long long seed,
                                                                 unsigned long long step, float L00,
                                                                 float L10, float L11, float2* out) {
-    const long long idx = (long long)blockIdx.x * kThreads + threadIdx.x;
-    const int tp = (T + 1) / 2;
-    if (idx >= (long long)K_local * tp) return;
-    const int k = (int)(idx % K_local);
-    const int t0 = 2 * (int)(idx / K_local);
+    const int k = (int)blockIdx.x * kThreads + (int)threadIdx.x;
+    if (k >= K_local) return;
+    const int t0 = 2 * (int)blockIdx.y;
     const unsigned long long kg = (unsigned long long)(k_offset + k);
     const uint4 ctr = make_uint4((unsigned)kg, (unsigned)(kg >> 32), (unsigned)t0, (unsigned)step);
     const uint2 key = make_uint2((unsigned)seed, (unsigned)(seed >> 32) ^ (unsigned)(step >> 32));
@@ -1340,9 +1340,8 @@ int mppi_noise_philox(mppi_ctx* c, unsigned long long seed, unsigned long long s
     const double L00 = sqrt(S[0]), L10 = s01 / L00, d = S[3] - L10 * L10;
     if (!(d >= 0.0)) return fail(MPPI_E_ARG, "Sigma not positive semi-definite");
     const double L11 = sqrt(d);
-    const long long n = (long long)c->cfg.K_local * ((c->cfg.T + 1) / 2);
-    const int blocks = (int)((n + kThreads - 1) / kThreads);
-    hipLaunchKernelGGL(philox_noise_kernel, dim3(blocks), dim3(kThreads), 0, c->stream, c->cfg.K_local,
+    const dim3 grid((unsigned)((c->cfg.K_local + kThreads - 1) / kThreads), (unsigned)((c->cfg.T + 1) / 2));
+    hipLaunchKernelGGL(philox_noise_kernel, grid, dim3(kThreads), 0, c->stream, c->cfg.K_local,
                        c->cfg.T, (long long)c->cfg.k_offset, seed, step, (float)L00, (float)L10, (float)L11,
                        reinterpret_cast<float2*>(out_dev));
     return launch_check("philox_noise_kernel");
