@@ -169,13 +169,13 @@ int mppi_sync(mppi_ctx *ctx);
  * timeline (16 uint64 per workgroup) to dbg_dev; product builds ignore it. */
 int mppi_debug_set_buffer(mppi_ctx *ctx, void *dbg_dev);
 
-/* Tests: the nearest window slot of n end-effector points pts_dev[n][2] (fp32
- * device), once through the window-search candidate table and once by the full
- * 30-slot scan, into out_dev[n][2] (int32 device).  The two must agree bit for
- * bit (control.py:200-232 as the device evaluates it).  The table is opt-in:
- * MPPI_SEARCH=table in the environment at mppi_ctx_create (lanes_per_sample 1);
- * MPPI_E_ARG otherwise. */
-int mppi_debug_search(mppi_ctx *ctx, const float *pts_dev, int n, int *out_dev);
+/* Tests: the nearest window slot of the first K samples at every step, as the
+ * rollout evaluates it (_get_nearest_waypoint inside _c, control.py:176-180 and
+ * :205-215): the same fp32 dynamics and packed argmin on the current step
+ * inputs and noise_dev ([T][K_local][2] fp32).  slot_dev[K][T] (int32 device)
+ * receives the window slot (0-based, relative to prev_waypoints_idx) and
+ * pos_dev[K][T][2] (fp32 device) the end-effector position it was searched for. */
+int mppi_debug_nearest(mppi_ctx *ctx, const float *noise_dev, int K, int *slot_dev, float *pos_dev);
 
 /* ------------------------------------------------------------------------
  * n-link planar chain (BASELINE config 5: "7-DoF arm dynamics (extended

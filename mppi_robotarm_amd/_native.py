@@ -30,7 +30,7 @@ EXPORTS = (
     "mppi_get_weighted_noise",
     "mppi_get_nominal", "mppi_rollout_traj", "mppi_optimal_traj", "mppi_get_step_outputs", "mppi_noise_philox",
     "mppi_sync", "mppi_debug_set_buffer",
-    "mppi_debug_search",
+    "mppi_debug_nearest",
     "mppi_chain_ctx_create", "mppi_chain_ctx_destroy", "mppi_chain_set_stream", "mppi_chain_ctx_info",
     "mppi_chain_set_step_inputs", "mppi_chain_rollout", "mppi_chain_merge_partials", "mppi_chain_exchange_handle",
     "mppi_chain_exchange_attach",
@@ -105,7 +105,7 @@ def open_library(path: str):
         "mppi_noise_philox": ([vp, C.c_ulonglong, C.c_ulonglong, fp], C.c_int),
         "mppi_sync": ([vp], C.c_int),
         "mppi_debug_set_buffer": ([vp, vp], C.c_int),
-        "mppi_debug_search": ([vp, fp, C.c_int, fp], C.c_int),
+        "mppi_debug_nearest": ([vp, fp, C.c_int, vp, fp], C.c_int),
         "mppi_chain_ctx_create": ([C.POINTER(ChainConfigC), C.c_int, vp, C.POINTER(vp)], C.c_int),
         "mppi_chain_ctx_destroy": ([vp], None),
         "mppi_chain_set_stream": ([vp, vp], C.c_int),

@@ -148,8 +148,10 @@ class ChainEngine:
             pass
 
     def _sync_stream(self):
+        """Follow torch's current stream; the new stream first waits for the old one."""
         s = torch.cuda.current_stream(self.device)
         if s.cuda_stream != self.stream.cuda_stream:
+            s.wait_stream(self.stream)
             self.stream = s
             N.check(self._lib.mppi_chain_set_stream(self._ctx, C.c_void_p(s.cuda_stream)), "mppi_chain_set_stream")
 

@@ -102,6 +102,7 @@ class MPPIControllerForPathTracking:
         self._engine = None
         self._step_count = 0
         self._noise_ready = None       # (seed, step) of the device noise already in the buffer
+        self._engine_built_for = None  # _engine_key() of the live engine
         self.host_update = bool(host_update) or self.T < 5   # the device median needs T >= 5
         self.keep_costs = False        # set True to keep per-sample S (self.last_S)
         self.last_S = None
@@ -113,15 +114,33 @@ class MPPIControllerForPathTracking:
         import torch.distributed as dist
         return dist.get_world_size(self.process_group), dist.get_rank(self.process_group)
 
+    def _engine_key(self):
+        """Everything the engine bakes in at creation that the reference reads on
+        every call (Sigma at control.py:84,106; lambda :112; gamma :106; the cost
+        weights :185,198; the exploration split :98; delta_t :256-259)."""
+        return (np.asarray(self.Sigma, dtype=np.float64).tobytes(), float(self.param_lambda),
+                float(self.param_gamma), np.asarray(self.stage_cost_weight, dtype=np.float64).tobytes(),
+                np.asarray(self.terminal_cost_weight, dtype=np.float64).tobytes(), float(self.param_exploration),
+                float(self.delta_t))
+
     def _get_engine(self) -> RolloutEngine:
+        key = self._engine_key()
+        if self._engine is not None and key != self._engine_built_for:
+            self.close()             # an attribute the engine baked in changed: rebuild, as the reference re-reads it
         if self._engine is None:
             world, rank = self._shard()
             K_local, k_offset = shard_geometry(self.K, world, rank)
             device = self._device if self._device is not None else torch.cuda.current_device()
+            # gamma is fixed at construction in the reference (control.py:45) while lambda is
+            # re-read per call; the engine takes (lambda, alpha), so carry gamma through alpha
+            alpha = self.param_alpha
+            if self.param_lambda * (1.0 - alpha) != self.param_gamma and self.param_lambda != 0:
+                alpha = 1.0 - self.param_gamma / self.param_lambda
             self._engine = RolloutEngine(
-                K_local, self.T, self.delta_t, self.param_lambda, self.param_alpha, self.Sigma,
+                K_local, self.T, self.delta_t, self.param_lambda, alpha, self.Sigma,
                 self.stage_cost_weight, self.terminal_cost_weight, self.param_exploration, self.arm,
                 K_total=self.K, k_offset=k_offset, device=device, lanes_per_sample=self._lanes_per_sample)
+            self._engine_built_for = key
             self._noise_dev = self._engine.new_noise()
             self._partial = self._engine.new_partial()
             self._S_dev = torch.empty(K_local, dtype=torch.float64, device=self._engine.device)
@@ -287,3 +306,5 @@ class MPPIControllerForPathTracking:
         if self._engine is not None:
             self._engine.close()
             self._engine = None
+        self._noise_ready = None       # the next engine's noise buffer is fresh: draw again
+        self._engine_built_for = None

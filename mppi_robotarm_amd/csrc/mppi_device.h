@@ -245,100 +245,6 @@ struct Search {
     }
 };
 
-// The same search (LPS = 1) with the keys of a whole wave from the matrix core.
-// The 32 slots x 64 samples of keys are a product  [c' ry' rx' 0] x [1 ay ax 0]^T,
-// two chained v_mfma_f32_32x32x2_f32 per half-wave of samples:
-//   D = mfma(A2 = (rx', 0), B2 = (ax, 0), mfma(A1 = (c', ry'), B1 = (1, ay), 0)),
-// which is bit-identical to Search's fma(ax, rx', fma(ay, ry', c')) (each MFMA
-// rounds its 2-term dot product plus accumulator once; c' * 1 and 0 * b are
-// exact; checked on 8.4 M keys by tools/mfma_probe.hip, and end to end by the
-// parity tests).  Operand lane l holds A[i = l % 32][k = l / 32] and
-// B[k = l / 32][j = l % 32]; result register r of lane l is D[slot][j] with
-//   slot = 8 (r / 4) + 4 (l / 32) + r % 4,   j = l % 32,
-// so each lane ends with 16 of the 32 keys of one sample of each half: sample
-// l % 32 (half 0) and 32 + l % 32 (half 1).  It packs the slot index into them
-// as Search does, takes the two 16-key minima, and one v_permlane32_swap hands
-// each half's minimum to the sample's own lane.  The wave's VALU work per step
-// drops from 15 v_pk_fma (30 keys) to the operand set-up (one swap, four
-// bitwise selects); the 4 MFMAs run on the matrix pipe in two dependent pairs,
-// spread over the kernel's steps (rollout_kernel's mstep).
-// Every lane of the wave must execute issue() and reduce() (full EXEC).
-typedef float f32x16 __attribute__((ext_vector_type(16)));
-
-__device__ __forceinline__ void permlane32_swap(float& a, float& b) {
-    // lanes 32..63 of a trade places with lanes 0..31 of b (probed: tools/mfma_probe.hip)
-    const auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(a), __float_as_uint(b), false, false);
-    a = __uint_as_float(r[0]);
-    b = __uint_as_float(r[1]);
-}
-
-struct SearchMFMA {
-    float a1, a2;            // A operands: (c', ry') and (rx', 0) of slot lane % 32
-    unsigned mlo, mhi, one;  // lane selects: ~0 on lanes 0..31 / 32..63, 1.0f bits on lanes 0..31
-    unsigned hi4;            // 4 on lanes 32..63 (slot offset of the lane's result rows)
-    float cx, cy;
-    float b2_0, b2_1;        // second-stage B operands of the keys in flight
-    f32x16 d0[2], d1[2];     // keys of half 0 / half 1, double-buffered by step parity
-
-    __device__ __forceinline__ void load(const float4* key, float4 ctr, int lane) {
-        const bool hi = lane >= 32;
-        const float4 kk = key[lane & 31];
-        a1 = hi ? kk.y : kk.z;
-        a2 = hi ? 0.f : kk.x;
-        // opaque lane masks: as known selects the compiler would turn them into v_cndmask
-        unsigned m;
-        asm volatile("v_mov_b32 %0, %1" : "=v"(m) : "v"(hi ? 0u : ~0u));
-        mlo = m;
-        mhi = ~m;
-        one = m & 0x3f800000u;
-        hi4 = ~m & 4u;
-        cx = ctr.x;
-        cy = ctr.y;
-    }
-
-    // Stage 1 (after the step's kinematics): B operands of this lane's sample at
-    // (px, py) — the same ax, ay as Search::nearest — and the first MFMA pair,
-    // fma(ay, ry', c') per key.  Selects are bitwise, so a non-finite lane cannot
-    // leak into another sample's keys.
-    template <int P>
-    __device__ __forceinline__ void issue1(float px, float py) {
-        const float ax = -2.f * (px - cx), ay = -2.f * (py - cy);
-        const float b1_1 = __uint_as_float((__float_as_uint(ay) & mhi) | one);
-        b2_0 = __uint_as_float(__float_as_uint(ax) & mlo);
-        float x = ax, y = ay;
-        permlane32_swap(x, y);   // x = [ax 0..31 | ay 0..31], y = [ax 32..63 | ay 32..63]
-        const float b1_0 = __uint_as_float((__float_as_uint(x) & mhi) | one);
-        b2_1 = __uint_as_float(__float_as_uint(y) & mlo);
-        const f32x16 z = {};
-        d0[P] = __builtin_amdgcn_mfma_f32_32x32x2f32(a1, b1_0, z, 0, 0, 0);
-        d1[P] = __builtin_amdgcn_mfma_f32_32x32x2f32(a1, b1_1, z, 0, 0, 0);
-    }
-    // Stage 2 (a stretch of independent work later: in-order issue would stall
-    // on the first pair's result): + ax rx' per key.
-    template <int P>
-    __device__ __forceinline__ void issue2() {
-        d0[P] = __builtin_amdgcn_mfma_f32_32x32x2f32(a2, b2_0, d0[P], 0, 0, 0);
-        d1[P] = __builtin_amdgcn_mfma_f32_32x32x2f32(a2, b2_1, d1[P], 0, 0, 0);
-    }
-
-    __device__ __forceinline__ float pk(float key, int r) const {
-        return __uint_as_float((__float_as_uint(key) & ~31u) | ((unsigned)(8 * (r >> 2) + (r & 3)) + hi4));
-    }
-    __device__ __forceinline__ float min16(const f32x16& d) const {
-        float b = min3_raw(pk(d[0], 0), pk(d[1], 1), pk(d[2], 2));
-#pragma unroll
-        for (int r = 3; r < 15; r += 2) b = min3_raw(b, pk(d[r], r), pk(d[r + 1], r + 1));
-        return min_raw(b, pk(d[15], 15));
-    }
-    // Stage 3: nearest slot of buffer P's keys (same packed argmin as Search::nearest)
-    template <int P>
-    __device__ __forceinline__ unsigned reduce() const {
-        float b0 = min16(d0[P]), b1 = min16(d1[P]);
-        permlane32_swap(b0, b1);   // lane < 32: b1 = half 0's other 16; lane >= 32: b0 = half 1's other 16
-        return __float_as_uint(min_raw(b0, b1)) & 31u;
-    }
-};
-
 // The same search with the window keys in LDS instead of registers: the keys
 // are uniform across the workgroup, so every read is a broadcast ds_read_b128
 // (two per two slots: {rx'0, rx'1, ry'0, ry'1}, {c'0, c'1, -, -}).  Costs one
@@ -384,202 +290,6 @@ struct SearchLDS {
             best = min3_raw(best, k0, k1);
         }
         return __float_as_uint(best) & 31u;
-    }
-};
-
-// ----------------------------------------------- window search: candidate table
-//
-// The window is the same for every sample and step of a launch, so its
-// nearest-waypoint map can be tabulated once per window and the 30-slot scan
-// replaced by a lookup.  Cells are polar around the window centre: a diamond
-// angle a in [0, 4) (monotone in the polar angle, no atan2) by
-// sigma = 1 / |p'| (uniform in sigma: the key differences scale with |p'|, so
-// this keeps the cells' resolution matched to them).  With
-//   f_j(p') = key_j / |p'| = sigma c'_j - 2 u.r'_j,        u = p' / |p'|,
-// slot j can be the (packed, fp32) argmin somewhere in a cell only if for
-// every slot i the minimum over the cell of f_j - f_i = sigma A - 2 u.B
-// (A = c'_j - c'_i, B = r'_j - r'_i) is at most the fp32 margin; that minimum
-// is separable — linear in sigma (ends of the sigma interval) plus
-// -2 max_u u.B over the angle interval (|B| if B's direction lies inside,
-// else the better end) — so the test is exact arithmetic on the cell bounds.
-// Each cell stores the smallest candidate lo and the candidate span:
-//   byte = lo | (min(span, 8) - 1) << 5       (0xFF: search everything)
-// The kernel takes lo directly when every lane of the wave has span 1, scans
-// lo..lo+3 when every span is <= 4, and the whole window otherwise.  The set
-// of candidates always contains the full scan's packed argmin (the margin
-// covers the fp32 evaluation of the keys and the 5-bit index packing with a
-// 16x factor; the cells are widened by guard bands covering the fp32 cell
-// index), so the result is bit-identical to Search / SearchLDS.
-//
-// The sigma bins cover [0, sigma_max) with sigma_max = 2 / R_w (R_w the largest
-// |r'_j|; set by the host as sscale = kTabSig / sigma_max).  Points closer than
-// R_w / 2 to the centre fall into the sentinel row: the near field, where every
-// slot is a candidate.
-constexpr int kTabPhi = 256;                       // diamond-angle bins
-constexpr int kTabSig = 32;                        // sigma bins
-constexpr int kTabBytes = kTabPhi * (kTabSig + 1); // + sentinel row
-constexpr int kTabVec = kTabBytes / 16;            // uint4 words
-constexpr int kKeyRows = kSlots + 4;               // key rows for lo..lo+3 (pads past the window)
-static_assert(kTabBytes % 16 == 0, "table is copied as uint4");
-constexpr double kTabGuardA = 4.0e-6;   // diamond-angle guard band (fp32 a error < 5e-7)
-constexpr double kTabGuardS = 1.0e-5;   // relative sigma guard band (fp32 sigma * scale < 2^-21)
-
-__device__ __forceinline__ unsigned cvt_u32_sat(float x) {
-    // v_cvt_u32_f32 saturates (negative and NaN -> 0, large -> 0xFFFFFFFF)
-    unsigned r;
-    asm("v_cvt_u32_f32 %0, %1" : "=v"(r) : "v"(x));
-    return r;
-}
-
-// Cell of the centred point (dx, dy) (pp = dx^2 + dy^2): a row-major index
-// sigma_bin * kTabPhi + angle_bin into the table, always in range.
-__device__ __forceinline__ unsigned tab_cell(float dx, float dy, float pp, float sscale) {
-    const float s = fabsf(dx) + fabsf(dy);
-    const float q = dx * __builtin_amdgcn_rcpf(s);
-    const float sg = __builtin_copysignf(1.f, dy);
-    const float a = fmaf(-q, sg, 2.f - sg);  // dy >= 0: 1 - q, dy < 0: 3 + q
-    const unsigned ab = min(cvt_u32_sat(a * (kTabPhi / 4.f)), (unsigned)(kTabPhi - 1));
-    const unsigned sb = min(cvt_u32_sat(__builtin_amdgcn_rsqf(pp) * sscale), (unsigned)kTabSig);
-    return sb * kTabPhi + ab;
-}
-
-// Direction of diamond angle a (any real; taken mod 4), normalised, fp64.
-__device__ inline void diamond_dir(double a, double* ux, double* uy) {
-    a -= 4.0 * floor(a * 0.25);
-    const double q = floor(a), f = a - q;
-    double x, y;
-    if (q < 1.0) { x = 1.0 - f; y = f; }
-    else if (q < 2.0) { x = -f; y = 1.0 - f; }
-    else if (q < 3.0) { x = f - 1.0; y = -f; }
-    else { x = f; y = f - 1.0; }
-    const double n = 1.0 / sqrt(x * x + y * y);
-    *ux = x * n;
-    *uy = y * n;
-}
-
-// Table builder: one thread per (cell, slot j), 32 threads per cell; keys are
-// the launch's fp32 centred keys (rx', ry', c', -) as float4, W real slots,
-// sscale = kTabSig / sigma_max as the kernels read it.  fp64 throughout.
-__device__ inline void build_tab_cell(const float4* __restrict__ key, int W, float sscale,
-                                      unsigned char* __restrict__ tab) {
-    const int gid = blockIdx.x * blockDim.x + threadIdx.x;
-    const int cell = gid >> 5, j = gid & 31;
-    const int ab = cell % kTabPhi, sb = cell / kTabPhi;
-    bool cand;
-    if (cell >= kTabBytes) {
-        cand = false;
-    } else if (sb >= kTabSig || !(sscale > 0.f)) {
-        cand = j < W;  // near field (or a degenerate window): everything
-    } else if (j >= W) {
-        cand = false;
-    } else {
-        double R2 = 0.0;
-        for (int i = 0; i < W; ++i) R2 = fmax(R2, (double)key[i].z);
-        const double sc = (double)sscale;
-        const double s0 = sb == 0 ? 0.0 : (double)sb / sc * (1.0 - kTabGuardS);
-        const double s1 = (double)(sb + 1) / sc * (1.0 + kTabGuardS);
-        double u0x, u0y, u1x, u1y;
-        diamond_dir(ab * (4.0 / kTabPhi) - kTabGuardA, &u0x, &u0y);
-        diamond_dir((ab + 1) * (4.0 / kTabPhi) + kTabGuardA, &u1x, &u1y);
-        // fp32 key error <= 2^-17 (c' + 2|p'| R) per key, 2^-16 per difference;
-        // in f units (x sigma) <= 2^-16 (sigma R^2 + 2R): the margin is 16x that
-        const double margin = 0x1p-12 * (s1 * R2 + 2.0 * sqrt(R2));
-        const float4 kj = key[j];
-        cand = true;
-        for (int i = 0; i < W; ++i) {
-            if (i == j) continue;
-            const float4 ki = key[i];
-            const double A = (double)kj.z - (double)ki.z;
-            const double Bx = (double)kj.x - (double)ki.x, By = (double)kj.y - (double)ki.y;
-            const double smin = fmin(s0 * A, s1 * A);
-            const bool inside = (u0x * By - u0y * Bx >= 0.0) && (Bx * u1y - By * u1x >= 0.0);
-            const double hmax = inside ? sqrt(Bx * Bx + By * By) : fmax(u0x * Bx + u0y * By, u1x * Bx + u1y * By);
-            if (smin - 2.0 * hmax > margin) {  // NaN keeps j a candidate
-                cand = false;
-                break;
-            }
-        }
-    }
-    const unsigned long long m = __ballot(cand);
-    if (j == 0 && cell < kTabBytes) {
-        const unsigned half = (unsigned)(m >> (threadIdx.x & 32));
-        unsigned char b = 0xFF;
-        if (half != 0u && sb < kTabSig) {
-            const int lo = __builtin_ctz(half), hi = 31 - __builtin_clz(half);
-            const int span = min(hi - lo + 1, 8);
-            b = (unsigned char)(lo | (span - 1) << 5);
-        }
-        tab[cell] = b;
-    }
-}
-
-// Window search through the candidate table (LPS = 1).  tab: the table in LDS;
-// rows: kKeyRows key rows (rx', ry', c', -), pads c' = 1e30; kp: the key pairs
-// of SearchLDS for the whole-window fallback.  nearest<n>() resolves n steps'
-// positions together so the LDS latencies overlap.
-struct TabSearch {
-    const unsigned char* tab;
-    const float4* rows;
-    const KeyPair* kp;
-    float cx, cy, sscale;
-
-    __device__ __forceinline__ unsigned cell_code(float dx, float dy) const {
-        const float pp = fmaf(dx, dx, dy * dy);
-        return tab[tab_cell(dx, dy, pp, sscale)];
-    }
-    // slots lo..lo+3 (lo = code & 31); every lane's candidates lie inside
-    __device__ __forceinline__ unsigned scan4(float dx, float dy, unsigned code) const {
-        const float ax = -2.f * dx, ay = -2.f * dy;
-        const unsigned lo = code & 31u;
-        float best = 3.0e38f;
-#pragma unroll
-        for (int i = 0; i < 4; ++i) {
-            const unsigned jj = min(lo + (unsigned)i, (unsigned)(kSlots - 1));  // slot 31 is a pad
-            const float4 r = rows[jj];
-            const float key = fmaf(ax, r.x, fmaf(ay, r.y, r.z));
-            best = min_raw(best, __uint_as_float((__float_as_uint(key) & ~31u) | jj));
-        }
-        return __float_as_uint(best) & 31u;
-    }
-    __device__ __forceinline__ unsigned scan_all(float dx, float dy) const {
-        const float ax = -2.f * dx, ay = -2.f * dy;
-        const f32x2 ax2 = {ax, ax}, ay2 = {ay, ay};
-        float best = 3.0e38f;
-        constexpr int SP = (MPPI_SEARCH_LEN + 1) / 2;
-#pragma unroll
-        for (int i = 0; i < SP; ++i) {
-            const float4 xy = kp[i].xy, cc = kp[i].c;
-            const f32x2 key = __builtin_elementwise_fma(ax2, f32x2{xy.x, xy.y},
-                                                        __builtin_elementwise_fma(ay2, f32x2{xy.z, xy.w}, f32x2{cc.x, cc.y}));
-            const unsigned j = (unsigned)(2 * i);
-            const float k0 = __uint_as_float((__float_as_uint(key.x) & ~31u) | j);
-            const float k1 = __uint_as_float((__float_as_uint(key.y) & ~31u) | (j + 1));
-            best = min3_raw(best, k0, k1);
-        }
-        return __float_as_uint(best) & 31u;
-    }
-    __device__ __forceinline__ unsigned resolve(float dx, float dy, unsigned code) const {
-        if (__all(code < 128u)) return scan4(dx, dy, code);
-        return scan_all(dx, dy);
-    }
-    template <int n>
-    __device__ __forceinline__ void nearest(const float* px, const float* py, unsigned* j) const {
-        float dx[n], dy[n];
-        unsigned code[n], any = 0u;
-#pragma unroll
-        for (int s = 0; s < n; ++s) {
-            dx[s] = px[s] - cx;
-            dy[s] = py[s] - cy;
-            code[s] = cell_code(dx[s], dy[s]);
-            any |= code[s];
-        }
-        if (__all(any < 32u)) {  // every lane, every step: a single candidate
-#pragma unroll
-            for (int s = 0; s < n; ++s) j[s] = code[s];
-            return;
-        }
-#pragma unroll
-        for (int s = 0; s < n; ++s) j[s] = resolve(dx[s], dy[s], code[s]);
     }
 };
 

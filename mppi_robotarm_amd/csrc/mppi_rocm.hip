@@ -51,7 +51,7 @@ struct alignas(16) DevStep {
     float4 win[kSlots];   // rx, ry, rdq1, rdq2 of window slot j (lookup after argmin)
     float4 key[kSlots];   // rx', ry', c' = rx'^2 + ry'^2 (centred), 0; pads c' = 1e30
     float4 x0;            // q1, q2, dq1, dq2
-    float4 ctr;           // window centre (cx, cy), W, sscale of the candidate table (mppi_device.h)
+    float4 ctr;           // window centre (cx, cy), W, 0
     float4 ua[kMaxT];     // u0, u1, a0, a1 (a = (gamma u_t)^T Sigma^-1), fp32
     double u[kMaxT][2];   // nominal control sequence, fp64 (device closed loop)
 };
@@ -151,46 +151,7 @@ __device__ void nominal_update_block(DevStep* nxt, const KConst& c, Scratch& sm,
 
 // ------------------------------------------------------------ rollout kernel
 
-// Noise row load for step t.  Each prefetch is followed by an empty asm
-// statement with a memory clobber: a scheduling boundary that keeps the load
-// where it is written (otherwise the scheduler sinks it next to its use and
-// every step pays the full memory latency).
-#ifdef MPPI_ABL_NONOISE  // diagnostic ablation: no noise traffic (wrong results)
-__device__ __forceinline__ float2 noise_ld(const float2* p) {
-    const unsigned a = (unsigned)(uintptr_t)p;
-    return make_float2((float)(a & 255u) * 0.01f - 1.2f, (float)((a >> 8) & 255u) * 0.01f - 1.2f);
-}
-#else
-__device__ __forceinline__ float2 noise_ld(const float2* p) { return *p; }
-#endif
-
 constexpr int kPF = 4;  // noise rows in flight per lane
-// Blocked horizon loop for the full scan too (MPPI_BLOCKED builds): the
-// dynamics of kPF steps, then their searches, then one batch of LDS lookups.
-// Measured 0.9 % slower than step by step (tools/ab.py), so off by default.
-#ifdef MPPI_BLOCKED
-constexpr bool kBlockSteps = true;
-#else
-constexpr bool kBlockSteps = false;
-#endif
-// Deferred cost (default): each step's waypoint row is consumed after the next
-// step's dynamics (see dstep); MPPI_STEP_COST builds keep step() (diagnostics).
-#ifdef MPPI_STEP_COST
-constexpr bool kDeferCost = false;
-#else
-constexpr bool kDeferCost = true;
-#endif
-// Window keys from the matrix core (SearchMFMA, LPS = 1 full scan; opt-in
-// MPPI_MFMA_SEARCH builds, bit-identical): measured +14% at K = 65536 T = 64
-// against the VALU scan (dstep).  FP32 MFMA runs at the FP32 vector rate on the
-// same SIMD (MI355X guide: 64 FLOP/clk/SIMD either way), and the 32 x 32 x 2
-// shape computes 2x the needed products (zero K half, padded slots), so the
-// matrix core buys no issue slots here; kept for the record.
-#ifdef MPPI_MFMA_SEARCH
-constexpr bool kMfmaSearch = kDeferCost;
-#else
-constexpr bool kMfmaSearch = false;
-#endif
 
 // POLL: the partial rows travel as tagged granules (see st_gran) to consumer
 // workgroups that poll for them — the first workgroup of each group of kGroup
@@ -200,22 +161,15 @@ constexpr bool kMfmaSearch = false;
 // when the grid is at most one workgroup per CU); correctness does not depend
 // on placement or order, every value is tag-checked.  Otherwise (!POLL) the
 // last workgroup to arrive on a counter merges (arrive_last).
-// TAB (LPS = 1): the window search goes through the candidate table (TabSearch,
-// built per window by search_table_kernel), resolving each block of kPF steps
-// after their dynamics; results are bit-identical to the full scan.
-template <int LPS, int NT, bool POLL, bool TAB>
+template <int LPS, int NT, bool POLL>
 __global__ __launch_bounds__(NT) void rollout_kernel(
-    const KConst c, const DevStep* __restrict__ st, const uint4* __restrict__ tab, const float2* __restrict__ noise,
+    const KConst c, const DevStep* __restrict__ st, const float2* __restrict__ noise,
     double* __restrict__ S_out, double* __restrict__ slab, double* __restrict__ gslab,
     unsigned* __restrict__ counters, double* __restrict__ partial_out, double* __restrict__ w_eps_out,
     DevStep* __restrict__ nxt, unsigned flags, const XDesc xd, unsigned* __restrict__ epoch, unsigned* __restrict__ tmo,
     float* __restrict__ upd, unsigned long long* __restrict__ dbg) {
-    static_assert(!TAB || LPS == 1, "table search is per lane");
     __shared__ float4 s_win[kSlots];
-    __shared__ float4 s_ua[kDeferCost ? kMaxT : 1];   // per-step constants (u_t, a_t), kDeferCost
-    __shared__ __attribute__((aligned(16))) unsigned char s_tab[TAB ? kTabBytes : 16];
-    __shared__ float4 s_rows[TAB ? kKeyRows : 1];
-    __shared__ KeyPair s_kp[TAB ? kKeyPairs : 1];
+    __shared__ float4 s_ua[kMaxT];   // per-step constants (u_t, a_t)
     __shared__ float s_redf[NT / 64];
     __shared__ int s_cnt[NT / 64];
     __shared__ int s_k[NT];
@@ -240,7 +194,7 @@ __global__ __launch_bounds__(NT) void rollout_kernel(
     const float2* np = noise + k;
     float2 ring[kPF];   // noise rows eps[t][k] in flight
 #pragma unroll
-    for (int j = 0; j < kPF; ++j) ring[j] = noise_ld(np + (size_t)(j < T ? j : T - 1) * K);
+    for (int j = 0; j < kPF; ++j) ring[j] = np[(size_t)(j < T ? j : T - 1) * K];
     // this launch's granule tag (device epoch + 1), fetched now so its latency is hidden
     const unsigned tag_v = POLL ? __hip_atomic_load(epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) + 1u : 0u;
     // nominal element for the fused update, fetched now so its latency is hidden
@@ -249,23 +203,8 @@ __global__ __launch_bounds__(NT) void rollout_kernel(
     // window row for the LDS copy: loaded unconditionally (a load inside the
     // tid < kSlots branch would be waited for right there), stored before the barrier
     const float4 wrow = st->win[tid & (kSlots - 1)];
-    constexpr bool MF = kMfmaSearch && LPS == 1 && !TAB && !kBlockSteps;
     Search<LPS> sr;
-    SearchMFMA ms;
-    TabSearch ts;
-    if constexpr (MF) {
-        ms.load(st->key, st->ctr, lane);
-        sr.sub = 0;
-    } else if constexpr (TAB) {
-        for (int i = tid; i < kTabVec; i += NT) reinterpret_cast<uint4*>(s_tab)[i] = tab[i];
-        if (tid < kKeyRows) s_rows[tid] = tid < kSlots ? st->key[tid] : make_float4(0.f, 0.f, kPadKey, 0.f);
-        SearchLDS<false>::fill(s_kp, st->key, tid);
-        const float4 ctr = st->ctr;
-        ts = TabSearch{s_tab, s_rows, s_kp, ctr.x, ctr.y, ctr.w};
-        sr.sub = 0;
-    } else {
-        sr.load(st->key, st->ctr, tid & (LPS - 1));
-    }
+    sr.load(st->key, st->ctr, tid & (LPS - 1));
     const float4 x0 = st->x0;
     ArmState x;
     x.q1 = x0.x;
@@ -274,61 +213,25 @@ __global__ __launch_bounds__(NT) void rollout_kernel(
     x.dq2 = x0.w;
     sincos_f32(x.q1, &x.s1, &x.c1);
     sincos_f32(x.q1 + x.q2, &x.s12, &x.c12);
-    cfloat* cua = (cfloat*)(st->ua);
-    float4 uring[kPF];  // per-step constants (u_t, a_t), uniform
-    if constexpr (kDeferCost) {
-        for (int i = tid; i < T; i += NT) s_ua[i] = st->ua[i];
-    } else {
-#pragma unroll
-        for (int j = 0; j < kPF; ++j) uring[j] = const_ld4(cua + 4 * (j < T ? j : T - 1));
-    }
+    // the per-step constants go to LDS: the ring reads them there, so no scalar
+    // load shares lgkmcnt with the deferred row lookup below
+    for (int i = tid; i < T; i += NT) s_ua[i] = st->ua[i];
     if (tid < kSlots) s_win[tid] = wrow;
     __syncthreads();
-    if constexpr (kDeferCost) {
+    float4 uring[kPF];  // per-step constants (u_t, a_t), uniform
 #pragma unroll
-        for (int j = 0; j < kPF; ++j) uring[j] = s_ua[j < T ? j : T - 1];
-    }
+    for (int j = 0; j < kPF; ++j) uring[j] = s_ua[j < T ? j : T - 1];
 
     // Horizon loop (control.py:95-109): v = u + eps -> _F -> end effector ->
     // nearest waypoint -> stage cost + control cost, S in fp64.
+    //
+    // Deferred cost: the LDS row of step t's nearest waypoint is consumed one
+    // step later, after step t + 1's dynamics, so the lookup's latency is
+    // hidden.  The costs are still added in step order and folded into fp64
+    // every kPF steps (S4), so S is the sum of the same fp32 terms.
     double S = 0.0;
     float S4 = 0.f;  // fp32 partial over one 4-step block, folded into fp64 S
     float ex = 0.f, ey = 0.f, e1 = 0.f, e2 = 0.f;
-    // `slot` (= t % kPF) is a compile-time constant at every call, so the rings
-    // stay in registers (a runtime index sends them to scratch).
-    auto step = [&](int t, auto slot_c) {
-        constexpr int slot = decltype(slot_c)::value;
-        const float2 e = ring[slot];
-        const float4 ua = uring[slot];
-        const int tl = t + kPF < T ? t + kPF : T - 1;
-        ring[slot] = noise_ld(np + (size_t)tl * K);
-        uring[slot] = const_ld4(cua + 4 * tl);
-        PIN_LOADS();
-        const float v1 = fmaf(exf, ua.x, e.x);  // u[t] + eps (exploit) or eps, control.py:99-101
-        const float v2 = fmaf(exf, ua.y, e.y);
-        dyn_step(x, v1, v2, c);
-        const float px = fmaf(c.fk1, x.c1, c.fk2 * x.c12);  // control.py:178-179
-        const float py = fmaf(c.fk1, x.s1, c.fk2 * x.s12);
-#if defined(MPPI_ABL_NOSEARCH)   // diagnostic ablations (wrong results): no window scan / no LDS row lookup
-        const float4 r = s_win[(__float_as_uint(px) ^ __float_as_uint(py)) & 31u];
-#elif defined(MPPI_ABL_NOLOOKUP)
-        const unsigned jj = sr.nearest(px, py);
-        const float4 r = make_float4((float)jj * 1e-3f, 0.f, (float)jj, 0.f);
-#else
-        const float4 r = s_win[sr.nearest(px, py)];
-#endif
-        ex = px - r.x;
-        ey = py - r.y;
-        e1 = x.dq1 - r.z;
-        e2 = x.dq2 - r.w;
-        const float g = fmaf(ua.z, v1, ua.w * v2);  // (gamma u^T Sigma^-1) v, control.py:106
-        S4 += weighted_sq(ex, ey, e1, e2, c.sw) + g;
-    };
-    // kDeferCost: the LDS row of step t's nearest waypoint is consumed one step
-    // later, after step t + 1's dynamics, so the lookup's latency is hidden; the
-    // per-step constants come from LDS (no scalar load shares lgkmcnt with the
-    // lookup).  The costs are added in step order and folded every kPF steps as
-    // in step() (same sums).
     float4 pr = make_float4(0.f, 0.f, 0.f, 0.f);
     float ppx = 0.f, ppy = 0.f, pd1 = 0.f, pd2 = 0.f, pg = 0.f;
     auto add_pending = [&]() {
@@ -338,9 +241,11 @@ __global__ __launch_bounds__(NT) void rollout_kernel(
         e2 = pd2 - pr.w;
         S4 += weighted_sq(ex, ey, e1, e2, c.sw) + pg;
     };
-    // (H: step t - 1 exists — 0 no, 1 yes, 2 test t > 0 at run time.  LPS = 1
-    // peels the first step so the unrolled loop body is one basic block: -2.9%
-    // at K = 65536; the LPS > 1 kernels keep the test, +5% when peeled at K = 4096)
+    // `slot` (= t % kPF) is a compile-time constant at every call, so the rings
+    // stay in registers (a runtime index sends them to scratch).  H: step t - 1
+    // exists — 0 no, 1 yes, 2 test t > 0 at run time.  LPS = 1 peels the first
+    // step so the unrolled loop body is one basic block (-2.9% at K = 65536);
+    // the LPS > 1 kernels keep the test (+5% when peeled at K = 4096).
     auto dstep = [&](int t, auto slot_c, auto h_c) {
         constexpr int slot = decltype(slot_c)::value;
         constexpr int H = decltype(h_c)::value;
@@ -348,7 +253,7 @@ __global__ __launch_bounds__(NT) void rollout_kernel(
         const float2 e = ring[slot];
         const float4 ua = uring[slot];
         const int tl = t + kPF < T ? t + kPF : T - 1;
-        ring[slot] = noise_ld(np + (size_t)tl * K);
+        ring[slot] = np[(size_t)tl * K];
         uring[slot] = s_ua[tl];
         PIN_LOADS();
         const float v1 = fmaf(exf, ua.x, e.x);  // u[t] + eps (exploit) or eps, control.py:99-101
@@ -368,210 +273,47 @@ __global__ __launch_bounds__(NT) void rollout_kernel(
         pg = fmaf(ua.z, v1, ua.w * v2);  // (gamma u^T Sigma^-1) v, control.py:106
         pr = s_win[sr.nearest(ppx, ppy)];
     };
-    // MF: a three-stage pipeline over the steps, so that no instruction waits on
-    // the matrix core (issue is in order) and every cost is still added in step
-    // order:  step t:  [first MFMA pair of step t - 1 is done] second pair of
-    // step t - 1 -> dynamics t -> kinematics t, first pair of step t -> cost of
-    // step t - 2 (row looked up during step t - 1) -> reduce step t - 1's keys
-    // and look its row up.  Pending records: q = step t - 1, pp = step t - 2.
-    // Costs are folded after every step = 3 mod 4, as in step() / dstep().
-    float qx1 = 0.f, qy1 = 0.f, qd1 = 0.f, qe1 = 0.f, qg1 = 0.f;
-    // (h1, h2: steps t - 1 / t - 2 exist; compile-time, the first two steps are peeled)
-    auto mstep = [&](int t, auto slot_c, auto h1_c, auto h2_c) {
-        constexpr int slot = decltype(slot_c)::value;
-        constexpr int P = slot & 1, Q = P ^ 1;   // key buffers of steps t and t - 1
-        constexpr bool h1 = decltype(h1_c)::value, h2 = decltype(h2_c)::value;
-        const float2 e = ring[slot];
-        const float4 ua = uring[slot];
-        const int tl = t + kPF < T ? t + kPF : T - 1;
-        ring[slot] = noise_ld(np + (size_t)tl * K);
-        uring[slot] = s_ua[tl];
-        PIN_LOADS();
-        if constexpr (h1) ms.template issue2<Q>();
-        __builtin_amdgcn_sched_barrier(0);
-        const float v1 = fmaf(exf, ua.x, e.x);  // u[t] + eps (exploit) or eps, control.py:99-101
-        const float v2 = fmaf(exf, ua.y, e.y);
-        dyn_step(x, v1, v2, c);
-        const float nx = fmaf(c.fk1, x.c1, c.fk2 * x.c12);  // control.py:178-179
-        const float ny = fmaf(c.fk1, x.s1, c.fk2 * x.s12);
-        ms.template issue1<P>(nx, ny);
-        __builtin_amdgcn_sched_barrier(0);
-        if constexpr (h2) {
-            add_pending();   // step t - 2
-            if (slot == 1) {
-                S += (double)S4;
-                S4 = 0.f;
-            }
-        }
-        if constexpr (h1) {
-            pr = s_win[ms.template reduce<Q>()];   // step t - 1's row
-            ppx = qx1;
-            ppy = qy1;
-            pd1 = qd1;
-            pd2 = qe1;
-            pg = qg1;
-        }
-        qx1 = nx;
-        qy1 = ny;
-        qd1 = x.dq1;
-        qe1 = x.dq2;
-        qg1 = fmaf(ua.z, v1, ua.w * v2);  // (gamma u^T Sigma^-1) v, control.py:106
-    };
-    // TAB: the dynamics of steps t..t+n-1 first, then their n window searches
-    // together (independent of each other: the lookups' LDS latencies overlap),
-    // then the costs in step order (the same fp32 sums as step()).
-    auto block = [&](int t, auto n_c) {
-        constexpr int n = decltype(n_c)::value;
-        float px[n], py[n], d1[n], d2[n], gc[n];
-        unroll_seq([&](auto s_c) {
-            constexpr int s = decltype(s_c)::value;
-            const float2 e = ring[s];
-            const float4 ua = uring[s];
-            const int tl = t + s + kPF < T ? t + s + kPF : T - 1;
-            ring[s] = noise_ld(np + (size_t)tl * K);
-            PIN_LOADS();
-            const float v1 = fmaf(exf, ua.x, e.x);
-            const float v2 = fmaf(exf, ua.y, e.y);
-            dyn_step(x, v1, v2, c);
-            px[s] = fmaf(c.fk1, x.c1, c.fk2 * x.c12);
-            py[s] = fmaf(c.fk1, x.s1, c.fk2 * x.s12);
-            d1[s] = x.dq1;
-            d2[s] = x.dq2;
-            gc[s] = fmaf(ua.z, v1, ua.w * v2);
-        }, std::make_integer_sequence<int, n>{});
-        unsigned jn[n];
-        if constexpr (TAB) {
-            ts.nearest<n>(px, py, jn);
-        } else {
-#pragma unroll
-            for (int s = 0; s < n; ++s) jn[s] = sr.nearest(px[s], py[s]);
-        }
-#pragma unroll
-        for (int s = 0; s < n; ++s) {
-            const float4 r = s_win[jn[s]];
-            ex = px[s] - r.x;
-            ey = py[s] - r.y;
-            e1 = d1[s] - r.z;
-            e2 = d2[s] - r.w;
-            S4 += weighted_sq(ex, ey, e1, e2, c.sw) + gc[s];
-        }
-        // scalar prefetches after the block's LDS lookups (see step())
-        PIN_LOADS();
-        unroll_seq([&](auto s_c) {
-            constexpr int s = decltype(s_c)::value;
-            uring[s] = const_ld4(cua + 4 * (t + s + kPF < T ? t + s + kPF : T - 1));
-        }, std::make_integer_sequence<int, n>{});
-        PIN_LOADS();
-    };
     using I0 = std::integral_constant<int, 0>;
     using I1 = std::integral_constant<int, 1>;
     using I2 = std::integral_constant<int, 2>;
     using I3 = std::integral_constant<int, 3>;
+    using H0 = std::integral_constant<int, 0>;
+    using H1 = std::integral_constant<int, 1>;
+    using H2 = std::integral_constant<int, 2>;
     static_assert(kPF == 4, "unrolled for a 4-deep ring");
     int t = 0;
-    if constexpr (TAB || kBlockSteps) {
-        for (; t + kPF <= T; t += kPF) {
-            block(t, std::integral_constant<int, kPF>{});
-            S += (double)S4;
-            S4 = 0.f;
-        }
-        const int rem = T - t;  // slots 0..rem-1, t % kPF == 0
-        if (rem == 1) block(t, I1{});
-        else if (rem == 2) block(t, I2{});
-        else if (rem == 3) block(t, I3{});
-    } else if constexpr (MF) {
-        STAMP(12, NOW());
-        using BF = std::false_type;
-        using BT = std::true_type;
-        mstep(0, I0{}, BF{}, BF{});
-        if (T > 1) mstep(1, I1{}, BT{}, BF{});
-        for (t = 2; t + kPF <= T; t += kPF) {   // slots 2, 3, 0, 1
-            mstep(t, I2{}, BT{}, BT{});
-            mstep(t + 1, I3{}, BT{}, BT{});
-            mstep(t + 2, I0{}, BT{}, BT{});
-            mstep(t + 3, I1{}, BT{}, BT{});
+    STAMP(12, NOW());
+    if constexpr (LPS == 1) {
+        dstep(0, I0{}, H0{});
+        for (t = 1; t + kPF <= T; t += kPF) {   // slots 1, 2, 3, 0
+            dstep(t, I1{}, H1{});
+            dstep(t + 1, I2{}, H1{});
+            dstep(t + 2, I3{}, H1{});
+            dstep(t + 3, I0{}, H1{});
 #ifdef MPPI_STAMPS
-            if (t == 2) STAMP(13, NOW());
-            if (t + kPF == T / 2 + 2) STAMP(14, NOW());
+            if (t == 1) STAMP(13, NOW());
+            if (t + kPF == T / 2 + 1) STAMP(14, NOW());
 #endif
         }
-        if (t < T) mstep(t, I2{}, BT{}, BT{});          // remainder: t % kPF == 2, 3, 0 in order
-        if (t + 1 < T) mstep(t + 1, I3{}, BT{}, BT{});
-        if (t + 2 < T) mstep(t + 2, I0{}, BT{}, BT{});
-        if (T >= 2) {
-            add_pending();                   // step T - 2
-            if ((T - 2) % kPF == kPF - 1) {
-                S += (double)S4;
-                S4 = 0.f;
-            }
-        }
-        if ((T - 1) & 1) {                   // step T - 1: its second MFMA pair, then its row
-            ms.template issue2<1>();
-            pr = s_win[ms.template reduce<1>()];
-        } else {
-            ms.template issue2<0>();
-            pr = s_win[ms.template reduce<0>()];
-        }
-        ppx = qx1;
-        ppy = qy1;
-        pd1 = qd1;
-        pd2 = qe1;
-        pg = qg1;
-        add_pending();
-    } else if constexpr (kDeferCost) {
-        STAMP(12, NOW());
-        using H0 = std::integral_constant<int, 0>;
-        using H1 = std::integral_constant<int, 1>;
-        using H2 = std::integral_constant<int, 2>;
-        if constexpr (LPS == 1) {
-            dstep(0, I0{}, H0{});
-            for (t = 1; t + kPF <= T; t += kPF) {   // slots 1, 2, 3, 0
-                dstep(t, I1{}, H1{});
-                dstep(t + 1, I2{}, H1{});
-                dstep(t + 2, I3{}, H1{});
-                dstep(t + 3, I0{}, H1{});
-#ifdef MPPI_STAMPS
-                if (t == 1) STAMP(13, NOW());
-                if (t + kPF == T / 2 + 1) STAMP(14, NOW());
-#endif
-            }
-            if (t < T) dstep(t, I1{}, H1{});          // remainder: t % kPF == 1, 2, 3 in order
-            if (t + 1 < T) dstep(t + 1, I2{}, H1{});
-            if (t + 2 < T) dstep(t + 2, I3{}, H1{});
-        } else {
-            for (; t + kPF <= T; t += kPF) {
-                dstep(t, I0{}, H2{});
-                dstep(t + 1, I1{}, H2{});
-                dstep(t + 2, I2{}, H2{});
-                dstep(t + 3, I3{}, H2{});
-#ifdef MPPI_STAMPS
-                if (t == 0) STAMP(13, NOW());
-                if (t + kPF == T / 2) STAMP(14, NOW());
-#endif
-            }
-            if (t < T) dstep(t, I0{}, H2{});          // remainder: t % kPF == 0, 1, 2 in order
-            if (t + 1 < T) dstep(t + 1, I1{}, H2{});
-            if (t + 2 < T) dstep(t + 2, I2{}, H2{});
-        }
-        add_pending();                       // step T - 1
+        if (t < T) dstep(t, I1{}, H1{});          // remainder: t % kPF == 1, 2, 3 in order
+        if (t + 1 < T) dstep(t + 1, I2{}, H1{});
+        if (t + 2 < T) dstep(t + 2, I3{}, H1{});
     } else {
-        STAMP(12, NOW());
         for (; t + kPF <= T; t += kPF) {
-            step(t, I0{});
-            step(t + 1, I1{});
-            step(t + 2, I2{});
-            step(t + 3, I3{});
-            S += (double)S4;
-            S4 = 0.f;
+            dstep(t, I0{}, H2{});
+            dstep(t + 1, I1{}, H2{});
+            dstep(t + 2, I2{}, H2{});
+            dstep(t + 3, I3{}, H2{});
 #ifdef MPPI_STAMPS
             if (t == 0) STAMP(13, NOW());
             if (t + kPF == T / 2) STAMP(14, NOW());
 #endif
         }
-        if (t < T) step(t, I0{});          // remainder: t % kPF == 0, 1, 2 in order
-        if (t + 1 < T) step(t + 1, I1{});
-        if (t + 2 < T) step(t + 2, I2{});
+        if (t < T) dstep(t, I0{}, H2{});          // remainder: t % kPF == 0, 1, 2 in order
+        if (t + 1 < T) dstep(t + 1, I1{}, H2{});
+        if (t + 2 < T) dstep(t + 2, I2{}, H2{});
     }
+    add_pending();                       // step T - 1
     S += (double)S4;
     S += (double)weighted_sq(ex, ey, e1, e2, c.tw);  // terminal cost, control.py:109
 
@@ -772,35 +514,35 @@ __global__ __launch_bounds__(kThreads) void traj_kernel(const KConst c, const De
     }
 }
 
-// Candidate table of the window search (mppi_device.h, build_tab_cell): one
-// thread per (cell, slot), from the step block's fp32 keys as the rollouts read them.
-__global__ __launch_bounds__(256) void search_table_kernel(const DevStep* __restrict__ st, unsigned char* __restrict__ tab) {
-    const float4 ctr = st->ctr;
-    build_tab_cell(st->key, (int)ctr.z, ctr.w, tab);
-}
-
-// Diagnostics / tests: the table search and the full scan of the same points
-// (pts[n] = (px, py)); out[2i] = table result, out[2i + 1] = full scan.
-__global__ __launch_bounds__(256) void search_check_kernel(const DevStep* __restrict__ st, const uint4* __restrict__ tab,
-                                                           const float2* __restrict__ pts, int n, int* __restrict__ out) {
-    __shared__ __attribute__((aligned(16))) unsigned char s_tab[kTabBytes];
-    __shared__ float4 s_rows[kKeyRows];
-    __shared__ KeyPair s_kp[kKeyPairs];
-    const int tid = threadIdx.x;
-    for (int i = tid; i < kTabVec; i += 256) reinterpret_cast<uint4*>(s_tab)[i] = tab[i];
-    if (tid < kKeyRows) s_rows[tid] = tid < kSlots ? st->key[tid] : make_float4(0.f, 0.f, kPadKey, 0.f);
-    SearchLDS<false>::fill(s_kp, st->key, tid);
-    __syncthreads();
-    const float4 ctr = st->ctr;
-    const TabSearch ts{s_tab, s_rows, s_kp, ctr.x, ctr.y, ctr.w};
-    const int i = blockIdx.x * 256 + tid;
-    const float2 p = pts[min(i, n - 1)];
-    unsigned j;
-    ts.nearest<1>(&p.x, &p.y, &j);
-    const unsigned jf = ts.scan_all(p.x - ctr.x, p.y - ctr.y);
-    if (i < n) {
-        out[2 * i] = (int)j;
-        out[2 * i + 1] = (int)jf;
+// Diagnostics / tests (mppi_debug_nearest): the nearest window slot of every
+// sample and step as the rollout evaluates it — the same dyn_step and
+// Search<1>::nearest on the same inputs, so the same fp32 positions and slots —
+// with the end-effector position: slot[k][t], pos[k][t] = (px, py).
+__global__ __launch_bounds__(kThreads) void nearest_debug_kernel(const KConst c, const DevStep* __restrict__ st,
+                                                                 const float2* __restrict__ noise, int Kn,
+                                                                 int* __restrict__ slot, float2* __restrict__ pos) {
+    const int k = blockIdx.x * kThreads + threadIdx.x;
+    if (k >= Kn) return;
+    const int T = c.T;
+    const float exf = (c.k_offset + k) < c.k_exploit ? 1.f : 0.f;
+    Search<1> sr;
+    sr.load(st->key, st->ctr, 0);
+    const float4 x0 = st->x0;
+    ArmState x;
+    x.q1 = x0.x;
+    x.q2 = x0.y;
+    x.dq1 = x0.z;
+    x.dq2 = x0.w;
+    sincos_f32(x.q1, &x.s1, &x.c1);
+    sincos_f32(x.q1 + x.q2, &x.s12, &x.c12);
+    for (int t = 0; t < T; ++t) {
+        const float4 ua = st->ua[t];
+        const float2 e = noise[(size_t)t * c.K_local + k];
+        dyn_step(x, fmaf(exf, ua.x, e.x), fmaf(exf, ua.y, e.y), c);
+        const float px = fmaf(c.fk1, x.c1, c.fk2 * x.c12);
+        const float py = fmaf(c.fk1, x.s1, c.fk2 * x.s12);
+        slot[(size_t)k * T + t] = (int)sr.nearest(px, py);
+        pos[(size_t)k * T + t] = make_float2(px, py);
     }
 }
 
@@ -836,8 +578,6 @@ struct mppi_ctx {
     KConst kc;
     DevStep* d_step = nullptr;  // [2] ping-pong
     int cur = 0;
-    uint4* d_tab = nullptr;     // window-search candidate table (built per window)
-    bool use_tab = false;       // LPS = 1 and MPPI_SEARCH=table
     DevStep* h_step = nullptr;  // pinned staging
     hipEvent_t staged = nullptr;
     double* d_slab = nullptr;
@@ -894,7 +634,7 @@ int launch_check(const char* what) {
 
 template <int L, int N>
 int occupancy(int* per_cu) {
-    return (int)hipOccupancyMaxActiveBlocksPerMultiprocessor(per_cu, (const void*)rollout_kernel<L, N, true, L == 1>, N, 0);
+    return (int)hipOccupancyMaxActiveBlocksPerMultiprocessor(per_cu, (const void*)rollout_kernel<L, N, true>, N, 0);
 }
 
 int check_timeout(mppi_ctx* c) {
@@ -947,11 +687,6 @@ int mppi_ctx_create(const mppi_config* cfg, int device, void* stream, mppi_ctx**
         return fail(MPPI_E_ARG, "lanes_per_sample must be 0, 1, 2 or 4");
     }
     c->lps = lps;
-    // window search: the full 30-slot scan (default), or MPPI_SEARCH=table for the
-    // candidate table (LPS = 1; bit-identical; faster only while the samples stay
-    // away from the window — DESIGN §3, "Tried and measured")
-    const char* sv = getenv("MPPI_SEARCH");
-    c->use_tab = lps == 1 && sv && !strcmp(sv, "table");
     // 512-thread workgroups when the grid fills every CU with one of them (8 waves:
     // two per SIMD); 256 otherwise.  MPPI_BLOCK=256|512 overrides (diagnostics).
     const long long lanes = (long long)cfg->K_local * lps;
@@ -1025,8 +760,6 @@ int mppi_ctx_create(const mppi_config* cfg, int device, void* stream, mppi_ctx**
     const size_t gslab = (size_t)ngroups * (2 + 2 * cfg->T) * val;
     const size_t ctr_bytes = ((size_t)(ngroups + 2) * sizeof(unsigned) + 255) & ~(size_t)255;
     if ((e = hipMalloc(&c->d_step, 2 * sizeof(DevStep))) != hipSuccess ||
-        (e = hipMalloc(&c->d_tab, kTabBytes)) != hipSuccess ||
-        (e = hipMemset(c->d_tab, 0xFF, kTabBytes)) != hipSuccess ||
         (e = hipMalloc(&c->d_slab, slab)) != hipSuccess ||
         (e = hipMalloc(&c->d_gslab, gslab)) != hipSuccess ||
         (e = hipMalloc(&c->d_counter, ctr_bytes)) != hipSuccess ||
@@ -1060,7 +793,6 @@ void mppi_ctx_destroy(mppi_ctx* c) {
     if (c->stream) (void)hipStreamSynchronize(c->stream);
     (void)hipDeviceSynchronize();
     (void)hipFree(c->d_step);
-    (void)hipFree(c->d_tab);
     (void)hipFree(c->d_slab);
     (void)hipFree(c->d_counter);
     (void)hipFree(c->d_gslab);
@@ -1119,11 +851,7 @@ int mppi_set_step_inputs(mppi_ctx* c, const double* x0, const double* window, in
         }
     }
     h->x0 = make_float4((float)x0[0], (float)x0[1], (float)x0[2], (float)x0[3]);
-    // candidate table scale: sigma bins over [0, 2 / R_w), R_w = max |r'_j| of the fp32 keys
-    double R2 = 0.0;
-    for (int j = 0; j < W; ++j) R2 = fmax(R2, (double)h->key[j].z);
-    const float sscale = R2 > 0.0 && isfinite(R2) ? (float)(kTabSig * 0.5 * sqrt(R2)) : 0.f;
-    h->ctr = make_float4((float)cx, (float)cy, (float)W, sscale);
+    h->ctr = make_float4((float)cx, (float)cy, (float)W, 0.f);
     size_t bytes = offsetof(DevStep, ua);
     if (u) {
         const KConst& k = c->kc;
@@ -1142,12 +870,6 @@ int mppi_set_step_inputs(mppi_ctx* c, const double* x0, const double* window, in
     HIP_TRY(hipMemcpyAsync(c->d_step + (c->cur ^ 1), h, offsetof(DevStep, ua), hipMemcpyHostToDevice, c->stream));
     HIP_TRY(hipMemcpyAsync(c->d_step + c->cur, h, bytes, hipMemcpyHostToDevice, c->stream));
     HIP_TRY(hipEventRecord(c->staged, c->stream));
-    if (c->use_tab) {
-        // one thread per (cell, slot); stream-ordered after the copies above
-        hipLaunchKernelGGL(search_table_kernel, dim3(kTabBytes * 32 / 256), dim3(256), 0, c->stream, c->d_step + c->cur,
-                           reinterpret_cast<unsigned char*>(c->d_tab));
-        return launch_check("search_table_kernel");
-    }
     return MPPI_OK;
 }
 
@@ -1163,38 +885,26 @@ int mppi_rollout(mppi_ctx* c, const float* noise_dev, double* S_dev, double* par
     const DevStep* cur = c->d_step + c->cur;
     DevStep* nxt = c->d_step + (c->cur ^ 1);
     const float2* nz = reinterpret_cast<const float2*>(noise_dev);
-#define MPPI_LAUNCH3(L, NTH, P, TB)                                                                             \
-    hipLaunchKernelGGL((rollout_kernel<L, NTH, P, TB>), dim3(c->nblocks), dim3(NTH), 0, c->stream, c->kc, cur, c->d_tab, nz, \
-                       S_dev, c->d_slab, c->d_gslab, c->d_counter, partial_dev, c->d_weps, nxt, flags, c->xd, c->d_epoch, \
+#define MPPI_LAUNCH(L, NTH, P)                                                                                   \
+    hipLaunchKernelGGL((rollout_kernel<L, NTH, P>), dim3(c->nblocks), dim3(NTH), 0, c->stream, c->kc, cur, nz, S_dev,  \
+                       c->d_slab, c->d_gslab, c->d_counter, partial_dev, c->d_weps, nxt, flags, c->xd, c->d_epoch,       \
                        c->d_tmo, reinterpret_cast<float*>(c->d_upd), c->d_dbg)
-#define MPPI_LAUNCH2(L, NTH, P)                  \
-    do {                                        \
-        if (c->use_tab) MPPI_LAUNCH3(L, NTH, P, true); \
-        else MPPI_LAUNCH3(L, NTH, P, false);    \
-    } while (0)
-#define MPPI_LAUNCH(L, NTH)               \
-    do {                                  \
-        if (c->poll) MPPI_LAUNCH2(L, NTH, true);  \
-        else MPPI_LAUNCH2(L, NTH, false); \
-    } while (0)
-#define MPPI_LAUNCH_NT(L, NTH, P)         \
-    do {                                  \
-        if (P) MPPI_LAUNCH3(L, NTH, true, false);  \
-        else MPPI_LAUNCH3(L, NTH, false, false);   \
+#define MPPI_LAUNCH_P(L, NTH)                \
+    do {                                     \
+        if (c->poll) MPPI_LAUNCH(L, NTH, true);  \
+        else MPPI_LAUNCH(L, NTH, false);     \
     } while (0)
     if (c->nt == 512) {
-        if (c->lps == 1) MPPI_LAUNCH(1, 512);
-        else if (c->lps == 2) MPPI_LAUNCH_NT(2, 512, c->poll);
-        else MPPI_LAUNCH_NT(4, 512, c->poll);
+        if (c->lps == 1) MPPI_LAUNCH_P(1, 512);
+        else if (c->lps == 2) MPPI_LAUNCH_P(2, 512);
+        else MPPI_LAUNCH_P(4, 512);
     } else {
-        if (c->lps == 1) MPPI_LAUNCH(1, 256);
-        else if (c->lps == 2) MPPI_LAUNCH_NT(2, 256, c->poll);
-        else MPPI_LAUNCH_NT(4, 256, c->poll);
+        if (c->lps == 1) MPPI_LAUNCH_P(1, 256);
+        else if (c->lps == 2) MPPI_LAUNCH_P(2, 256);
+        else MPPI_LAUNCH_P(4, 256);
     }
-#undef MPPI_LAUNCH_NT
+#undef MPPI_LAUNCH_P
 #undef MPPI_LAUNCH
-#undef MPPI_LAUNCH2
-#undef MPPI_LAUNCH3
     const int rc = launch_check("rollout_kernel");
     if (rc == MPPI_OK && (flags & MPPI_FLAG_FUSED_UPDATE)) {
         c->cur ^= 1;
@@ -1353,12 +1063,12 @@ int mppi_debug_set_buffer(mppi_ctx* c, void* dbg_dev) {
     return MPPI_OK;
 }
 
-int mppi_debug_search(mppi_ctx* c, const float* pts_dev, int n, int* out_dev) {
-    if (!c || !pts_dev || !out_dev || n < 1) return fail(MPPI_E_ARG, "bad argument");
-    if (!c->use_tab) return fail(MPPI_E_ARG, "context does not use the candidate table (MPPI_SEARCH=table, LPS 1)");
-    hipLaunchKernelGGL(search_check_kernel, dim3((n + 255) / 256), dim3(256), 0, c->stream, c->d_step + c->cur, c->d_tab,
-                       reinterpret_cast<const float2*>(pts_dev), n, out_dev);
-    return launch_check("search_check_kernel");
+int mppi_debug_nearest(mppi_ctx* c, const float* noise_dev, int K, int* slot_dev, float* pos_dev) {
+    if (!c || !noise_dev || !slot_dev || !pos_dev || K < 1 || K > c->cfg.K_local) return fail(MPPI_E_ARG, "bad argument");
+    hipLaunchKernelGGL(nearest_debug_kernel, dim3((K + kThreads - 1) / kThreads), dim3(kThreads), 0, c->stream, c->kc,
+                       c->d_step + c->cur, reinterpret_cast<const float2*>(noise_dev), K, slot_dev,
+                       reinterpret_cast<float2*>(pos_dev));
+    return launch_check("nearest_debug_kernel");
 }
 
 int mppi_sync(mppi_ctx* c) {

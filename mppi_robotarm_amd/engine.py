@@ -83,9 +83,13 @@ class RolloutEngine:
             pass
 
     def _sync_stream(self):
-        """Follow torch's current stream (it may change between calls)."""
+        """Follow torch's current stream (it may change between calls).  The new
+        stream first waits for the old one: work already queued there (a noise
+        draw, a rollout writing a buffer the next call reads) is finished before
+        anything issued on the new stream runs."""
         s = torch.cuda.current_stream(self.device)
         if s.cuda_stream != self.stream.cuda_stream:
+            s.wait_stream(self.stream)
             self.stream = s
             N.check(self._lib.mppi_set_stream(self._ctx, C.c_void_p(s.cuda_stream)), "mppi_set_stream")
 
@@ -216,16 +220,20 @@ class RolloutEngine:
                                             C.c_void_p(out.data_ptr())), "mppi_noise_philox")
         return out
 
-    def search_check(self, points) -> np.ndarray:
-        """Tests: nearest window slot of end-effector points (n, 2) through the
-        candidate table and by the full scan -> (n, 2) int32 (must agree)."""
+    def nearest_slots(self, noise: torch.Tensor, K: int | None = None) -> tuple[np.ndarray, np.ndarray]:
+        """Tests: the window slot the rollout picks for each of the first K samples at
+        every step (_get_nearest_waypoint in _c, control.py:176-180, 205-215), and the
+        fp32 end-effector position it searched for -> (slot (K, T) int32, pos (K, T, 2))."""
         self._sync_stream()
-        pts = torch.as_tensor(np.ascontiguousarray(points, dtype=np.float32).reshape(-1, 2), device=self.device)
-        out = torch.empty((pts.shape[0], 2), dtype=torch.int32, device=self.device)
-        N.check(self._lib.mppi_debug_search(self._ctx, C.c_void_p(pts.data_ptr()), int(pts.shape[0]),
-                                            C.c_void_p(out.data_ptr())), "mppi_debug_search")
+        self._check_noise(noise)
+        K = self.K_local if K is None else int(K)
+        slot = torch.empty((K, self.T), dtype=torch.int32, device=self.device)
+        pos = torch.empty((K, self.T, 2), dtype=torch.float32, device=self.device)
+        N.check(self._lib.mppi_debug_nearest(self._ctx, C.c_void_p(noise.data_ptr()), K,
+                                             C.c_void_p(slot.data_ptr()), C.c_void_p(pos.data_ptr())),
+                "mppi_debug_nearest")
         self.synchronize()
-        return out.cpu().numpy()
+        return slot.cpu().numpy(), pos.cpu().numpy()
 
     def synchronize(self) -> None:
         N.check(self._lib.mppi_sync(self._ctx), "mppi_sync")

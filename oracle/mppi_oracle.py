@@ -131,15 +131,18 @@ def state_cost(q1, q2, dq1, dq2, ref_path, prev_idx, weight, p: ArmParams):
 
 
 def rollout_costs(x0, u, eps, ref_path, prev_idx, dt, lam, alpha, sigma, stage_w, term_w,
-                  expl=0.0, p: ArmParams = ArmParams(), k_offset=0, K_total=None):
+                  expl=0.0, p: ArmParams = ArmParams(), k_offset=0, K_total=None, gamma=None):
     """The K x T hot loop, control.py:81-109.  Returns S (K,) fp64.
 
     ``k_offset`` / ``K_total`` restate the exploration split
     ``k < (1 - expl) * K`` (control.py:98) for a shard of a larger sample set.
+    ``gamma``: the controller's ``param_gamma`` (fixed at construction,
+    control.py:45, read at :106); default lam (1 - alpha).
     """
     K, T, _ = eps.shape
     K_total = K if K_total is None else K_total
-    gamma = lam * (1.0 - alpha)                       # control.py:45
+    if gamma is None:
+        gamma = lam * (1.0 - alpha)                   # control.py:45
     sig_inv = np.linalg.inv(sigma)                    # control.py:106 (raises on singular)
     kg = np.arange(K) + k_offset
     exploit = kg < (1.0 - expl) * K_total             # control.py:98
@@ -273,7 +276,7 @@ class OracleController:
         S = rollout_costs(x0, u, eps, self.ref_path, self.prev_waypoints_idx, self.delta_t,
                           self.param_lambda, self.param_alpha, self.Sigma,
                           self.stage_cost_weight, self.terminal_cost_weight,
-                          self.param_exploration, self.arm)
+                          self.param_exploration, self.arm, gamma=self.param_gamma)
         w = compute_weights(S, self.param_lambda)
         w_eps_raw = weighted_noise(w, eps)
         w_eps = moving_median_filter(w_eps_raw, 10)

@@ -1,0 +1,172 @@
+"""Index-level parity of the per-(sample, step) nearest-waypoint search.
+
+The reference evaluates ``_get_nearest_waypoint`` (control.py:200-232) inside
+``_c`` (control.py:176-180) for every sample and step: the first-occurrence
+argmin of ``((x - rx)^2 + (y - ry)^2) * 100`` over the window, in fp64 on raw
+coordinates.  The device does it in fp32 on window-centred keys with the slot
+index packed into 5 mantissa bits (mppi_device.h ``Search``).  The cost tests
+(S within 5e-5, same argmin of S) bound its effect on the output; this file
+checks the indices themselves through ``mppi_debug_nearest``, which runs the
+rollout's own dynamics and search code on the same inputs:
+
+  (a) search exactness at the device's own fp32 positions: every device slot is
+      the fp64 argmin there, or a tie within the key resolution
+      (SEARCH_TOL: 2^-16 of the key scale, the 5-bit packing plus the fp32 key
+      rounding, plus the fp32 rounding of the window coordinates);
+  (b) against the fp64 oracle's indices on its fp64 trajectory: the mismatch
+      rate is reported, and every mismatch is a near-tie at the oracle's
+      position — its gap is within what the fp32/fp64 position drift |dp| can
+      move (|f(p) - f(p')| <= |dp| (|p - r| + |p' - r|) for f = |p - r|^2) plus
+      the search tolerance of (a).
+"""
+import numpy as np
+import pytest
+
+torch = pytest.importorskip("torch")
+pytestmark = pytest.mark.gpu
+
+import mppi_oracle as O  # noqa: E402
+from conftest import load_step  # noqa: E402
+
+RUNPY = dict(param_exploration=0.0, param_lambda=100.0, param_alpha=0.98, sigma=np.eye(2) * 20.0,
+             stage_cost_weight=np.array([0.5, 0.5, 5.0, 5.0]),
+             terminal_cost_weight=np.array([5.0, 5.0, 50.0, 50.0]))
+X0 = np.array([1.152198236517471885e00, -1.266101672070702344e00, 0.0, 0.0])
+
+
+@pytest.fixture(scope="module", autouse=True)
+def _gpu():
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    torch.cuda.set_device(0)
+
+
+def _engine(K, T, **over):
+    from mppi_robotarm_amd.engine import RolloutEngine
+    from mppi_robotarm_amd.params import ArmParams
+    kw = dict(RUNPY)
+    kw.update(over)
+    return RolloutEngine(K, T, 0.006, kw["param_lambda"], kw["param_alpha"], kw["sigma"],
+                         kw["stage_cost_weight"], kw["terminal_cost_weight"], kw["param_exploration"],
+                         ArmParams(), device=0)
+
+
+def oracle_positions_and_slots(x0, u, eps_kt, win, dt, expl=0.0):
+    """fp64 end-effector positions (K, T, 2) and window slots (K, T) of the
+    reference loop control.py:91-109 (forward_dynamics = _F, then the FK and
+    argmin of _get_nearest_waypoint), for noise eps_kt (K, T, 2)."""
+    K, T, _ = eps_kt.shape
+    p = O.ArmParams()
+    exploit = np.arange(K) < (1.0 - expl) * K
+    q1, q2 = np.full(K, float(x0[0])), np.full(K, float(x0[1]))
+    dq1, dq2 = np.full(K, float(x0[2])), np.full(K, float(x0[3]))
+    pos = np.zeros((K, T, 2))
+    slot = np.zeros((K, T), dtype=np.int64)
+    for t in range(T):
+        e = eps_kt[:, t, :].astype(np.float64)
+        v1 = np.where(exploit, u[t, 0] + e[:, 0], e[:, 0])
+        v2 = np.where(exploit, u[t, 1] + e[:, 1], e[:, 1])
+        q1, q2, dq1, dq2 = O.forward_dynamics(q1, q2, dq1, dq2, v1, v2, dt, p)
+        x = p.fk_l1 * np.cos(q1) + p.fk_l2 * np.cos(q1 + q2)
+        y = p.fk_l1 * np.sin(q1) + p.fk_l2 * np.sin(q1 + q2)
+        d = ((x[:, None] - win[None, :, 0]) ** 2 + (y[:, None] - win[None, :, 1]) ** 2) * 100
+        slot[:, t] = np.argmin(d, axis=1)
+        pos[:, t, 0], pos[:, t, 1] = x, y
+    return pos, slot
+
+
+def _sqdist(pos, win):
+    """fp64 squared distances (..., W) from positions (..., 2) to window rows."""
+    return (pos[..., None, 0] - win[:, 0]) ** 2 + (pos[..., None, 1] - win[:, 1]) ** 2
+
+
+def search_tol(pos, win):
+    """Key resolution of the device search at these positions (see the module doc):
+    keys are |r'|^2 - 2 p'.r' in window-centred coordinates, quantised to 2^-18
+    of their magnitude by the index packing and rounded to fp32 (2^-24 per term);
+    the window coordinates themselves are fp32 (2^-24 |r| per coordinate)."""
+    c = win[:, :2].mean(0)
+    R = float(np.max(np.hypot(win[:, 0] - c[0], win[:, 1] - c[1])))
+    pp = np.hypot(pos[..., 0] - c[0], pos[..., 1] - c[1])
+    scale = R * R + 2.0 * pp * R
+    dist = np.sqrt(np.min(_sqdist(pos, win), axis=-1))
+    rmax = float(np.max(np.abs(win[:, :2])))
+    return 2.0 ** -16 * scale + 4 * 2.0 ** -24 * rmax * (dist + R)
+
+
+def check_indices(slot_dev, pos_dev, x0, u, eps_kt, win, dt, expl=0.0):
+    """(a) and (b) above; returns (mismatch rate vs the fp64 oracle, device-search
+    tie rate, max normalised gap of (b))."""
+    pos_dev = pos_dev.astype(np.float64)
+    # (a): the device slot at the device's own positions
+    d_dev = _sqdist(pos_dev, win)
+    best = np.min(d_dev, axis=-1)
+    got = np.take_along_axis(d_dev, slot_dev[..., None].astype(np.int64), -1)[..., 0]
+    gap_a = got - best
+    tol_a = search_tol(pos_dev, win)
+    assert np.all(gap_a <= tol_a), float(np.max(gap_a / tol_a))
+    ties_a = float(np.mean(slot_dev != np.argmin(d_dev, axis=-1)))
+    # (b): the oracle's fp64 trajectory and indices
+    pos_o, slot_o = oracle_positions_and_slots(x0, u, eps_kt, win, dt, expl)
+    mis = slot_dev != slot_o
+    rate = float(np.mean(mis))
+    if not np.any(mis):
+        return rate, ties_a, 0.0
+    d_o = _sqdist(pos_o, win)
+    gap_b = (np.take_along_axis(d_o, slot_dev[..., None].astype(np.int64), -1)[..., 0]
+             - np.take_along_axis(d_o, slot_o[..., None], -1)[..., 0])
+    dp = np.hypot(*(pos_o - pos_dev).transpose(2, 0, 1))
+    r_dev = win[slot_dev, :2]
+    r_o = win[slot_o, :2]
+    drift = dp * (np.hypot(*(pos_o - r_dev).transpose(2, 0, 1)) + np.hypot(*(pos_dev - r_dev).transpose(2, 0, 1))
+                  + np.hypot(*(pos_o - r_o).transpose(2, 0, 1)) + np.hypot(*(pos_dev - r_o).transpose(2, 0, 1)))
+    bound = drift + tol_a
+    ratio = gap_b[mis] / bound[mis]
+    assert np.all(ratio <= 1.0), float(np.max(ratio))
+    return rate, ties_a, float(np.max(ratio))
+
+
+@pytest.mark.parametrize("name", ["c1_circle_k128_t20", "runpy_k100_t30", "mid_k256_t32", "dense_k256_t24",
+                                  "expl_k128_t20"])
+def test_fixture_indices(name, paths):
+    """The reference's own fixture steps (captured from control.py): indices per (k, t)."""
+    g = load_step(name)
+    K, T = int(g["K"]), int(g["T"])
+    ref = paths[str(g["path"])]
+    prev = int(g["prev_idx_after"])
+    win = ref[prev:prev + 30]
+    eng = _engine(K, T, param_exploration=float(g["param_exploration"]), sigma=g["sigma"],
+                  param_lambda=float(g["param_lambda"]), param_alpha=float(g["param_alpha"]))
+    eng.set_step_inputs(g["x0"], win, g["u_prev"])
+    noise = eng.upload_noise(g["eps"])
+    slot, pos = eng.nearest_slots(noise)
+    rate, ties, worst = check_indices(slot, pos, g["x0"], g["u_prev"], g["eps"], win, float(g["delta_t"]),
+                                      float(g["param_exploration"]))
+    print(f"{name}: K={K} T={T} mismatches vs fp64 oracle {rate:.3e}, search ties {ties:.3e}, "
+          f"worst gap / bound {worst:.3f}")
+    eng.close()
+
+
+@pytest.mark.parametrize("converged", [False, True])
+def test_c3_window_indices(paths, converged):
+    """Config 3's workload (run.py constants, xydq_circle.txt's first window,
+    Philox noise) on 4096 of its samples at T = 64: from the initial nominal
+    [10, -2], and from the nominal after 30 fused device steps (the regime
+    bench.py times, where the samples hover near the window)."""
+    K_full, K, T = 65536, 4096, 64
+    win = paths["xydq_circle"][:30]
+    u = np.array([[10.0, -2.0]] * T)
+    eng = _engine(K_full, T)
+    eng.set_step_inputs(X0, win, u)
+    if converged:
+        for s in range(30):
+            eng.rollout(eng.philox_noise(3, 100 + s), fused_update=True)
+        u = eng.nominal()
+    noise = eng.philox_noise(3, 7)
+    slot, pos = eng.nearest_slots(noise, K)
+    eps_kt = noise[:, :K, :].cpu().numpy().transpose(1, 0, 2)
+    rate, ties, worst = check_indices(slot, pos, X0, u, eps_kt, win, 0.006)
+    print(f"c3 window (converged={converged}): mismatches vs fp64 oracle {rate:.3e} "
+          f"({int(round(rate * K * T))} of {K * T}), search ties {ties:.3e}, worst gap / bound {worst:.3f}")
+    assert rate < 1e-2
+    eng.close()

@@ -484,3 +484,135 @@ def test_dropin_short_horizons_match_oracle_controller(K, T, paths):
         np.testing.assert_allclose(opt, r_opt, rtol=1e-4, atol=1e-4)
         x = r_opt[-1].copy()
     c.close()
+
+
+@pytest.mark.parametrize("lam", [100.0, 3.0e6])
+def test_config4_eight_virtual_shards(lam, paths, monkeypatch):
+    """BASELINE config 4 at its real geometry on one device: K = 524288, T = 64,
+    sharded as 8 x 65536 (the per-GPU shard of the 8-GPU run, control.py:91-118
+    restricted to a K slice).  Each shard draws its Philox slice (== the slice of
+    the unsharded draw), rolls out into a partial row, and the 8 rows are merged
+    with the fused update; against (i) one unsharded K = 524288 launch (1e-10)
+    and (ii) the C fp64 oracle at full size (S <= 5e-5 rel, same argmin,
+    w_eps <= 1e-4).  lam = 3e6 spreads the weights over many shards.
+
+    The unsharded launch is held to the shards' 256-thread workgroups: the
+    epilogue's weights are fp32 relative to the workgroup minimum, so a different
+    workgroup partition (the default 512 threads at this K) moves w_eps by ~1e-8
+    relative, the fp32 weight rounding; with the same partition only the fp64
+    merge order differs."""
+    K, T, G = 524288, 64, 8
+    Kl = K // G
+    u = np.array([[10.0, -2.0]] * T) + np.random.default_rng(4).normal(0, 0.5, (T, 2))
+    win = _window(paths)
+    monkeypatch.setenv("MPPI_BLOCK", "256")
+    full = _engine(K, T, param_lambda=lam)
+    monkeypatch.delenv("MPPI_BLOCK")
+    assert full.threads == 256
+    assert full.handoff == "counter"     # 2048 workgroups: more than one per CU
+    full.set_step_inputs(X0, win, u)
+    noise = full.philox_noise(2024, 9)
+    S_full = torch.empty(K, dtype=torch.float64, device="cuda")
+    full.rollout(noise, S_out=S_full)
+    w_full = full.weighted_noise()
+    full.set_step_inputs(X0, win, u)
+    full.rollout(noise, fused_update=True)
+    u_full = full.nominal()
+    parts = torch.empty(G * (2 + 2 * T), dtype=torch.float64, device="cuda")
+    S_sh = torch.empty(K, dtype=torch.float64, device="cuda")
+    engs = []
+    for g in range(G):
+        e = _engine(Kl, T, K_total=K, k_offset=g * Kl, param_lambda=lam)
+        assert e.handoff == "poll" and e.lanes_per_sample == 1
+        e.set_step_inputs(X0, win, u)
+        nz = e.philox_noise(2024, 9)
+        assert torch.equal(nz, noise[:, g * Kl:(g + 1) * Kl])   # Philox slice == unsharded draw
+        e.rollout(nz, S_out=S_sh[g * Kl:(g + 1) * Kl], partial_out=parts[g * e.partial_len:(g + 1) * e.partial_len])
+        engs.append(e)
+        del nz
+    engs[0].merge(parts, G)
+    w_sh = engs[0].weighted_noise()
+    engs[0].merge(parts, G, fused_update=True)
+    u_sh = engs[0].nominal()
+    S_dev = S_sh.cpu().numpy()
+    assert np.array_equal(S_dev, S_full.cpu().numpy())          # a shard is an exact slice
+    np.testing.assert_allclose(w_sh, w_full, rtol=1e-10, atol=1e-12)
+    np.testing.assert_allclose(u_sh, u_full, rtol=1e-10, atol=1e-12)
+    eps_tk = noise.cpu().numpy()
+    ref_S = coracle.rollout_costs(X0, u, eps_tk, win, 0.006, lam, 0.98, np.eye(2) * 20.0,
+                                  RUNPY["stage_cost_weight"], RUNPY["terminal_cost_weight"], O.ArmParams(),
+                                  layout="TK")
+    rel = np.abs(S_dev - ref_S) / np.abs(ref_S)
+    assert float(np.max(rel)) < S_TOL
+    assert int(np.argmin(S_dev)) == int(np.argmin(ref_S))
+    _, ref_weps = coracle.weighted_noise(ref_S, eps_tk, lam, layout="TK")
+    assert _urel(w_sh, ref_weps) < U_TOL
+    if lam > 1e6:   # the weights really are spread over the shards
+        w = np.exp(-(ref_S - ref_S.min()) / lam)
+        assert w.sum() ** 2 / (w ** 2).sum() > 100
+        assert len({int(k) // Kl for k in np.argsort(ref_S)[:64]}) == G
+    print(f"config 4 lam={lam}: S max rel-err {float(np.max(rel)):.2e}, w_eps rel-err {_urel(w_sh, ref_weps):.2e}")
+    for e in engs + [full]:
+        e.close()
+
+
+def _runpy_ctrl(paths, K=4096, T=32, **kw):
+    from mppi_robotarm_amd.controller import MPPIControllerForPathTracking
+    return MPPIControllerForPathTracking(delta_t=0.006, ref_path=paths["xydq_circle"], horizon_step_T=T,
+                                         number_of_samples_K=K, verbose=False, **{**RUNPY, **kw})
+
+
+def test_device_noise_ticks_on_alternating_streams(paths):
+    """noise='device' draws the next tick's noise asynchronously after the read-back;
+    a caller that issues each tick on a different torch stream must still roll out
+    the finished draw (the engine makes the new stream wait for the old one)."""
+    ref = _runpy_ctrl(paths, noise="device", seed=5)
+    want = [ref.calc_control_input(X0)[1].copy() for _ in range(4)]
+    ref.close()
+    c = _runpy_ctrl(paths, noise="device", seed=5)
+    streams = [torch.cuda.Stream(), torch.cuda.Stream()]
+    for i in range(4):
+        with torch.cuda.stream(streams[i % 2]):
+            got = c.calc_control_input(X0)[1].copy()
+        assert np.array_equal(got, want[i]), i
+    c.close()
+
+
+def test_close_then_continue_redraws_device_noise(paths):
+    """close() drops the engine and its noise buffer; the next call must draw the
+    step's noise into the new buffer, not trust the old 'noise ready' mark."""
+    a = _runpy_ctrl(paths, noise="device", seed=9)
+    a.calc_control_input(X0)
+    want = a.calc_control_input(X0)[1].copy()
+    a.close()
+    b = _runpy_ctrl(paths, noise="device", seed=9)
+    b.calc_control_input(X0)
+    b.close()
+    got = b.calc_control_input(X0)[1].copy()
+    assert np.array_equal(got, want)
+    b.close()
+
+
+def test_sigma_and_lambda_reread_per_call(paths):
+    """The reference reads self.Sigma (control.py:84,106) and self.param_lambda
+    (:112) on every call, with gamma fixed at construction (:45): changing them
+    between calls must act on the next step exactly as a controller built with
+    the new values (and the constructor's gamma) would."""
+    sig2 = np.array([[12.0, 3.0], [3.0, 25.0]])
+    c = _runpy_ctrl(paths)
+    np.random.seed(1)
+    c.calc_control_input(X0)
+    c.Sigma = sig2
+    c.param_lambda = 40.0
+    u_prev, prev = c.u_prev.copy(), c.prev_waypoints_idx
+    np.random.seed(2)
+    got = c.calc_control_input(X0)[1].copy()
+    c.close()
+    oc = O.OracleController(delta_t=0.006, ref_path=paths["xydq_circle"], horizon_step_T=32,
+                            number_of_samples_K=4096, **{**RUNPY, "sigma": sig2, "param_lambda": 40.0})
+    oc.param_gamma = RUNPY["param_lambda"] * (1.0 - RUNPY["param_alpha"])   # gamma as constructed (control.py:45)
+    oc.u_prev, oc.prev_waypoints_idx = u_prev, prev
+    np.random.seed(2)
+    eps = np.random.multivariate_normal(np.zeros(2), sig2, (4096, 32)).astype(np.float32).astype(np.float64)
+    want = oc.calc_control_input(X0, epsilon=eps)[1]
+    assert _urel(got, want) < U_TOL
