@@ -94,15 +94,27 @@ def parse():
                    help="measured HBM bytes per launch (default profiles/traffic.json, c5: profiles/traffic_c5.json)")
     p.add_argument("--launch", choices=("eager", "graph"), default="eager",
                    help="N = 1: back-to-back launches from the host loop (default) or replay of a captured HIP graph")
-    p.add_argument("--backend", default="nccl", help="torch.distributed backend for N > 1 (nccl = RCCL)")
+    p.add_argument("--backend", default=None,
+                   help="torch.distributed backend for N > 1: nccl (= RCCL; default when every rank has its own GPU) "
+                        "or gloo (default when ranks share GPUs: a one-GPU rehearsal, RCCL refuses two ranks on one "
+                        "GPU)")
     p.add_argument("--exchange", choices=("auto", "launch", "rccl"), default="auto",
                    help="N > 1: partial rows exchanged inside the rollout launch (IPC inboxes over xGMI; auto: "
                         "after a one-step check against RCCL, else RCCL) or by an RCCL all_gather + merge launch")
     return p.parse_args()
 
 
+def host_cores() -> int:
+    """CPUs this process may run on (its affinity mask / cgroup share): on the GPU box
+    os.cpu_count() reports the whole host (256) while a one-GPU job is allotted 16."""
+    try:
+        return len(os.sched_getaffinity(0))
+    except AttributeError:  # pragma: no cover
+        return os.cpu_count() or 1
+
+
 def cpu_baseline(args, window, x0, u):
-    """C oracle restatement (OpenMP over samples) on the host cores, rank 0, N = 1."""
+    """C oracle restatement (OpenMP over samples) on the host cores this job may use, rank 0, N = 1."""
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import coracle  # checker / baseline only
     arm = ArmParams()
@@ -110,31 +122,36 @@ def cpu_baseline(args, window, x0, u):
     rng = np.random.default_rng(7)
     eps = (rng.standard_normal((K, T, 2)) * np.sqrt(20.0)).astype(np.float32)
     lam = 100.0
+    avail = host_cores()
+    threads = min(avail, int(os.environ.get("OMP_NUM_THREADS") or avail))
     t0 = time.perf_counter()
     n = 0
     while True:
         S = coracle.rollout_costs(x0, u, eps, window, 0.006, lam, 0.98, np.eye(2) * 20.0,
-                                  [0.5, 0.5, 5.0, 5.0], [5.0, 5.0, 50.0, 50.0], arm)
+                                  [0.5, 0.5, 5.0, 5.0], [5.0, 5.0, 50.0, 50.0], arm, nthreads=threads)
         coracle.weighted_noise(S, eps, lam)
         n += 1
         el = time.perf_counter() - t0
-        if el >= args.cpu_seconds:
+        if el >= args.cpu_seconds / 2:
             break
-    out = {"value": K * T * n / el, "unit": "state-steps/s", "cores": coracle.max_threads(),
+    out = {"value": K * T * n / el, "unit": "state-steps/s", "cores": threads,
            "kind": "port",
            "sample": f"{n} full steps of K={K} T={T} (rollout+cost+softmin+weighted noise), "
-                     f"C fp64 restatement oracle/mppi_oracle.c, OpenMP, {el:.1f} s",
-           "os_cpu_count": os.cpu_count(), "OMP_NUM_THREADS": os.environ.get("OMP_NUM_THREADS")}
-    out["numpy_fp64_1thread"] = numpy_baseline(eps, window, x0, u, lam, max(1.0, args.cpu_seconds / 4))
+                     f"C fp64 restatement oracle/mppi_oracle.c, OpenMP on {threads} threads, {el:.1f} s",
+           "cores_available": avail, "os_cpu_count": os.cpu_count(),
+           "OMP_NUM_THREADS": os.environ.get("OMP_NUM_THREADS"),
+           "cores_note": "threads = the CPUs in this job's affinity mask (the pool allots 16 host CPUs per GPU; "
+                         "os_cpu_count is the whole host)"}
+    out["numpy_fp64_1thread"] = numpy_baseline(eps, window, x0, u, lam, args.cpu_seconds / 2)
     return out
 
 
 def numpy_baseline(eps, window, x0, u, lam, seconds):
-    """the vectorised fp64 NumPy restatement (oracle/mppi_oracle.py), one thread, on the first
-    4096 samples of the same workload (whole steps: rollout + cost + weights + weighted noise)."""
+    """the vectorised fp64 NumPy restatement (oracle/mppi_oracle.py), one thread, on the
+    whole workload (whole steps: rollout + cost + weights + weighted noise; at least one)."""
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import mppi_oracle as O  # checker / baseline only
-    sub = np.ascontiguousarray(eps[:4096])
+    sub = eps
     Ks, T = sub.shape[0], sub.shape[1]
     t0 = time.perf_counter()
     n = 0
@@ -147,7 +164,7 @@ def numpy_baseline(eps, window, x0, u, lam, seconds):
         if el >= seconds:
             break
     return {"value": Ks * T * n / el, "unit": "state-steps/s", "cores": 1,
-            "sample": f"{n} full steps of K={Ks} T={T} (first {Ks} samples of the workload), "
+            "sample": f"{n} full steps of K={Ks} T={T} (the whole workload), "
                       f"oracle/mppi_oracle.py NumPy fp64, {el:.1f} s"}
 
 
@@ -159,37 +176,82 @@ def cpu_baseline_c5(args, window, x0, u, K, T):
     from mppi_robotarm_amd.chain import CHAIN7_SIGMA
     rng = np.random.default_rng(7)
     eps = (rng.standard_normal((T, 7, K)) * np.sqrt(np.diag(CHAIN7_SIGMA))[None, :, None]).astype(np.float32)
+    avail = host_cores()
+    threads = min(avail, int(os.environ.get("OMP_NUM_THREADS") or avail))
     t0 = time.perf_counter()
     n = 0
     while True:
         S = coracle.chain_rollout_costs(x0, u, eps, window, 0.006, 100.0, 0.98, CHAIN7_SIGMA, [0.5, 0.5, 5.0, 5.0],
-                                        [5.0, 5.0, 50.0, 50.0], chain_oracle.ChainParams(), layout="TNK")
+                                        [5.0, 5.0, 50.0, 50.0], chain_oracle.ChainParams(), layout="TNK",
+                                        nthreads=threads)
         coracle.chain_weighted_noise(S, eps, 100.0, layout="TNK")
         n += 1
         el = time.perf_counter() - t0
         if el >= args.cpu_seconds:
             break
-    return {"value": K * T * n / el, "unit": "state-steps/s", "cores": coracle.max_threads(), "kind": "port",
+    return {"value": K * T * n / el, "unit": "state-steps/s", "cores": threads, "kind": "port",
             "sample": f"{n} full steps of K={K} T={T} (7-link rollout+cost+softmin+weighted noise), C fp64 "
-                      f"restatement oracle/chain_oracle.c, OpenMP, {el:.1f} s"}
+                      f"restatement oracle/chain_oracle.c, OpenMP on {threads} threads, {el:.1f} s",
+            "cores_available": avail, "os_cpu_count": os.cpu_count()}
 
 
-def dropin_latency(K, T, device, ticks=60):
+def dropin_latency(K, T, device, ticks=100):
     """SURVEY §8(d)'s control-step latency: the wall time of the drop-in's
-    calc_control_input (host work + device noise + the fused rollout launch +
-    the host update of control.py:120-152), median over a closed loop of
-    run.py's driver (mppi_robotarm_amd.harness) at the bench's K and T."""
+    calc_control_input, median over a closed loop of run.py's driver
+    (mppi_robotarm_amd.harness, the plant stepped on the host between ticks) at
+    the bench's K and T, plus the same calls back to back (nothing between them,
+    so each call also waits for the previous call's noise draw)."""
     from mppi_robotarm_amd.harness import run_closed_loop
+    from mppi_robotarm_amd.controller import MPPIControllerForPathTracking
+    from mppi_robotarm_amd.params import runpy_config
     path = np.load(os.path.join(ROOT, "tests", "golden", "paths.npz"))["xydq_circle"][:, :4]
     rec = run_closed_loop(path, ticks=ticks, number_of_samples_K=K, horizon_step_T=T, noise="device", seed=0,
                           verbose=False, visualze_sampled_trajs=False, device=device)
     rec["controller"].close()
-    lat = rec["latency_s"][2:] * 1e3
-    return float(np.median(lat)), float(np.percentile(lat, 90))
+    lat = rec["latency_s"][3:] * 1e3
+    kw = runpy_config()
+    kw.update(number_of_samples_K=K, horizon_step_T=T, visualze_sampled_trajs=False)
+    c = MPPIControllerForPathTracking(ref_path=path, noise="device", seed=0, verbose=False, device=device, **kw)
+    x = X0_RUNPY.copy()
+    b2b = []
+    for i in range(ticks):
+        c.prev_waypoints_idx = 0
+        t0 = time.perf_counter()
+        c.calc_control_input(x)
+        b2b.append(time.perf_counter() - t0)
+    c.close()
+    b2b = np.array(b2b[3:]) * 1e3
+    return float(np.median(lat)), float(np.percentile(lat, 90)), float(np.median(b2b))
+
+
+def launch_ranks(args) -> int:
+    """`--gpus N` (N > 1) without a launcher: start N rank processes under
+    torch.distributed.run on this node (127.0.0.1) and return their exit code.
+    Runs before anything touches the GPU (device_count() does not initialise HIP
+    on this image), and starts the ranks as children rather than exec-ing."""
+    import socket
+    import subprocess
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    cmd = launcher_cmd(args.gpus, port, sys.argv[1:])
+    return subprocess.call(cmd, env=dict(os.environ, HSA_ENABLE_IPC_MODE_LEGACY="0"))
+
+
+def launcher_cmd(n: int, port: int, argv) -> list:
+    return [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
+            "--master-addr", "127.0.0.1", f"--master-port={port}", os.path.abspath(__file__)] + list(argv)
+
+
+def default_backend(world: int) -> str:
+    """nccl (RCCL over xGMI) when every rank can own a GPU, else gloo."""
+    return "nccl" if torch.cuda.device_count() >= world else "gloo"
 
 
 def main():
     args = parse()
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        sys.exit(launch_ranks(args))
     c5 = args.workload == "c5"
     if args.K is None:
         args.K = 131072 if c5 else 65536
@@ -204,6 +266,8 @@ def main():
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
     local_rank = local_rank % max(1, torch.cuda.device_count())  # rehearsal: several ranks on one GPU
     torch.cuda.set_device(local_rank)
+    if args.backend is None:
+        args.backend = default_backend(world)
     if world > 1:
         import torch.distributed as dist
         if args.backend == "nccl":
@@ -326,10 +390,15 @@ def main():
         kern_ms = whole[0].elapsed_time(whole[1]) / steps
     else:
         kern_ms = sum(a.elapsed_time(b) for a, b in ev) / steps
+    ranks_seen = 1
     if world > 1:
-        tt = torch.tensor([elapsed, kern_ms], dtype=torch.float64, device=eng.device)
+        dev = eng.device if args.backend == "nccl" else "cpu"
+        tt = torch.tensor([elapsed, kern_ms], dtype=torch.float64, device=dev)
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
         elapsed, kern_ms = float(tt[0]), float(tt[1])
+        one = torch.ones(1, dtype=torch.float64, device=dev)
+        dist.all_reduce(one, op=dist.ReduceOp.SUM)      # every rank took part in the timed region
+        ranks_seen = int(one.item())
     args.steps = steps
     eng.synchronize()   # raises if an in-launch hand-off timed out anywhere in the run (results invalid)
     u_final = eng.nominal()
@@ -351,11 +420,12 @@ def main():
             except Exception:
                 traffic = None
         out = {
-            "metric": ("MPPI rollouts/sec (K×T state-steps/s), 7-DoF chain K=131072 T=128 (BASELINE config 5)" if c5
-                       else "MPPI rollouts/sec (K×T state-steps/s) + control-step latency, K=65536 T=64"),
+            "metric": (f"MPPI rollouts/sec (K×T state-steps/s), 7-DoF chain K={K_total} T={T} (BASELINE config 5)"
+                       if c5 else f"MPPI rollouts/sec (K×T state-steps/s) + control-step latency, K={K} T={T}"),
             "value": value,
             "unit": "state-steps/s",
-            "n_gpus": world,
+            "n_gpus": dist.get_world_size() if world > 1 else 1,
+            "ranks_seen": ranks_seen,
             "steps": args.steps,
             "warmup": args.warmup, "settle_ms": args.settle_ms,
             "ms_per_step": ms_per_step,
@@ -375,6 +445,7 @@ def main():
                                     f"xydq_circle.txt window, Philox N(0,20I) noise x{args.nbuf} buffers"),
                        "K_total": K_total, "K_per_gpu": K, "T": T,
                        "lanes_per_sample": 1 if c5 else eng.lanes_per_sample,
+                       "exchange": xmode, "backend": args.backend if world > 1 else None,
                        "parallelism": (f"samples sharded x{world}, " + (
                            "partial rows exchanged inside the rollout launch (IPC inboxes over xGMI)"
                            if xmode == "launch" else "RCCL all_gather of partials + merge launch")) if world > 1
@@ -385,12 +456,17 @@ def main():
             "valu_roofline": valu,
         }
         if world == 1 and not c5:
-            med, p90 = dropin_latency(K, T, local_rank)
+            med, p90, b2b = dropin_latency(K, T, local_rank)
             out["control_step_latency_ms"] = med
             out["control_step_latency_p90_ms"] = p90
-            out["control_step_latency_def"] = ("median wall time of MPPIControllerForPathTracking.calc_control_input "
-                                               "(drop-in, noise='device', host update included) in run.py's closed "
-                                               "loop at this K, T; ms_per_step is the device-resident loop")
+            out["control_step_latency_back_to_back_ms"] = b2b
+            out["control_step_latency_def"] = (
+                "median wall time of MPPIControllerForPathTracking.calc_control_input (drop-in, noise='device') "
+                "in run.py's closed loop at this K, T: stage inputs, one fused launch (rollouts, soft-min, "
+                "weighted noise, median filter, update, shift), wait on its host-mapped result, fp64 optimal "
+                "trajectory on the host; the next tick's Philox draw is queued behind the launch and overlaps the "
+                "plant step between ticks. back_to_back: the same calls with nothing between them (each then "
+                "also waits for the previous draw). ms_per_step is the device-resident loop")
         if world == 1 and args.cpu_seconds > 0:
             out["cpu_baseline"] = (cpu_baseline_c5(args, window, x0, u, K, T) if c5
                                    else cpu_baseline(args, window, x0, u))

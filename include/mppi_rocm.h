@@ -37,6 +37,9 @@ extern "C" {
                                    /* shift (control.py:122-149) on device                */
 #define MPPI_FLAG_EXCHANGE 2u      /* multi-GPU: the launch exchanges the ranks' partial  */
                                    /* rows itself and merges them (mppi_exchange_attach)  */
+#define MPPI_FLAG_HOST_OUT 4u      /* with FUSED_UPDATE: the final workgroup also writes   */
+                                   /* the shifted nominal to host-mapped memory; read it  */
+                                   /* with mppi_wait_outputs (no copy, no stream sync)    */
 #define MPPI_IPC_HANDLE_BYTES 64   /* hipIpcMemHandle_t                                    */
 #define MPPI_MAX_WORLD 8           /* ranks of one node for the in-launch exchange         */
 
@@ -153,6 +156,38 @@ int mppi_optimal_traj(mppi_ctx *ctx, float *out_dev);
  * traj_dev is not NULL, the fp32 [T][4] trajectory it holds into traj_host. */
 int mppi_get_step_outputs(mppi_ctx *ctx, double *u_host, const float *traj_dev, float *traj_host);
 
+/* The optimal trajectory of control.py:129-134 on the host in fp64 from the
+ * updated controls u_new[T][2] (before the shift): x_{t+1} = _F(x_t, u_new[t-1])
+ * from x0[4], _F as control.py:234-263 (the context's arm constants and
+ * delta_t).  O(T) host work; traj_out[T][4] fp64. */
+int mppi_optimal_traj_host(const mppi_ctx *ctx, const double *x0, const double *u_new, double *traj_out);
+
+/* Wait for the last MPPI_FLAG_HOST_OUT launch (mppi_rollout or
+ * mppi_merge_partials) to publish its outputs (a spin on a host-mapped flag
+ * word), then return the shifted nominal u_out[T][2] fp64 and, if traj_out is
+ * not NULL, the fp64 optimal trajectory from x0 (as mppi_optimal_traj_host on
+ * the update's u_new). */
+int mppi_wait_outputs(mppi_ctx *ctx, const double *x0, double *u_out, double *traj_out);
+
+/* The whole single-device control step of calc_control_input (control.py:81-152)
+ * in one call, for the drop-in: stage x0, the window and the nominal u[T][2]
+ * (NULL: keep the device-resident one), launch the fused rollout + update on
+ * noise_dev ([T][K_local][2] fp32; S_dev nullable), wait until the launch's final
+ * workgroup has written the shifted nominal to coherent host-mapped memory (a
+ * spin on its flag word: no copy, no stream synchronise), return it in
+ * u_out[T][2] fp64 (the new self.u_prev), and, if traj_out is not NULL, the
+ * optimal trajectory of control.py:129-134 (off-by-one u_new[t-1]) in fp64
+ * computed on the host from the update (O(T): one re-roll of _F,
+ * control.py:234-263, in fp64 like the reference).  If next_noise_dev is not
+ * NULL, the next step's Philox noise (seed, next_step) is queued into it right
+ * after the rollout launch (stream-ordered behind it: the draw runs once the
+ * rollout has read noise_dev, which may be the same buffer), so it overlaps the
+ * host's remaining work and the caller's.  Needs T >= 5
+ * (device median filter) and a single device (no exchange attached). */
+int mppi_step_dropin(mppi_ctx *ctx, const double *x0, const double *window, int W, const double *u,
+                     const float *noise_dev, double *S_dev, float *next_noise_dev, unsigned long long seed,
+                     unsigned long long next_step, double *u_out, double *traj_out);
+
 /* Counter-based Philox4x32-10 Gaussian noise with covariance Sigma (replaces
  * np.random.multivariate_normal, control.py:163, for device-resident runs; not
  * bit-equal to NumPy).  Values depend only on (seed, step, t, global k), so a
@@ -168,6 +203,12 @@ int mppi_sync(mppi_ctx *ctx);
 /* Diagnostics: in a -DMPPI_STAMPS build the rollout kernel writes a per-workgroup
  * timeline (16 uint64 per workgroup) to dbg_dev; product builds ignore it. */
 int mppi_debug_set_buffer(mppi_ctx *ctx, void *dbg_dev);
+
+/* Diagnostics: host-side phase ends (microseconds from entry) of the last
+ * mppi_step_dropin: [0] inputs staged, [1] rollout launched, [2] next noise
+ * queued, [3] the rollout's outputs seen in host memory, [4] outputs copied +
+ * trajectory. */
+int mppi_debug_dropin_times(const mppi_ctx *ctx, double *us_out);
 
 /* Tests: the nearest window slot of the first K samples at every step, as the
  * rollout evaluates it (_get_nearest_waypoint inside _c, control.py:176-180 and

@@ -20,6 +20,8 @@ MPPI_E_HIP = -2
 MPPI_E_SINGULAR = -3
 MPPI_FLAG_FUSED_UPDATE = 1
 MPPI_FLAG_EXCHANGE = 2
+MPPI_FLAG_HOST_OUT = 4
+DP = C.POINTER(C.c_double)
 MPPI_IPC_HANDLE_BYTES = 64
 MPPI_MAX_WORLD = 8
 
@@ -28,9 +30,11 @@ EXPORTS = (
     "mppi_ctx_create", "mppi_ctx_destroy", "mppi_last_error", "mppi_set_stream", "mppi_ctx_info", "mppi_ctx_handoff",
     "mppi_set_step_inputs", "mppi_rollout", "mppi_merge_partials", "mppi_exchange_handle", "mppi_exchange_attach",
     "mppi_get_weighted_noise",
-    "mppi_get_nominal", "mppi_rollout_traj", "mppi_optimal_traj", "mppi_get_step_outputs", "mppi_noise_philox",
+    "mppi_get_nominal", "mppi_rollout_traj", "mppi_optimal_traj", "mppi_get_step_outputs", "mppi_step_dropin",
+    "mppi_optimal_traj_host", "mppi_wait_outputs",
+    "mppi_noise_philox",
     "mppi_sync", "mppi_debug_set_buffer",
-    "mppi_debug_nearest",
+    "mppi_debug_nearest", "mppi_debug_dropin_times",
     "mppi_chain_ctx_create", "mppi_chain_ctx_destroy", "mppi_chain_set_stream", "mppi_chain_ctx_info",
     "mppi_chain_set_step_inputs", "mppi_chain_rollout", "mppi_chain_merge_partials", "mppi_chain_exchange_handle",
     "mppi_chain_exchange_attach",
@@ -102,9 +106,14 @@ def open_library(path: str):
         "mppi_rollout_traj": ([vp, dp, fp, C.c_int, fp], C.c_int),
         "mppi_optimal_traj": ([vp, fp], C.c_int),
         "mppi_get_step_outputs": ([vp, dp, fp, fp], C.c_int),
+        "mppi_optimal_traj_host": ([vp, dp, dp, dp], C.c_int),
+        "mppi_wait_outputs": ([vp, dp, dp, dp], C.c_int),
+        # raw addresses (ints) for every pointer: the per-step hot call skips ctypes pointer objects
+        "mppi_step_dropin": ([vp, vp, vp, C.c_int, vp, vp, vp, vp, C.c_ulonglong, C.c_ulonglong, vp, vp], C.c_int),
         "mppi_noise_philox": ([vp, C.c_ulonglong, C.c_ulonglong, fp], C.c_int),
         "mppi_sync": ([vp], C.c_int),
         "mppi_debug_set_buffer": ([vp, vp], C.c_int),
+        "mppi_debug_dropin_times": ([vp, dp], C.c_int),
         "mppi_debug_nearest": ([vp, fp, C.c_int, vp, fp], C.c_int),
         "mppi_chain_ctx_create": ([C.POINTER(ChainConfigC), C.c_int, vp, C.POINTER(vp)], C.c_int),
         "mppi_chain_ctx_destroy": ([vp], None),

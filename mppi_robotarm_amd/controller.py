@@ -123,8 +123,8 @@ class MPPIControllerForPathTracking:
                 np.asarray(self.terminal_cost_weight, dtype=np.float64).tobytes(), float(self.param_exploration),
                 float(self.delta_t))
 
-    def _get_engine(self) -> RolloutEngine:
-        key = self._engine_key()
+    def _get_engine(self, key=None) -> RolloutEngine:
+        key = self._engine_key() if key is None else key
         if self._engine is not None and key != self._engine_built_for:
             self.close()             # an attribute the engine baked in changed: rebuild, as the reference re-reads it
         if self._engine is None:
@@ -167,8 +167,10 @@ class MPPIControllerForPathTracking:
         else:
             epsilon = None
             self._check_sigma(self.Sigma, self.dim_u)
-        np.linalg.inv(self.Sigma)                          # LinAlgError exactly as control.py:106
-        eng = self._get_engine()
+        key = self._engine_key()
+        if key != self._engine_built_for:
+            np.linalg.inv(self.Sigma)                      # LinAlgError exactly as control.py:106
+        eng = self._get_engine(key)
         if epsilon is not None:
             lo = eng.k_offset
             eng.upload_noise(epsilon[lo:lo + eng.K_local], out=self._noise_dev)
@@ -177,10 +179,12 @@ class MPPIControllerForPathTracking:
         self._step_count += 1
 
         window = self.ref_path[self.prev_waypoints_idx:(self.prev_waypoints_idx + SEARCH_IDX_LEN)]
-        eng.set_step_inputs(np.asarray(x0, dtype=np.float64), window, u)
         world, _ = self._shard()
+        if not self.host_update and world == 1 and not self.visualze_sampled_trajs:
+            return self._dropin_step(eng, x0, window, u)
+        eng.set_step_inputs(np.asarray(x0, dtype=np.float64), window, u)
         if not self.host_update:
-            return self._fused_step(eng, u, world)
+            return self._fused_step(eng, x0, u, world)
         if world == 1:
             eng.rollout(self._noise_dev, S_out=self._S_dev if self.keep_costs else None)
         else:
@@ -196,7 +200,7 @@ class MPPIControllerForPathTracking:
 
         optimal_traj = np.zeros((self.T, self.dim_x))
         if self.visualize_optimal_traj:
-            optimal_traj = eng.trajectories(base_u=u, K=1)[0].double().cpu().numpy()
+            optimal_traj = eng.optimal_traj_host(x0, u)
 
         sampled_traj_list = np.zeros((self.K, self.T, self.dim_x))
         if self.visualze_sampled_trajs:
@@ -215,24 +219,44 @@ class MPPIControllerForPathTracking:
         self._prefetch_noise(eng)
         return u[0], u, optimal_traj, sampled_traj_list
 
-    def _fused_step(self, eng: RolloutEngine, u: np.ndarray, world: int):
-        """control.py:81-152 with the update inside the launch: rollouts + merge +
-        median filter + u += w_eps + shift on device, the optimal trajectory from the
-        updated controls, one read-back.  u is self.u_prev (updated in place)."""
+    def _dropin_step(self, eng: RolloutEngine, x0, window, u: np.ndarray):
+        """control.py:81-152 on one device in one native call (mppi_step_dropin):
+        rollouts + soft-min + weighted noise + median filter + u += w_eps + shift in
+        the launch, the result read from host-mapped memory, the optimal trajectory
+        in fp64 on the host from the update, then the next step's device noise queued
+        behind the rollout.  u is self.u_prev (updated in place)."""
+        nxt = self._noise_dev if self.noise_source == "device" else None
+        u_new, traj = eng.step_dropin(x0, window, u, self._noise_dev,
+                                      S_out=self._S_dev if self.keep_costs else None, next_noise=nxt,
+                                      seed=self.seed, next_step=self._step_count,
+                                      want_traj=self.visualize_optimal_traj)
+        if nxt is not None:
+            self._noise_ready = (self.seed, self._step_count)
+        if self.keep_costs:
+            self.last_S = self._S_dev.cpu().numpy()
+        u[:] = u_new                                       # the shifted nominal, in place (aliasing kept)
+        optimal_traj = traj if traj is not None else np.zeros((self.T, self.dim_x))
+        return u[0], u, optimal_traj, np.zeros((self.K, self.T, self.dim_x))
+
+    def _fused_step(self, eng: RolloutEngine, x0, u: np.ndarray, world: int):
+        """control.py:81-152 with the update inside the launch (the multi-GPU merge
+        launch, or the rollout when sampled trajectories are asked for): median filter
+        + u += w_eps + shift on device, the result read from host-mapped memory, the
+        optimal trajectory in fp64 on the host from the update.  u is self.u_prev
+        (updated in place)."""
         S_out = self._S_dev if self.keep_costs else None
         u_before = u.copy() if self.visualze_sampled_trajs else None
         if world == 1:
-            eng.rollout(self._noise_dev, S_out=S_out, fused_update=True)
+            eng.rollout(self._noise_dev, S_out=S_out, fused_update=True, host_out=True)
         else:
             eng.rollout(self._noise_dev, S_out=S_out, partial_out=self._partial)
             exchange_partials(self._partial, self._gathered, self.process_group)
-            eng.merge(self._gathered, world, fused_update=True)
-        traj = eng.optimal_traj(out=self._traj_dev) if self.visualize_optimal_traj else None
+            eng.merge(self._gathered, world, fused_update=True, host_out=True)
         sampled_traj_list = np.zeros((self.K, self.T, self.dim_x))
         tr = None
         if self.visualze_sampled_trajs:
             tr = eng.trajectories(base_u=u_before, noise=self._noise_dev)   # pre-update u, v[k, t-1]
-        u_new, traj_host = eng.step_outputs(traj)
+        u_new, traj = eng.wait_outputs(x0 if self.visualize_optimal_traj else None)
         if self.keep_costs:
             self.last_S = self._S_dev.cpu().numpy()
         if tr is not None:
@@ -245,10 +269,10 @@ class MPPIControllerForPathTracking:
             else:
                 sampled_traj_list[:] = tr.double().cpu().numpy()
         # next step's noise after the last read-back: the draw overlaps the caller's
-        # work between ticks instead of sitting in front of this call's synchronise
+        # work between ticks instead of sitting in front of this call's wait
         self._prefetch_noise(eng)
         u[:] = u_new                                       # the shifted nominal, in place (aliasing kept)
-        optimal_traj = traj_host.astype(np.float64) if traj is not None else np.zeros((self.T, self.dim_x))
+        optimal_traj = traj if traj is not None else np.zeros((self.T, self.dim_x))
         return u[0], u, optimal_traj, sampled_traj_list
 
     def _prefetch_noise(self, eng: RolloutEngine) -> None:

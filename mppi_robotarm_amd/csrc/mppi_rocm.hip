@@ -33,6 +33,7 @@
 #include <stdlib.h>
 #include <string.h>
 
+#include <chrono>
 #include <string>
 #include <type_traits>
 
@@ -118,35 +119,56 @@ __device__ __forceinline__ double nominal_first(const DevStep* st, int tid) {
     return tid < 2 ? st->u[0][tid] : 0.0;
 }
 
+// Host-mapped outputs of a drop-in step (mppi_step_dropin): hout (device view
+// of coherent pinned host memory, nullable) receives
+//   [0] flag word (= seq once the rest is written), [2..3] u_new[0],
+//   [4 .. 4 + 2T) the shifted nominal u_next[t][d],
+// so the host reads the step's result without a copy or a stream synchronise.
+struct HostOut {
+    double* p;
+    unsigned seq;
+};
+
 // upd (nullable): the updated, not yet shifted controls u_new[t] in fp32, the
 // base of the optimal trajectory (control.py:129-134, mppi_optimal_traj):
 // u_new[t + 1] is this thread's shifted element, u_new[0] one more median.
+// Every thread of the workgroup must call it (it ends with a barrier when
+// host outputs are requested).
 template <int NT>
 __device__ void nominal_update_block(DevStep* nxt, const KConst& c, Scratch& sm, double u_src, double u_first,
-                                     float* upd) {
+                                     float* upd, HostOut ho) {
     const int tid = threadIdx.x;
     const int T = c.T;
-    if (tid >= ((2 * T + 63) & ~63)) return;   // whole waves: the DPP pairs stay complete
-    const int t = tid >> 1, d = tid & 1;
-    const int src = t + 1 < T ? t + 1 : T - 1;
-    const double un = tid < 2 * T ? u_src + median_at(sm, src, d, T, 2) : 0.0;
-    const double other = dpp_f64<0xB1>(un);   // quad_perm [1,0,3,2]: the partner element
-    if (upd && tid < 2 * T) {
-        if (t + 1 < T) upd[2 * (t + 1) + d] = (float)un;
-        if (t == 0) upd[d] = (float)(u_first + median_at(sm, 0, d, T, 2));
-    }
-    if (tid < 2 * T) {
-        nxt->u[t][d] = un;
-        if (d == 0) {
-            const double u0 = un, u1 = other;
-            const double g0 = c.gamma * u0, g1 = c.gamma * u1;
-            const double a0 = g0 * c.sig_inv[0] + g1 * c.sig_inv[2];
-            const double a1 = g0 * c.sig_inv[1] + g1 * c.sig_inv[3];
-            nxt->ua[t] = make_float4((float)u0, (float)u1, (float)a0, (float)a1);
+    if (tid < ((2 * T + 63) & ~63)) {   // whole waves: the DPP pairs stay complete
+        const int t = tid >> 1, d = tid & 1;
+        const int src = t + 1 < T ? t + 1 : T - 1;
+        const double un = tid < 2 * T ? u_src + median_at(sm, src, d, T, 2) : 0.0;
+        const double other = dpp_f64<0xB1>(un);   // quad_perm [1,0,3,2]: the partner element
+        if ((upd || ho.p) && tid < 2) {
+            const double u0 = u_first + median_at(sm, 0, d, T, 2);
+            if (upd) upd[d] = (float)u0;
+            if (ho.p) ho.p[2 + d] = u0;
+        }
+        if (tid < 2 * T) {
+            if (upd && t + 1 < T) upd[2 * (t + 1) + d] = (float)un;
+            if (ho.p) ho.p[4 + tid] = un;
+            nxt->u[t][d] = un;
+            if (d == 0) {
+                const double u0 = un, u1 = other;
+                const double g0 = c.gamma * u0, g1 = c.gamma * u1;
+                const double a0 = g0 * c.sig_inv[0] + g1 * c.sig_inv[2];
+                const double a1 = g0 * c.sig_inv[1] + g1 * c.sig_inv[3];
+                nxt->ua[t] = make_float4((float)u0, (float)u1, (float)a0, (float)a1);
+            }
         }
     }
-    // win / key / x0 / ctr are written to both ping-pong blocks by
-    // mppi_set_step_inputs, so only the nominal moves here.
+    // win / key / x0 / ctr stay in the static part of the step block (see
+    // mppi_ctx::static_valid), so only the nominal moves here.
+    if (ho.p) {
+        __threadfence_system();   // this thread's host stores are out before the barrier
+        __syncthreads();
+        if (tid == 0) __hip_atomic_store(reinterpret_cast<unsigned*>(ho.p), ho.seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+    }
 }
 
 // ------------------------------------------------------------ rollout kernel
@@ -167,7 +189,7 @@ __global__ __launch_bounds__(NT) void rollout_kernel(
     double* __restrict__ S_out, double* __restrict__ slab, double* __restrict__ gslab,
     unsigned* __restrict__ counters, double* __restrict__ partial_out, double* __restrict__ w_eps_out,
     DevStep* __restrict__ nxt, unsigned flags, const XDesc xd, unsigned* __restrict__ epoch, unsigned* __restrict__ tmo,
-    float* __restrict__ upd, unsigned long long* __restrict__ dbg) {
+    float* __restrict__ upd, const HostOut ho, unsigned long long* __restrict__ dbg) {
     __shared__ float4 s_win[kSlots];
     __shared__ float4 s_ua[kMaxT];   // per-step constants (u_t, a_t)
     __shared__ float s_redf[NT / 64];
@@ -465,14 +487,15 @@ __global__ __launch_bounds__(NT) void rollout_kernel(
     STAMP(11, NOW());
     STAMP(6, (unsigned long long)sm.nrel);
     if (flags & MPPI_FLAG_EXCHANGE) exchange_merge<NT, 1>(xd, geo, c.inv_lambda, sm, w_eps_out, tmo);
-    if (flags & MPPI_FLAG_FUSED_UPDATE) nominal_update_block<NT>(nxt, c, sm, u_cur, u_first, upd);
+    if (flags & MPPI_FLAG_FUSED_UPDATE) nominal_update_block<NT>(nxt, c, sm, u_cur, u_first, upd, ho);
     STAMP(7, NOW());
 }
 
 // Merge of the all-gathered per-device rows (multi-GPU), plus the fused update.
 template <int NT>
 __global__ __launch_bounds__(NT) void merge_kernel(const KConst c, const double* parts, int n, double* w_eps_out,
-                                                   const DevStep* cur, DevStep* nxt, unsigned flags, float* upd) {
+                                                   const DevStep* cur, DevStep* nxt, unsigned flags, float* upd,
+                                                   const HostOut ho) {
     __shared__ Scratch sm;
     const int tid = threadIdx.x;
     const double u_cur = (flags & MPPI_FLAG_FUSED_UPDATE) ? nominal_src(cur, tid, c.T) : 0.0;
@@ -480,7 +503,7 @@ __global__ __launch_bounds__(NT) void merge_kernel(const KConst c, const double*
     const __amdgpu_buffer_rsrc_t r = rows_rsrc(parts, n * (2 + 2 * c.T) * 8);
     merge_rows_block<NT, 1, true, false>(r, 0, n, RowGeo(2 * c.T), c.inv_lambda, sm, nullptr, 0, nullptr, w_eps_out,
                                          0u, nullptr);
-    if (flags & MPPI_FLAG_FUSED_UPDATE) nominal_update_block<NT>(nxt, c, sm, u_cur, u_first, upd);
+    if (flags & MPPI_FLAG_FUSED_UPDATE) nominal_update_block<NT>(nxt, c, sm, u_cur, u_first, upd, ho);
 }
 
 // Trajectory re-roll (control.py:129-145): control(t) = base[(t-1) mod T] (+ eps).
@@ -578,8 +601,16 @@ struct mppi_ctx {
     KConst kc;
     DevStep* d_step = nullptr;  // [2] ping-pong
     int cur = 0;
+    // static part (win, key, x0, ctr) up to date in block i; the drop-in stages
+    // one block per step (one copy), the others fetch it on demand (ensure_static)
+    bool static_valid[2] = {false, false};
     DevStep* h_step = nullptr;  // pinned staging
     hipEvent_t staged = nullptr;
+    bool stage_pending = false;     // a staging copy may still be reading h_step
+    double* h_dout = nullptr;       // coherent host-mapped drop-in outputs (HostOut layout)
+    double* d_dout = nullptr;       // its device view
+    unsigned dseq = 0;
+    double dropin_us[6] = {};       // phase ends of the last mppi_step_dropin (mppi_debug_dropin_times)
     double* d_slab = nullptr;
     double* d_gslab = nullptr;
     unsigned* d_counter = nullptr;  // [ngroups + 1] arrival counters (counter hand-off), then the epoch word
@@ -772,6 +803,9 @@ int mppi_ctx_create(const mppi_config* cfg, int device, void* stream, mppi_ctx**
         (e = hipHostMalloc(&c->h_buf, 2 * kMaxT * sizeof(double), hipHostMallocDefault)) != hipSuccess ||
         (e = hipHostMalloc(&c->h_base, kMaxT * sizeof(float2), hipHostMallocDefault)) != hipSuccess ||
         (e = hipHostMalloc(&c->h_tmo, 256, hipHostMallocMapped)) != hipSuccess ||
+        (e = hipHostMalloc(&c->h_dout, (4 + 2 * kMaxT) * sizeof(double), hipHostMallocMapped | hipHostMallocCoherent)) !=
+            hipSuccess ||
+        (e = hipHostGetDevicePointer((void**)&c->d_dout, c->h_dout, 0)) != hipSuccess ||
         (e = hipHostGetDevicePointer((void**)&c->d_tmo, c->h_tmo, 0)) != hipSuccess ||
         (e = hipEventCreateWithFlags(&c->staged, hipEventDisableTiming)) != hipSuccess ||
         (e = hipMemset(c->d_counter, 0, ctr_bytes)) != hipSuccess ||
@@ -782,6 +816,7 @@ int mppi_ctx_create(const mppi_config* cfg, int device, void* stream, mppi_ctx**
         (e = hipDeviceSynchronize()) != hipSuccess)
         return cleanup_fail(fail(MPPI_E_HIP, std::string("allocation: ") + hipGetErrorString(e)));
     memset(c->h_step, 0, sizeof(DevStep));
+    memset(c->h_dout, 0, (4 + 2 * kMaxT) * sizeof(double));
     *c->h_tmo = 0;
     c->d_epoch = c->d_counter + ngroups + 1;
     *out = c;
@@ -809,6 +844,7 @@ void mppi_ctx_destroy(mppi_ctx* c) {
     if (c->h_buf) (void)hipHostFree(c->h_buf);
     if (c->h_base) (void)hipHostFree(c->h_base);
     if (c->h_tmo) (void)hipHostFree(c->h_tmo);
+    if (c->h_dout) (void)hipHostFree(c->h_dout);
     if (c->staged) (void)hipEventDestroy(c->staged);
     delete c;
 }
@@ -827,10 +863,19 @@ int mppi_ctx_info(const mppi_ctx* c, int* lps, int* blocks, int* threads) {
     return MPPI_OK;
 }
 
-int mppi_set_step_inputs(mppi_ctx* c, const double* x0, const double* window, int W, const double* u) {
-    if (!c || !x0 || !window) return fail(MPPI_E_ARG, "null argument");
+}  // extern "C"
+
+namespace {
+
+// Fill the pinned staging block from the host inputs and copy it to the device
+// (stream-ordered).  both: the static part into both ping-pong blocks and the
+// nominal (if given) into the current one (mppi_set_step_inputs, device loops);
+// otherwise one copy: with a nominal the current block becomes block 0 and
+// takes static part + nominal contiguously (the drop-in's per-step form).
+int stage_inputs(mppi_ctx* c, const double* x0, const double* window, int W, const double* u, bool both) {
+    if (!x0 || !window) return fail(MPPI_E_ARG, "null argument");
     if (W < 1 || W > MPPI_SEARCH_LEN) return fail(MPPI_E_ARG, "window rows must be in [1, 30]");
-    HIP_TRY(hipEventSynchronize(c->staged));  // staging block free again
+    if (c->stage_pending) HIP_TRY(hipEventSynchronize(c->staged));  // staging block free again
     DevStep* h = c->h_step;
     double cx = 0.0, cy = 0.0;
     for (int j = 0; j < W; ++j) {
@@ -866,15 +911,110 @@ int mppi_set_step_inputs(mppi_ctx* c, const double* x0, const double* window, in
         }
         bytes = sizeof(DevStep);
     }
-    // static part (window, keys, x0) into both ping-pong blocks, nominal into the current one
-    HIP_TRY(hipMemcpyAsync(c->d_step + (c->cur ^ 1), h, offsetof(DevStep, ua), hipMemcpyHostToDevice, c->stream));
+    if (both) {
+        HIP_TRY(hipMemcpyAsync(c->d_step + (c->cur ^ 1), h, offsetof(DevStep, ua), hipMemcpyHostToDevice, c->stream));
+        c->static_valid[c->cur ^ 1] = true;
+    } else {
+        if (u) c->cur = 0;
+        c->static_valid[c->cur ^ 1] = false;
+    }
     HIP_TRY(hipMemcpyAsync(c->d_step + c->cur, h, bytes, hipMemcpyHostToDevice, c->stream));
+    c->static_valid[c->cur] = true;
     HIP_TRY(hipEventRecord(c->staged, c->stream));
+    c->stage_pending = true;
     return MPPI_OK;
+}
+
+// The static part of the current block before a kernel reads it: a
+// device-to-device copy from the other block if the drop-in staged only that one.
+int ensure_static(mppi_ctx* c) {
+    if (c->static_valid[c->cur]) return MPPI_OK;
+    if (!c->static_valid[c->cur ^ 1]) return MPPI_OK;   // nothing staged yet: zeros, as before
+    HIP_TRY(hipMemcpyAsync(c->d_step + c->cur, c->d_step + (c->cur ^ 1), offsetof(DevStep, ua),
+                           hipMemcpyDeviceToDevice, c->stream));
+    c->static_valid[c->cur] = true;
+    return MPPI_OK;
+}
+
+int launch_rollout(mppi_ctx* c, const float* noise_dev, double* S_dev, double* partial_dev, unsigned flags,
+                   HostOut ho);
+
+// The host-mapped output block of the next launch (MPPI_FLAG_HOST_OUT): a fresh
+// sequence number, never 0 (the flag word's initial value).
+HostOut next_host_out(mppi_ctx* c, unsigned flags) {
+    if (!(flags & MPPI_FLAG_HOST_OUT)) return HostOut{nullptr, 0u};
+    if (++c->dseq == 0) ++c->dseq;
+    return HostOut{c->d_dout, c->dseq};
+}
+
+// Wait until the last MPPI_FLAG_HOST_OUT launch has published its outputs: a spin
+// on the coherent host-mapped flag word (no interrupt, no copy); the launch's own
+// errors surface through hipStreamQuery.
+int wait_host_out(mppi_ctx* c) {
+    if (c->dseq == 0) return fail(MPPI_E_ARG, "no MPPI_FLAG_HOST_OUT launch to wait for");
+    const unsigned seq = c->dseq;
+    volatile unsigned* flag = reinterpret_cast<volatile unsigned*>(c->h_dout);
+    const auto t0 = std::chrono::steady_clock::now();
+    for (unsigned long long n = 0; __atomic_load_n(flag, __ATOMIC_ACQUIRE) != seq; ++n) {
+        if ((n & 1023) == 1023) {
+            const hipError_t e = hipStreamQuery(c->stream);
+            if (e != hipSuccess && e != hipErrorNotReady)
+                return fail(MPPI_E_HIP, std::string("fused step: ") + hipGetErrorString(e));
+            if (e == hipSuccess && __atomic_load_n(flag, __ATOMIC_ACQUIRE) != seq)
+                return fail(MPPI_E_HIP, "fused step finished without publishing its outputs");
+            if (std::chrono::steady_clock::now() - t0 > std::chrono::seconds(30))
+                return fail(MPPI_E_HIP, "fused step: no result after 30 s");
+        }
+        __builtin_ia32_pause();
+    }
+    c->stage_pending = false;   // the launch ran, so every staging copy before it did too
+    return check_timeout(c);
+}
+
+// _F (control.py:234-263) in fp64 on the host: the mass matrix as written, its
+// closed-form 2x2 inverse (np.linalg.inv), semi-implicit Euler.  Used for the one
+// optimal trajectory of a drop-in step (control.py:129-134), O(T) host work.
+void host_F(const mppi_arm_params& a, double dt, double* x, double u1, double u2) {
+    const double q1 = x[0], q2 = x[1], dq1 = x[2], dq2 = x[3];
+    const double c2 = cos(q2);
+    const double M11 = a.m1 * a.lc1 * a.lc1 + a.l1 + a.m2 * (a.l1 * a.l1 + a.lc2 * a.lc2 + 2 * a.l1 * a.lc2 * c2) + a.l2;
+    const double M22 = a.m2 * a.lc2 * a.lc2 + a.l2;
+    const double M12 = a.m2 * a.l1 * a.lc2 * c2 + a.m2 * a.lc2 * a.lc2 + a.l2;
+    const double h = a.m2 * a.l1 * a.lc2 * sin(q2);
+    const double g1 = a.m1 * a.lc1 * a.g * cos(q1) + a.m2 * a.g * (a.lc2 * cos(q1 + q2) + a.l1 * cos(q1));
+    const double g2 = a.m2 * a.lc2 * a.g * cos(q1 + q2);
+    const double r1 = u1 - ((-h * dq2) * dq1 + (-h * dq1 - h * dq2) * dq2) - g1;
+    const double r2 = u2 - ((h * dq1) * dq1 + 0.0 * dq2) - g2;
+    const double det = M11 * M22 - M12 * M12;
+    const double ddq1 = (M22 * r1 - M12 * r2) / det;
+    const double ddq2 = (-M12 * r1 + M11 * r2) / det;
+    x[2] = dq1 + ddq1 * dt;
+    x[3] = dq2 + ddq2 * dt;
+    x[0] = q1 + x[2] * dt;
+    x[1] = q2 + x[3] * dt;
+}
+
+}  // namespace
+
+extern "C" {
+
+int mppi_set_step_inputs(mppi_ctx* c, const double* x0, const double* window, int W, const double* u) {
+    if (!c) return fail(MPPI_E_ARG, "null argument");
+    return stage_inputs(c, x0, window, W, u, true);
 }
 
 int mppi_rollout(mppi_ctx* c, const float* noise_dev, double* S_dev, double* partial_dev, unsigned flags) {
     if (!c || !noise_dev) return fail(MPPI_E_ARG, "null argument");
+    if ((flags & MPPI_FLAG_HOST_OUT) && !(flags & MPPI_FLAG_FUSED_UPDATE))
+        return fail(MPPI_E_ARG, "MPPI_FLAG_HOST_OUT needs MPPI_FLAG_FUSED_UPDATE");
+    return launch_rollout(c, noise_dev, S_dev, partial_dev, flags, next_host_out(c, flags));
+}
+
+}  // extern "C"
+
+namespace {
+int launch_rollout(mppi_ctx* c, const float* noise_dev, double* S_dev, double* partial_dev, unsigned flags,
+                   HostOut ho) {
     if ((flags & MPPI_FLAG_FUSED_UPDATE) && c->cfg.T < 5)
         return fail(MPPI_E_ARG, "device median filter needs T >= 5 (use the host update)");
     if (flags & MPPI_FLAG_EXCHANGE) {
@@ -882,13 +1022,14 @@ int mppi_rollout(mppi_ctx* c, const float* noise_dev, double* S_dev, double* par
         if (partial_dev) return fail(MPPI_E_ARG, "MPPI_FLAG_EXCHANGE merges on device: no partial_out");
         partial_dev = c->d_xrow;
     }
+    if (int rc = ensure_static(c)) return rc;
     const DevStep* cur = c->d_step + c->cur;
     DevStep* nxt = c->d_step + (c->cur ^ 1);
     const float2* nz = reinterpret_cast<const float2*>(noise_dev);
 #define MPPI_LAUNCH(L, NTH, P)                                                                                   \
     hipLaunchKernelGGL((rollout_kernel<L, NTH, P>), dim3(c->nblocks), dim3(NTH), 0, c->stream, c->kc, cur, nz, S_dev,  \
                        c->d_slab, c->d_gslab, c->d_counter, partial_dev, c->d_weps, nxt, flags, c->xd, c->d_epoch,       \
-                       c->d_tmo, reinterpret_cast<float*>(c->d_upd), c->d_dbg)
+                       c->d_tmo, reinterpret_cast<float*>(c->d_upd), ho, c->d_dbg)
 #define MPPI_LAUNCH_P(L, NTH)                \
     do {                                     \
         if (c->poll) MPPI_LAUNCH(L, NTH, true);  \
@@ -912,6 +1053,9 @@ int mppi_rollout(mppi_ctx* c, const float* noise_dev, double* S_dev, double* par
     }
     return rc;
 }
+}  // namespace
+
+extern "C" {
 
 int mppi_exchange_handle(mppi_ctx* c, int world, void* handle_out) {
     if (!c || !handle_out || world < 1 || world > kMaxWorld) return fail(MPPI_E_ARG, "bad argument");
@@ -960,15 +1104,18 @@ int mppi_merge_partials(mppi_ctx* c, const double* partials_dev, int n, unsigned
     if (!c || !partials_dev || n < 1) return fail(MPPI_E_ARG, "bad argument");
     if ((flags & MPPI_FLAG_FUSED_UPDATE) && c->cfg.T < 5)
         return fail(MPPI_E_ARG, "device median filter needs T >= 5 (use the host update)");
+    if ((flags & MPPI_FLAG_HOST_OUT) && !(flags & MPPI_FLAG_FUSED_UPDATE))
+        return fail(MPPI_E_ARG, "MPPI_FLAG_HOST_OUT needs MPPI_FLAG_FUSED_UPDATE");
     const DevStep* cur = c->d_step + c->cur;
     DevStep* nxt = c->d_step + (c->cur ^ 1);
+    const HostOut ho = next_host_out(c, flags);
     // one workgroup, one thread per merged column (2T + 1 <= 256 up to T = 127)
     if (2 * c->cfg.T + 1 <= 256)
         hipLaunchKernelGGL(merge_kernel<256>, dim3(1), dim3(256), 0, c->stream, c->kc, partials_dev, n, c->d_weps,
-                           cur, nxt, flags, reinterpret_cast<float*>(c->d_upd));
+                           cur, nxt, flags, reinterpret_cast<float*>(c->d_upd), ho);
     else
         hipLaunchKernelGGL(merge_kernel<512>, dim3(1), dim3(512), 0, c->stream, c->kc, partials_dev, n, c->d_weps,
-                           cur, nxt, flags, reinterpret_cast<float*>(c->d_upd));
+                           cur, nxt, flags, reinterpret_cast<float*>(c->d_upd), ho);
     const int rc = launch_check("merge_kernel");
     if (rc == MPPI_OK && (flags & MPPI_FLAG_FUSED_UPDATE)) {
         c->cur ^= 1;
@@ -998,6 +1145,7 @@ int mppi_get_nominal(mppi_ctx* c, double* u_host) {
 
 int mppi_rollout_traj(mppi_ctx* c, const double* base_u, const float* noise_dev, int K, float* out_dev) {
     if (!c || !out_dev || K < 1 || K > c->cfg.K_local) return fail(MPPI_E_ARG, "bad argument");
+    if (int rc = ensure_static(c)) return rc;
     const DevStep* cur = c->d_step + c->cur;
     const float2* base;
     if (base_u) {
@@ -1021,6 +1169,7 @@ int mppi_rollout_traj(mppi_ctx* c, const double* base_u, const float* noise_dev,
 int mppi_optimal_traj(mppi_ctx* c, float* out_dev) {
     if (!c || !out_dev) return fail(MPPI_E_ARG, "null argument");
     if (!c->upd_valid) return fail(MPPI_E_ARG, "mppi_optimal_traj needs a preceding MPPI_FLAG_FUSED_UPDATE launch");
+    if (int rc = ensure_static(c)) return rc;
     // x0 and the window are in both ping-pong blocks, so the current one serves
     hipLaunchKernelGGL(traj_kernel, dim3(1), dim3(kThreads), 0, c->stream, c->kc, c->d_step + c->cur, c->d_upd,
                        (const float2*)nullptr, 1, reinterpret_cast<float4*>(out_dev));
@@ -1039,6 +1188,62 @@ int mppi_get_step_outputs(mppi_ctx* c, double* u_host, const float* traj_dev, fl
     memcpy(u_host, c->h_out, ub);
     if (traj_dev) memcpy(traj_host, h_traj, tb);
     return check_timeout(c);
+}
+
+int mppi_optimal_traj_host(const mppi_ctx* c, const double* x0, const double* u_new, double* traj_out) {
+    if (!c || !x0 || !u_new || !traj_out) return fail(MPPI_E_ARG, "null argument");
+    // control.py:129-134: x_{t+1} = _F(x_t, u_new[t - 1]), u_new[-1] = u_new[T - 1]
+    const int T = c->cfg.T;
+    double x[4] = {x0[0], x0[1], x0[2], x0[3]};
+    for (int t = 0; t < T; ++t) {
+        const double* ut = u_new + 2 * (t == 0 ? T - 1 : t - 1);
+        host_F(c->cfg.arm, c->cfg.delta_t, x, ut[0], ut[1]);
+        memcpy(traj_out + 4 * t, x, sizeof(x));
+    }
+    return MPPI_OK;
+}
+
+int mppi_wait_outputs(mppi_ctx* c, const double* x0, double* u_out, double* traj_out) {
+    if (!c || !u_out || (traj_out && !x0)) return fail(MPPI_E_ARG, "bad argument");
+    if (int rc = wait_host_out(c)) return rc;
+    const int T = c->cfg.T;
+    memcpy(u_out, c->h_dout + 4, 2 * (size_t)T * sizeof(double));
+    if (traj_out) {
+        // u_new[0] from the flag block, u_new[t] = shifted[t - 1] for t >= 1
+        double un[2 * kMaxT];
+        un[0] = c->h_dout[2];
+        un[1] = c->h_dout[3];
+        memcpy(un + 2, c->h_dout + 4, 2 * (size_t)(T - 1) * sizeof(double));
+        return mppi_optimal_traj_host(c, x0, un, traj_out);
+    }
+    return MPPI_OK;
+}
+
+int mppi_step_dropin(mppi_ctx* c, const double* x0, const double* window, int W, const double* u,
+                     const float* noise_dev, double* S_dev, float* next_noise_dev, unsigned long long seed,
+                     unsigned long long next_step, double* u_out, double* traj_out) {
+    if (!c || !x0 || !window || !noise_dev || !u_out) return fail(MPPI_E_ARG, "null argument");
+    if (c->cfg.T < 5) return fail(MPPI_E_ARG, "device median filter needs T >= 5 (use the host update)");
+    if (c->xd.world > 1) return fail(MPPI_E_ARG, "mppi_step_dropin is the single-device path");
+    using clk = std::chrono::steady_clock;
+    const auto t0 = clk::now();
+    auto mark = [&](int i) { c->dropin_us[i] = std::chrono::duration<double, std::micro>(clk::now() - t0).count(); };
+    if (int rc = stage_inputs(c, x0, window, W, u, false)) return rc;
+    mark(0);
+    const unsigned fl = MPPI_FLAG_FUSED_UPDATE | MPPI_FLAG_HOST_OUT;
+    if (int rc = launch_rollout(c, noise_dev, S_dev, nullptr, fl, next_host_out(c, fl))) return rc;
+    mark(1);
+    // the next step's noise, queued behind this step's rollout (stream order: the
+    // draw starts after the rollout has read the buffer); issuing it now hides the
+    // launch call under the rollout, and the draw overlaps the host's remaining work
+    if (next_noise_dev)
+        if (int rc = mppi_noise_philox(c, seed, next_step, next_noise_dev)) return rc;
+    mark(2);
+    if (int rc = wait_host_out(c)) return rc;
+    mark(3);
+    if (int rc = mppi_wait_outputs(c, x0, u_out, traj_out)) return rc;   // already published: copies + trajectory
+    mark(4);
+    return MPPI_OK;
 }
 
 int mppi_noise_philox(mppi_ctx* c, unsigned long long seed, unsigned long long step, float* out_dev) {
@@ -1065,10 +1270,17 @@ int mppi_debug_set_buffer(mppi_ctx* c, void* dbg_dev) {
 
 int mppi_debug_nearest(mppi_ctx* c, const float* noise_dev, int K, int* slot_dev, float* pos_dev) {
     if (!c || !noise_dev || !slot_dev || !pos_dev || K < 1 || K > c->cfg.K_local) return fail(MPPI_E_ARG, "bad argument");
+    if (int rc = ensure_static(c)) return rc;
     hipLaunchKernelGGL(nearest_debug_kernel, dim3((K + kThreads - 1) / kThreads), dim3(kThreads), 0, c->stream, c->kc,
                        c->d_step + c->cur, reinterpret_cast<const float2*>(noise_dev), K, slot_dev,
                        reinterpret_cast<float2*>(pos_dev));
     return launch_check("nearest_debug_kernel");
+}
+
+int mppi_debug_dropin_times(const mppi_ctx* c, double* us_out) {
+    if (!c || !us_out) return fail(MPPI_E_ARG, "null argument");
+    memcpy(us_out, c->dropin_us, 5 * sizeof(double));
+    return MPPI_OK;
 }
 
 int mppi_sync(mppi_ctx* c) {

@@ -18,6 +18,12 @@ from . import _native as N
 from .params import ArmParams
 
 
+def _raw_stream(index: int) -> int:
+    """Handle of torch's current stream on device `index` without building a Stream object."""
+    get = getattr(torch._C, "_cuda_getCurrentRawStream", None)
+    return get(index) if get is not None else torch.cuda.current_stream(index).cuda_stream
+
+
 def _dptr(a: np.ndarray):
     return a.ctypes.data_as(C.POINTER(C.c_double))
 
@@ -87,6 +93,8 @@ class RolloutEngine:
         stream first waits for the old one: work already queued there (a noise
         draw, a rollout writing a buffer the next call reads) is finished before
         anything issued on the new stream runs."""
+        if _raw_stream(self.device.index) == self.stream.cuda_stream:   # the usual case, ~0.3 us
+            return
         s = torch.cuda.current_stream(self.device)
         if s.cuda_stream != self.stream.cuda_stream:
             s.wait_stream(self.stream)
@@ -139,8 +147,10 @@ class RolloutEngine:
         self.exchange_world = int(world)
 
     def rollout(self, noise: torch.Tensor, S_out: torch.Tensor | None = None,
-                partial_out: torch.Tensor | None = None, fused_update: bool = False, exchange: bool = False) -> None:
-        """control.py:81-118 for this shard; `exchange`: also exchange and merge the ranks' rows in the launch."""
+                partial_out: torch.Tensor | None = None, fused_update: bool = False, exchange: bool = False,
+                host_out: bool = False) -> None:
+        """control.py:81-118 for this shard; `exchange`: also exchange and merge the ranks' rows in the launch;
+        `host_out` (with fused_update): publish the result to host-mapped memory for wait_outputs()."""
         self._sync_stream()
         self._check_noise(noise)
         if S_out is not None:
@@ -151,16 +161,32 @@ class RolloutEngine:
                                        C.c_void_p(S_out.data_ptr()) if S_out is not None else None,
                                        C.c_void_p(partial_out.data_ptr()) if partial_out is not None else None,
                                        (N.MPPI_FLAG_FUSED_UPDATE if fused_update else 0)
-                                       | (N.MPPI_FLAG_EXCHANGE if exchange else 0)),
+                                       | (N.MPPI_FLAG_EXCHANGE if exchange else 0)
+                                       | (N.MPPI_FLAG_HOST_OUT if host_out else 0)),
                 "mppi_rollout")
 
-    def merge(self, partials: torch.Tensor, n: int, fused_update: bool = False) -> None:
+    def merge(self, partials: torch.Tensor, n: int, fused_update: bool = False, host_out: bool = False) -> None:
         self._sync_stream()
         assert partials.dtype == torch.float64 and partials.is_contiguous()
         assert partials.numel() >= n * self.partial_len
         N.check(self._lib.mppi_merge_partials(self._ctx, C.c_void_p(partials.data_ptr()), int(n),
-                                              N.MPPI_FLAG_FUSED_UPDATE if fused_update else 0),
+                                              (N.MPPI_FLAG_FUSED_UPDATE if fused_update else 0)
+                                              | (N.MPPI_FLAG_HOST_OUT if host_out else 0)),
                 "mppi_merge_partials")
+
+    def wait_outputs(self, x0=None):
+        """After a host_out launch: (shifted nominal (T, 2) fp64, fp64 optimal trajectory (T, 4)
+        from x0, or None without x0) — mppi_wait_outputs, no stream synchronise."""
+        u_out = np.empty((self.T, 2))
+        traj = None
+        xp = None
+        if x0 is not None:
+            x = np.ascontiguousarray(np.asarray(x0, dtype=np.float64).ravel()[:4])
+            traj = np.empty((self.T, 4))
+            xp = _dptr(x)
+        N.check(self._lib.mppi_wait_outputs(self._ctx, xp, _dptr(u_out), _dptr(traj) if traj is not None else None),
+                "mppi_wait_outputs")
+        return u_out, traj
 
     def weighted_noise(self) -> np.ndarray:
         """w_eps (T, 2) fp64 of the last rollout / merge (synchronising)."""
@@ -211,6 +237,56 @@ class RolloutEngine:
                                                 tr.ctypes.data_as(C.c_void_p) if tr is not None else None),
                 "mppi_get_step_outputs")
         return u, tr
+
+    def step_dropin(self, x0, window, u, noise: torch.Tensor, S_out: torch.Tensor | None = None,
+                    next_noise: torch.Tensor | None = None, seed: int = 0, next_step: int = 0,
+                    want_traj: bool = True):
+        """The single-device control step in one native call (mppi_step_dropin):
+        stage inputs, fused rollout + update, wait on the host-mapped result, host
+        fp64 optimal trajectory, then queue the next step's noise into next_noise.
+        Returns (shifted nominal (T, 2) fp64 — a buffer reused by the next call —,
+        optimal trajectory (T, 4) fp64 or None)."""
+        self._sync_stream()
+        x = np.ascontiguousarray(x0, dtype=np.float64)
+        if x.shape != (4,):
+            x = np.ascontiguousarray(x.ravel()[:4])
+        win = window
+        if not (isinstance(win, np.ndarray) and win.dtype == np.float64 and win.ndim == 2 and win.shape[1] == 4
+                and win.flags.c_contiguous):
+            win = np.ascontiguousarray(np.asarray(window, dtype=np.float64)[:, :4])
+        if not 1 <= win.shape[0] <= N.MPPI_SEARCH_LEN:
+            raise ValueError("window must have 1..30 rows of [x, y, dq1, dq2]")
+        uu = None if u is None else np.ascontiguousarray(u, dtype=np.float64)
+        if uu is not None and uu.shape != (self.T, 2):
+            raise ValueError(f"u must be ({self.T}, 2)")
+        if noise.data_ptr() != getattr(self, "_checked_noise", 0):
+            self._check_noise(noise)
+            self._checked_noise = noise.data_ptr()
+        if getattr(self, "_u_out", None) is None:
+            self._u_out = np.empty((self.T, 2))
+        traj = np.empty((self.T, 4)) if want_traj else None
+        N.check(self._lib.mppi_step_dropin(
+            self._ctx, x.ctypes.data, win.ctypes.data, win.shape[0], uu.ctypes.data if uu is not None else None,
+            noise.data_ptr(), S_out.data_ptr() if S_out is not None else None,
+            next_noise.data_ptr() if next_noise is not None else None, seed & 0xFFFFFFFFFFFFFFFF,
+            next_step & 0xFFFFFFFFFFFFFFFF,
+            self._u_out.ctypes.data, traj.ctypes.data if traj is not None else None), "mppi_step_dropin")
+        return self._u_out, traj
+
+    def dropin_times(self) -> np.ndarray:
+        """Diagnostics: phase ends (us) of the last step_dropin (mppi_debug_dropin_times)."""
+        out = np.zeros(5)
+        N.check(self._lib.mppi_debug_dropin_times(self._ctx, _dptr(out)), "mppi_debug_dropin_times")
+        return out
+
+    def optimal_traj_host(self, x0, u_new) -> np.ndarray:
+        """(T, 4) fp64 optimal trajectory of control.py:129-134 from the updated, not yet
+        shifted controls u_new (T, 2), on the host (mppi_optimal_traj_host)."""
+        x = np.ascontiguousarray(np.asarray(x0, dtype=np.float64).ravel()[:4])
+        un = np.ascontiguousarray(u_new, dtype=np.float64).reshape(self.T, 2)
+        out = np.empty((self.T, 4))
+        N.check(self._lib.mppi_optimal_traj_host(self._ctx, _dptr(x), _dptr(un), _dptr(out)), "mppi_optimal_traj_host")
+        return out
 
     def philox_noise(self, seed: int, step: int = 0, out: torch.Tensor | None = None) -> torch.Tensor:
         self._sync_stream()

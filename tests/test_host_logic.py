@@ -4,6 +4,8 @@ runs before / after the device call, without a GPU."""
 import contextlib
 import io
 import math
+import os
+import sys
 
 import numpy as np
 import pytest
@@ -173,3 +175,32 @@ def test_bench_numpy_baseline_runs(paths):
     out = bench.numpy_baseline(eps, paths["xydq_circle"][:30], np.array([1.15, -1.27, 0.0, 0.0]),
                                np.array([[10.0, -2.0]] * 4), 100.0, 0.0)
     assert out["value"] > 0 and out["cores"] == 1 and "K=64 T=4" in out["sample"]
+
+
+def test_bench_launches_ranks_itself(monkeypatch):
+    """`bench.py --gpus N` without WORLD_SIZE starts N ranks itself (the driver's
+    N = 1, 2, 4, 8 calls then need no external launcher): a torch.distributed.run
+    child on 127.0.0.1 with the same arguments, before any GPU call; ranks own one
+    GPU each under nccl (RCCL) when there are enough, else share under gloo."""
+    import bench
+    cmd = bench.launcher_cmd(4, 29999, ["--gpus", "4", "--steps", "50"])
+    assert cmd[:3] == [sys.executable, "-m", "torch.distributed.run"]
+    assert "--nproc-per-node=4" in cmd and "--nnodes=1" in cmd and "127.0.0.1" in cmd
+    assert "--master-port=29999" in cmd
+    assert cmd[-5:] == [os.path.abspath(bench.__file__), "--gpus", "4", "--steps", "50"]
+    seen = {}
+    monkeypatch.delenv("WORLD_SIZE", raising=False)
+    monkeypatch.setattr(sys, "argv", ["bench.py", "--gpus", "2", "--steps", "3"])
+    monkeypatch.setattr(bench, "launch_ranks", lambda a: seen.setdefault("n", a.gpus) and 0)
+    with pytest.raises(SystemExit) as e:
+        bench.main()
+    assert e.value.code == 0 and seen["n"] == 2
+    monkeypatch.setattr(bench.torch.cuda, "device_count", lambda: 8)
+    assert bench.default_backend(8) == "nccl" and bench.default_backend(2) == "nccl"
+    monkeypatch.setattr(bench.torch.cuda, "device_count", lambda: 1)
+    assert bench.default_backend(2) == "gloo" and bench.default_backend(1) == "nccl"
+
+
+def test_bench_host_cores_is_the_affinity_mask():
+    import bench
+    assert bench.host_cores() == len(os.sched_getaffinity(0))

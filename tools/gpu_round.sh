@@ -20,6 +20,7 @@ for s in "$@"; do
     test)  step test 900 python -m pytest tests -m gpu -q -rf;;
     bench) step bench 600 python bench.py --steps 200 --warmup 20 --cpu-seconds 10;;
     benchq) step benchq 300 python bench.py --steps 100 --warmup 10 --cpu-seconds 0;;
+    lat) step lat 300 python tools/latency_breakdown.py;;
     prof)  step prof 600 rocprofv3 --kernel-trace --stats -d gpurun_out/prof -o run --output-format csv -- python3 bench.py --steps 100 --warmup 10 --cpu-seconds 0;;
     *) echo "unknown step $s"; exit 2;;
   esac

@@ -1,7 +1,16 @@
-"""Where the drop-in's control-step latency goes (diagnostic tool, not product):
-the phases of MPPIControllerForPathTracking.calc_control_input at the bench's
-K, T with device noise, timed on the host with a device sync after each phase
-(so each phase's GPU time lands in its own line), plus the untouched call.
+"""Where the drop-in's control-step latency goes (diagnostic tool, not product).
+
+MPPIControllerForPathTracking.calc_control_input at the bench's K, T with device
+noise, on the fused single-call path (mppi_step_dropin):
+
+  * closed loop: run.py's driver (harness), plant work between ticks — the
+    bench's control_step_latency_ms;
+  * back to back: calls with nothing in between (the next step's Philox draw,
+    queued behind each call, is then paid by the following call);
+  * phases of one call: Python before the native call (waypoint update, checks,
+    engine lookup), the native call (stage + launch + wait + host trajectory +
+    queue the next noise), Python after; the device work alone (one fused
+    rollout launch, and one Philox draw, HIP-event timed on the stream).
 
     python tools/latency_breakdown.py [K T calls]
 """
@@ -15,49 +24,90 @@ import numpy as np  # noqa: E402
 import torch  # noqa: E402
 
 from mppi_robotarm_amd.controller import MPPIControllerForPathTracking  # noqa: E402
+from mppi_robotarm_amd.harness import run_closed_loop  # noqa: E402
 from mppi_robotarm_amd.params import X0_RUNPY, runpy_config  # noqa: E402
+
+
+def us(v):
+    return f"{np.median(v) * 1e6:8.1f} us (p90 {np.percentile(v, 90) * 1e6:7.1f})"
 
 
 def main():
     a = [int(x) for x in sys.argv[1:]]
-    K, T, n = (a + [65536, 64, 60][len(a):])[:3]
+    K, T, n = (a + [65536, 64, 200][len(a):])[:3]
     torch.cuda.set_device(0)
     path = np.load(os.path.join(ROOT, "tests", "golden", "paths.npz"))["xydq_circle"][:, :4]
     kw = runpy_config()
     kw.update(number_of_samples_K=K, horizon_step_T=T, visualze_sampled_trajs=False)
+
+    rec = run_closed_loop(path, ticks=n, noise="device", seed=0, verbose=False, device=0, **kw)
+    rec["controller"].close()
+    closed = rec["latency_s"][3:]
+
     c = MPPIControllerForPathTracking(ref_path=path, noise="device", seed=0, verbose=False, device=0, **kw)
     x = X0_RUNPY.copy()
-    whole = []
-    for i in range(n):
-        t0 = time.perf_counter()
+    for _ in range(5):
         c.calc_control_input(x)
-        whole.append(time.perf_counter() - t0)
         c.prev_waypoints_idx = 0
     eng = c._get_engine()
-    sync = torch.cuda.synchronize
-    ph = {k: [] for k in ("waypoint", "philox", "set_inputs", "rollout", "w_eps D2H", "median+update", "opt traj")}
-    u = c.u_prev.copy()
-    for i in range(n):
-        t = time.perf_counter()
-        c._get_nearest_waypoint(x[0], x[1], update_prev_idx=True)
-        t1 = time.perf_counter(); ph["waypoint"].append(t1 - t)
-        eng.philox_noise(0, i, out=c._noise_dev); sync()
-        t2 = time.perf_counter(); ph["philox"].append(t2 - t1)
-        eng.set_step_inputs(x, path[0:30], u); sync()
-        t3 = time.perf_counter(); ph["set_inputs"].append(t3 - t2)
-        eng.rollout(c._noise_dev); sync()
-        t4 = time.perf_counter(); ph["rollout"].append(t4 - t3)
-        w = eng.weighted_noise()
-        t5 = time.perf_counter(); ph["w_eps D2H"].append(t5 - t4)
-        w = c._moving_median_filter(xx=w, window_size=10)
-        uu = u + w
-        t6 = time.perf_counter(); ph["median+update"].append(t6 - t5)
-        eng.trajectories(base_u=uu, K=1)[0].double().cpu().numpy()
-        t7 = time.perf_counter(); ph["opt traj"].append(t7 - t6)
-    print(f"K={K} T={T}: calc_control_input median {np.median(whole) * 1e3:.3f} ms")
-    for k, v in ph.items():
-        print(f"  {k:14s} {np.median(v) * 1e6:8.1f} us")
+    stamps = []
+    native = eng.step_dropin
+
+    def timed(*args, **kwargs):
+        t0 = time.perf_counter()
+        out = native(*args, **kwargs)
+        stamps.append((t0, time.perf_counter()))
+        return out
+
+    eng.step_dropin = timed
+    whole, pre, nat, post = [], [], [], []
+    for _ in range(n):
+        c.prev_waypoints_idx = 0
+        t0 = time.perf_counter()
+        c.calc_control_input(x)
+        t3 = time.perf_counter()
+        t1, t2 = stamps[-1]
+        whole.append(t3 - t0)
+        pre.append(t1 - t0)
+        nat.append(t2 - t1)
+        post.append(t3 - t2)
+    eng.step_dropin = native
+    phases = []
+    for _ in range(n):
+        c.prev_waypoints_idx = 0
+        c.calc_control_input(x)
+        phases.append(eng.dropin_times() * 1e-6)
+    phases = np.array(phases)
+
+    # device work alone, HIP events on the engine's stream
+    s = torch.cuda.current_stream()
+    ev = [torch.cuda.Event(enable_timing=True) for _ in range(4)]
+    kern, phil = [], []
+    for _ in range(50):
+        ev[0].record(s)
+        eng.rollout(c._noise_dev, fused_update=True)
+        ev[1].record(s)
+        eng.philox_noise(0, 1, out=c._noise_dev)
+        ev[2].record(s)
+        torch.cuda.synchronize()
+        kern.append(ev[0].elapsed_time(ev[1]) * 1e-3)
+        phil.append(ev[1].elapsed_time(ev[2]) * 1e-3)
     c.close()
+
+    print(f"K={K} T={T}, device noise, fused single-call drop-in (mppi_step_dropin), {n} calls")
+    print(f"  closed loop (run.py driver, plant between ticks) {us(closed)}")
+    print(f"  back to back (no work between calls)             {us(whole)}")
+    print(f"    Python before the native call                  {us(pre)}")
+    print(f"    native call (stage, launch, wait, traj, noise) {us(nat)}")
+    print(f"    Python after                                   {us(post)}")
+    names = ["stage inputs (host keys + H2D copy issued)", "launch fused rollout", "queue next Philox draw",
+             "wait for the rollout's outputs", "copy outputs + fp64 optimal trajectory"]
+    prev = np.zeros(len(phases))
+    for i, nm in enumerate(names):
+        print(f"      native: {nm:43s}{us(phases[:, i] - prev)}")
+        prev = phases[:, i]
+    print(f"  device: fused rollout launch                     {us(kern)}")
+    print(f"  device: Philox draw of the next step's noise     {us(phil)}")
 
 
 if __name__ == "__main__":
