@@ -939,7 +939,7 @@ int mppi_chain_set_step_inputs(mppi_chain_ctx* c, const double* x0, const double
             const double* r = window + 4 * j;
             h->win[j] = make_float4((float)r[0], (float)r[1], (float)r[2], (float)r[3]);
             const double rx = r[0] - cx, ry = r[1] - cy;
-            h->key[j] = make_float4((float)rx, (float)ry, (float)(rx * rx + ry * ry), 0.f);
+            h->key[j] = make_float4((float)(-2.0 * rx), (float)(-2.0 * ry), (float)(rx * rx + ry * ry), 0.f);
         } else {
             h->win[j] = make_float4(0.f, 0.f, 0.f, 0.f);
             h->key[j] = make_float4(0.f, 0.f, kPadKey, 0.f);

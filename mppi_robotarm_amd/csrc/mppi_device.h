@@ -156,6 +156,7 @@ typedef __attribute__((address_space(4))) const float cfloat;
 __device__ __forceinline__ float4 const_ld4(cfloat* p) { return make_float4(p[0], p[1], p[2], p[3]); }
 
 typedef float f32x2 __attribute__((ext_vector_type(2)));
+typedef float f32x4 __attribute__((ext_vector_type(4)));
 
 // v_min3_f32 / v_min_f32 issued directly: the operands are bit-packed keys, and
 // fminf() would make hipcc canonicalise every one of them (v_max x, x) first.
@@ -173,7 +174,8 @@ __device__ __forceinline__ float min_raw(float a, float b) {
 // ------------------------------------------------------------ window search
 
 // Nearest waypoint of the shared window (control.py:200-232): the window is
-// uploaded as centred keys (rx', ry', rx'^2 + ry'^2; pads 1e30), and
+// uploaded as centred keys (-2 rx', -2 ry', rx'^2 + ry'^2; pads 1e30 — the
+// factor -2 is exact, so it costs nothing to fold it into the table), and
 //   argmin_j |p - r_j|^2 = argmin_j (|r'_j|^2 - 2 p'.r'_j),
 // two slots per v_pk_fma_f32; the slot index is packed into the 5 low mantissa
 // bits so one v_min3 per two slots carries the argmin (first occurrence: equal
@@ -221,10 +223,11 @@ struct Search {
         cy = ctr.y;
     }
 
-    __device__ __forceinline__ unsigned nearest(float px, float py) const {
-        const float dx = px - cx, dy = py - cy;
-        const float ax = -2.f * dx, ay = -2.f * dy;
-        const f32x2 ax2 = {ax, ax}, ay2 = {ay, ay};
+    __device__ __forceinline__ unsigned nearest(float px, float py) const { return nearest_d(px - cx, py - cy); }
+
+    // dx, dy: the position relative to the window centre
+    __device__ __forceinline__ unsigned nearest_d(float dx, float dy) const {
+        const f32x2 ax2 = {dx, dx}, ay2 = {dy, dy};
         const float pp = fmaf(dx, dx, dy * dy);
         const f32x2 pp2 = {pp, pp};
         float best = 3.0e38f;
@@ -251,7 +254,7 @@ struct Search {
 // LDS read per slot and per step, frees the 3 x 30 key registers — for kernels
 // whose per-lane state is large (the n-link chain) that buys occupancy.
 struct alignas(16) KeyPair {
-    float4 xy;   // rx'(2i), rx'(2i+1), ry'(2i), ry'(2i+1)
+    float4 xy;   // -2 rx'(2i), -2 rx'(2i+1), -2 ry'(2i), -2 ry'(2i+1)
     float4 c;    // c'(2i), c'(2i+1), 0, 0
 };
 constexpr int kKeyPairs = kSlots / 2;
@@ -272,8 +275,7 @@ struct SearchLDS {
 
     __device__ __forceinline__ unsigned nearest(float px, float py) const {
         const float dx = px - cx, dy = py - cy;
-        const float ax = -2.f * dx, ay = -2.f * dy;
-        const f32x2 ax2 = {ax, ax}, ay2 = {ay, ay};
+        const f32x2 ax2 = {dx, dx}, ay2 = {dy, dy};
         const float pp = fmaf(dx, dx, dy * dy);
         const f32x2 pp2 = {pp, pp};
         float best = 3.0e38f;

@@ -50,7 +50,7 @@ constexpr int kThreads = 256;
 // Device-resident per-step parameter block (ping-pong pair in the context).
 struct alignas(16) DevStep {
     float4 win[kSlots];   // rx, ry, rdq1, rdq2 of window slot j (lookup after argmin)
-    float4 key[kSlots];   // rx', ry', c' = rx'^2 + ry'^2 (centred), 0; pads c' = 1e30
+    float4 key[kSlots];   // -2 rx', -2 ry', c' = rx'^2 + ry'^2 (centred), 0; pads c' = 1e30
     float4 x0;            // q1, q2, dq1, dq2
     float4 ctr;           // window centre (cx, cy), W, 0
     float4 ua[kMaxT];     // u0, u1, a0, a1 (a = (gamma u_t)^T Sigma^-1), fp32
@@ -71,34 +71,130 @@ struct KConst {
 //   M = [[A + B c2, D + E c2], [D + E c2, D]]   (M22 = m2 lc2^2 + l2 = D)
 //   h = E s2,  G = [P c1 + Q c12, Q c12],  C dq = [-h dq2 (2 dq1 + dq2), h dq1^2]
 //   ddq = M^-1 (v - C dq - G);  dq += ddq dt;  q += dq dt
-// c2/s2 come from the angle-difference identities of the cached sincos of
-// q1 and q1 + q2, so each step evaluates exactly two sincos (of the NEW q),
-// which the next step's dynamics and this step's kinematics share.
-struct ArmState {
-    float q1, q2, dq1, dq2;
-    float s1, c1, s12, c12;
+// written on register pairs, so most of it issues as v_pk_* (two fp32 lanes
+// per instruction):
+//  * the joint angles are kept in revolutions (q / 2 pi), the unit of the
+//    hardware v_sin_f32 / v_cos_f32, so no scaling per evaluation;
+//  * c2/s2 come from the angle-difference identities of the cached (cos, sin)
+//    of q1 and q1 + q2 — two packed ops — so a step evaluates exactly two
+//    sincos (of the NEW q), shared by the next step's dynamics and this
+//    step's kinematics;
+//  * the constants live in VGPR pairs (DynK) so a packed op never needs a
+//    second scalar operand moved in.
+struct Arm {
+    f32x2 Q;      // (q1, q2) / (2 pi)
+    f32x2 dq;     // (dq1, dq2)
+    f32x2 cs1;    // (cos q1, sin q1)
+    f32x2 cs12;   // (cos(q1 + q2), sin(q1 + q2))
 };
 
-__device__ __forceinline__ void dyn_step(ArmState& x, float v1, float v2, const KConst& c) {
-    const float c2 = fmaf(x.c12, x.c1, x.s12 * x.s1);
-    const float s2 = fmaf(x.s12, x.c1, -x.c12 * x.s1);
-    const float M11 = fmaf(c.B, c2, c.A);
-    const float M12 = fmaf(c.E, c2, c.D);
-    const float h = c.E * s2;
-    const float G2 = c.Q * x.c12;
-    const float G1 = fmaf(c.P, x.c1, G2);
-    const float r1 = fmaf(h * x.dq2, fmaf(2.f, x.dq1, x.dq2), v1 - G1);
-    const float r2 = fmaf(-h * x.dq1, x.dq1, v2 - G2);
-    const float det = fmaf(M11, c.D, -M12 * M12);
+// Per-launch constants in VGPR pairs (made lane-opaque once, before the loop:
+// as uniform values the compiler would keep them in SGPRs and move one into a
+// VGPR at every packed use).
+struct DynK {
+    f32x2 zB, DA;      // (0, B), (D, A): (D, M11) = DA + zB c2
+    f32x2 ED;          // (E, D): M12 = D + E c2, h = E s2
+    f32x2 nP0, nQ;     // (-P, 0), (-Q, -Q): v - G
+    f32x2 dt2;         // (dt, dt / (2 pi))
+    f32x2 fk;          // (fk1, fk2)
+    f32x2 ctr;         // window centre
+    f32x2 w01, w23;    // stage weights x 10000
+};
+
+template <class V>
+__device__ __forceinline__ V vgpr_opaque(V v) {
+    asm volatile("" : "+v"(v));
+    return v;
+}
+
+// One kernel-argument field as its own scalar: built straight from adjacent
+// fields, the vector pairs below made LLVM copy (dt, fk1, fk2) into a private
+// array that was then promoted to LDS — which costs the kernel a dispatch-packet
+// read per wave and spread the workgroup starts over 13 us (measured).
+__device__ __forceinline__ float arg_f(const float& f) {
+    float x = f;
+    asm volatile("" : "+s"(x));
+    return x;
+}
+
+__device__ __forceinline__ DynK make_dynk(const KConst& c, float cx, float cy) {
+    const float A = arg_f(c.A), B = arg_f(c.B), D = arg_f(c.D), E = arg_f(c.E), P = arg_f(c.P), Q = arg_f(c.Q);
+    const float dt = arg_f(c.dt), fk1 = arg_f(c.fk1), fk2 = arg_f(c.fk2);
+    DynK k;
+    k.zB = vgpr_opaque(f32x2{0.f, B});
+    k.DA = vgpr_opaque(f32x2{D, A});
+    k.ED = vgpr_opaque(f32x2{E, D});
+    k.nP0 = vgpr_opaque(f32x2{-P, 0.f});
+    k.nQ = vgpr_opaque(f32x2{-Q, -Q});
+    k.dt2 = vgpr_opaque(f32x2{dt, dt * 0.15915494309189535f});
+    k.fk = vgpr_opaque(f32x2{fk1, fk2});
+    k.ctr = vgpr_opaque(f32x2{cx, cy});
+    k.w01 = vgpr_opaque(f32x2{arg_f(c.sw[0]), arg_f(c.sw[1])});
+    k.w23 = vgpr_opaque(f32x2{arg_f(c.sw[2]), arg_f(c.sw[3])});
+    return k;
+}
+
+__device__ __forceinline__ f32x2 splat(float x) { return f32x2{x, x}; }
+
+// (cos, sin) of an angle given in revolutions
+__device__ __forceinline__ f32x2 cossin_rev(float a) {
+#ifdef MPPI_ACCURATE_TRIG
+    float s, co;
+    sincosf(a * 6.283185307179586f, &s, &co);
+    return f32x2{co, s};
+#else
+    return f32x2{__builtin_amdgcn_cosf(a), __builtin_amdgcn_sinf(a)};
+#endif
+}
+
+__device__ __forceinline__ void arm_init(Arm& x, float4 x0) {
+    x.Q = f32x2{x0.x, x0.y} * 0.15915494309189535f;
+    x.dq = f32x2{x0.z, x0.w};
+    x.cs1 = cossin_rev(x.Q.x);
+    x.cs12 = cossin_rev(x.Q.x + x.Q.y);
+}
+
+// (c2, s2) = (c12 c1 + s12 s1, s12 c1 - c12 s1) from cs1 = (c1, s1), cs12 =
+// (c12, s12): the swap and negation of cs12 are operand modifiers of the one
+// v_pk_fma (op_sel / op_sel_hi pick the halves, neg_hi negates c12), which the
+// compiler would otherwise build with a v_xor and two v_mov.
+__device__ __forceinline__ f32x2 cos_sin_diff(f32x2 cs1, f32x2 cs12) {
+    const f32x2 m = cs12 * splat(cs1.x);
+    f32x2 r;
+    asm("v_pk_fma_f32 %0, %1, %2, %3 op_sel:[1,1,0] op_sel_hi:[0,1,1] neg_hi:[1,0,0]"
+        : "=v"(r) : "v"(cs12), "v"(cs1), "v"(m));
+    return r;
+}
+
+__device__ __forceinline__ void arm_step(Arm& x, f32x2 v, const DynK& k) {
+    const float c1 = x.cs1.x, c12 = x.cs12.x;
+    const f32x2 cs2 = cos_sin_diff(x.cs1, x.cs12);
+    const float c2 = cs2.x, s2 = cs2.y;
+    const f32x2 DM11 = __builtin_elementwise_fma(k.zB, splat(c2), k.DA);   // (D, M11)
+    const float M12 = fmaf(k.ED.x, c2, k.ED.y);
+    const float h = k.ED.x * s2;
+    const f32x2 w = __builtin_elementwise_fma(k.nQ, splat(c12), __builtin_elementwise_fma(k.nP0, splat(c1), v));
+    const float dq1 = x.dq.x, dq2 = x.dq.y;
+    const float hd1 = h * dq1;
+    const f32x2 r = {fmaf(h * dq2, fmaf(2.f, dq1, dq2), w.x), fmaf(-hd1, dq1, w.y)};
+    const float det = fmaf(DM11.y, k.ED.y, -(M12 * M12));
     const float rdet = __builtin_amdgcn_rcpf(det);
-    const float ddq1 = fmaf(c.D, r1, -M12 * r2) * rdet;
-    const float ddq2 = fmaf(M11, r2, -M12 * r1) * rdet;
-    x.dq1 = fmaf(ddq1, c.dt, x.dq1);
-    x.dq2 = fmaf(ddq2, c.dt, x.dq2);
-    x.q1 = fmaf(x.dq1, c.dt, x.q1);
-    x.q2 = fmaf(x.dq2, c.dt, x.q2);
-    sincos_f32(x.q1, &x.s1, &x.c1);
-    sincos_f32(x.q1 + x.q2, &x.s12, &x.c12);
+    const f32x2 ddq = __builtin_elementwise_fma(splat(-M12), f32x2{r.y, r.x}, DM11 * r) * splat(rdet);
+    x.dq = __builtin_elementwise_fma(ddq, splat(k.dt2.x), x.dq);
+    x.Q = __builtin_elementwise_fma(x.dq, splat(k.dt2.y), x.Q);
+    x.cs1 = cossin_rev(x.Q.x);
+    x.cs12 = cossin_rev(x.Q.x + x.Q.y);
+}
+
+// end effector (control.py:178-179): (fk1 c1 + fk2 c12, fk1 s1 + fk2 s12)
+__device__ __forceinline__ f32x2 arm_fk(const Arm& x, const DynK& k) {
+    return __builtin_elementwise_fma(splat(k.fk.x), x.cs1, splat(k.fk.y) * x.cs12);
+}
+
+// stage / terminal cost (control.py:185-198, weights x 10000): e = (ex, ey), f = (e1, e2)
+__device__ __forceinline__ float cost_pk(f32x2 e, f32x2 f, f32x2 w01, f32x2 w23) {
+    const f32x2 s = __builtin_elementwise_fma(f * w23, f, (e * w01) * e);
+    return s.x + s.y;
 }
 
 using Scratch = MergeScratch<2 * kMaxT>;
@@ -191,7 +287,7 @@ __global__ __launch_bounds__(NT) void rollout_kernel(
     DevStep* __restrict__ nxt, unsigned flags, const XDesc xd, unsigned* __restrict__ epoch, unsigned* __restrict__ tmo,
     float* __restrict__ upd, const HostOut ho, unsigned long long* __restrict__ dbg) {
     __shared__ float4 s_win[kSlots];
-    __shared__ float4 s_ua[kMaxT];   // per-step constants (u_t, a_t)
+    __shared__ float4 s_ua[kMaxT + kPF];   // per-step constants (u_t, a_t); rows >= T repeat row T - 1
     __shared__ float s_redf[NT / 64];
     __shared__ int s_cnt[NT / 64];
     __shared__ int s_k[NT];
@@ -227,17 +323,12 @@ __global__ __launch_bounds__(NT) void rollout_kernel(
     const float4 wrow = st->win[tid & (kSlots - 1)];
     Search<LPS> sr;
     sr.load(st->key, st->ctr, tid & (LPS - 1));
-    const float4 x0 = st->x0;
-    ArmState x;
-    x.q1 = x0.x;
-    x.q2 = x0.y;
-    x.dq1 = x0.z;
-    x.dq2 = x0.w;
-    sincos_f32(x.q1, &x.s1, &x.c1);
-    sincos_f32(x.q1 + x.q2, &x.s12, &x.c12);
+    Arm x;
+    arm_init(x, st->x0);
+    const DynK dk = make_dynk(c, sr.cx, sr.cy);
     // the per-step constants go to LDS: the ring reads them there, so no scalar
     // load shares lgkmcnt with the deferred row lookup below
-    for (int i = tid; i < T; i += NT) s_ua[i] = st->ua[i];
+    for (int i = tid; i < T + kPF; i += NT) s_ua[i] = st->ua[i < T ? i : T - 1];
     if (tid < kSlots) s_win[tid] = wrow;
     __syncthreads();
     float4 uring[kPF];  // per-step constants (u_t, a_t), uniform
@@ -252,17 +343,26 @@ __global__ __launch_bounds__(NT) void rollout_kernel(
     // hidden.  The costs are still added in step order and folded into fp64
     // every kPF steps (S4), so S is the sum of the same fp32 terms.
     double S = 0.0;
-    float S4 = 0.f;  // fp32 partial over one 4-step block, folded into fp64 S
-    float ex = 0.f, ey = 0.f, e1 = 0.f, e2 = 0.f;
+    // fp32 partial sums over one 4-step block, folded into fp64 S: the two lanes
+    // of a pair accumulate (w0 ex^2 + w2 e1^2 + a0 v1, w1 ey^2 + w3 e2^2 + a1 v2),
+    // each term one v_pk_fma into the running pair
+    f32x2 S4 = {0.f, 0.f};
+    f32x2 ee = {0.f, 0.f}, ef = {0.f, 0.f};   // (ex, ey), (e1, e2) of the last step added
     float4 pr = make_float4(0.f, 0.f, 0.f, 0.f);
-    float ppx = 0.f, ppy = 0.f, pd1 = 0.f, pd2 = 0.f, pg = 0.f;
+    f32x2 pp = {0.f, 0.f}, pd = {0.f, 0.f};   // pending step: end effector, joint rates
     auto add_pending = [&]() {
-        ex = ppx - pr.x;
-        ey = ppy - pr.y;
-        e1 = pd1 - pr.z;
-        e2 = pd2 - pr.w;
-        S4 += weighted_sq(ex, ey, e1, e2, c.sw) + pg;
+        // the row is taken only once this step's dynamics are done (the asm
+        // needs x.cs12, the step's last result): left free, the scheduler pulls
+        // the cost up next to the lookup and waits on the LDS round trip there
+        f32x4 r = {pr.x, pr.y, pr.z, pr.w};
+        asm volatile("" : "+v"(r) : "v"(x.cs12));
+        ee = pp - f32x2{r.x, r.y};
+        ef = pd - f32x2{r.z, r.w};
+        S4 = __builtin_elementwise_fma(ef * dk.w23, ef, __builtin_elementwise_fma(ee * dk.w01, ee, S4));
     };
+    // uniform LDS byte offset of step t's row of s_ua, held in a VGPR (advanced
+    // once per 4 steps; the ring's reads add compile-time offsets)
+    int ua_off = vgpr_opaque(0);
     // `slot` (= t % kPF) is a compile-time constant at every call, so the rings
     // stay in registers (a runtime index sends them to scratch).  H: step t - 1
     // exists — 0 no, 1 yes, 2 test t > 0 at run time.  LPS = 1 peels the first
@@ -272,28 +372,39 @@ __global__ __launch_bounds__(NT) void rollout_kernel(
         constexpr int slot = decltype(slot_c)::value;
         constexpr int H = decltype(h_c)::value;
         const bool h = H == 2 ? t > 0 : H == 1;
-        const float2 e = ring[slot];
-        const float4 ua = uring[slot];
+        // The ring slot is fully consumed before its refill is issued: if the old
+        // value outlived the new load, the two would need different registers and
+        // the loop back-edge a v_mov of the refill — which waits for the load
+        // (s_waitcnt vmcnt(0) each iteration: 1.86x the step time, measured).
+        // The empty volatile asm takes the slot's values at this point of the
+        // program (volatile asm keeps its order against the previous step's
+        // PIN_LOADS): otherwise the scheduler hoists their uses towards the loop
+        // top, where waiting for them means waiting for every load in flight.
+        f32x2 e = {ring[slot].x, ring[slot].y};
+        f32x4 ua = {uring[slot].x, uring[slot].y, uring[slot].z, uring[slot].w};
+        asm volatile("" : "+v"(e), "+v"(ua));
+        // u[t] + eps (exploit) or eps, control.py:99-101
+        const f32x2 v = __builtin_elementwise_fma(splat(exf), f32x2{ua.x, ua.y}, e);
+        // (gamma u^T Sigma^-1) v, control.py:106
+        S4 = __builtin_elementwise_fma(f32x2{ua.z, ua.w}, v, S4);
         const int tl = t + kPF < T ? t + kPF : T - 1;
         ring[slot] = np[(size_t)tl * K];
-        uring[slot] = s_ua[tl];
+        uring[slot] = *reinterpret_cast<const float4*>(reinterpret_cast<const char*>(s_ua) + ua_off +
+                                                       (kPF + slot) * (int)sizeof(float4));
+        if (slot == kPF - 1) ua_off += kPF * (int)sizeof(float4);   // slot == t % kPF at every call
         PIN_LOADS();
-        const float v1 = fmaf(exf, ua.x, e.x);  // u[t] + eps (exploit) or eps, control.py:99-101
-        const float v2 = fmaf(exf, ua.y, e.y);
-        dyn_step(x, v1, v2, c);
+        arm_step(x, v, dk);
         if (h) {
             add_pending();   // step t - 1
             if (slot == 0) {
-                S += (double)S4;
-                S4 = 0.f;
+                S += (double)(S4.x + S4.y);
+                S4 = f32x2{0.f, 0.f};
             }
         }
-        ppx = fmaf(c.fk1, x.c1, c.fk2 * x.c12);  // control.py:178-179
-        ppy = fmaf(c.fk1, x.s1, c.fk2 * x.s12);
-        pd1 = x.dq1;
-        pd2 = x.dq2;
-        pg = fmaf(ua.z, v1, ua.w * v2);  // (gamma u^T Sigma^-1) v, control.py:106
-        pr = s_win[sr.nearest(ppx, ppy)];
+        pp = arm_fk(x, dk);   // control.py:178-179
+        pd = x.dq;
+        const f32x2 d = pp - dk.ctr;
+        pr = s_win[sr.nearest_d(d.x, d.y)];
     };
     using I0 = std::integral_constant<int, 0>;
     using I1 = std::integral_constant<int, 1>;
@@ -336,8 +447,8 @@ __global__ __launch_bounds__(NT) void rollout_kernel(
         if (t + 2 < T) dstep(t + 2, I2{}, H2{});
     }
     add_pending();                       // step T - 1
-    S += (double)S4;
-    S += (double)weighted_sq(ex, ey, e1, e2, c.tw);  // terminal cost, control.py:109
+    S += (double)(S4.x + S4.y);
+    S += (double)cost_pk(ee, ef, f32x2{arg_f(c.tw[0]), arg_f(c.tw[1])}, f32x2{arg_f(c.tw[2]), arg_f(c.tw[3])});  // terminal cost, control.py:109
 
     STAMP(1, NOW());
     const bool owner = valid && sr.sub == 0;
@@ -515,25 +626,20 @@ __global__ __launch_bounds__(kThreads) void traj_kernel(const KConst c, const De
     if (k >= Kn) return;
     const int T = c.T;
     const float exf = noise ? ((c.k_offset + k) < c.k_exploit ? 1.f : 0.f) : 1.f;
-    const float4 x0 = st->x0;
-    ArmState x;
-    x.q1 = x0.x;
-    x.q2 = x0.y;
-    x.dq1 = x0.z;
-    x.dq2 = x0.w;
-    sincos_f32(x.q1, &x.s1, &x.c1);
-    sincos_f32(x.q1 + x.q2, &x.s12, &x.c12);
+    Arm x;
+    arm_init(x, st->x0);
+    const DynK dk = make_dynk(c, 0.f, 0.f);
     for (int t = 0; t < T; ++t) {
         const int ti = t == 0 ? T - 1 : t - 1;
         const float2 b = base[ti];
-        float v1 = b.x, v2 = b.y;
+        f32x2 v = {b.x, b.y};
         if (noise) {
             const float2 e = noise[(size_t)ti * c.K_local + k];
-            v1 = fmaf(exf, b.x, e.x);
-            v2 = fmaf(exf, b.y, e.y);
+            v = __builtin_elementwise_fma(splat(exf), v, f32x2{e.x, e.y});
         }
-        dyn_step(x, v1, v2, c);
-        out[(size_t)k * T + t] = make_float4(x.q1, x.q2, x.dq1, x.dq2);
+        arm_step(x, v, dk);
+        const f32x2 q = x.Q * 6.283185307179586f;
+        out[(size_t)k * T + t] = make_float4(q.x, q.y, x.dq.x, x.dq.y);
     }
 }
 
@@ -550,22 +656,17 @@ __global__ __launch_bounds__(kThreads) void nearest_debug_kernel(const KConst c,
     const float exf = (c.k_offset + k) < c.k_exploit ? 1.f : 0.f;
     Search<1> sr;
     sr.load(st->key, st->ctr, 0);
-    const float4 x0 = st->x0;
-    ArmState x;
-    x.q1 = x0.x;
-    x.q2 = x0.y;
-    x.dq1 = x0.z;
-    x.dq2 = x0.w;
-    sincos_f32(x.q1, &x.s1, &x.c1);
-    sincos_f32(x.q1 + x.q2, &x.s12, &x.c12);
+    Arm x;
+    arm_init(x, st->x0);
+    const DynK dk = make_dynk(c, sr.cx, sr.cy);
     for (int t = 0; t < T; ++t) {
         const float4 ua = st->ua[t];
         const float2 e = noise[(size_t)t * c.K_local + k];
-        dyn_step(x, fmaf(exf, ua.x, e.x), fmaf(exf, ua.y, e.y), c);
-        const float px = fmaf(c.fk1, x.c1, c.fk2 * x.c12);
-        const float py = fmaf(c.fk1, x.s1, c.fk2 * x.s12);
-        slot[(size_t)k * T + t] = (int)sr.nearest(px, py);
-        pos[(size_t)k * T + t] = make_float2(px, py);
+        arm_step(x, __builtin_elementwise_fma(splat(exf), f32x2{ua.x, ua.y}, f32x2{e.x, e.y}), dk);
+        const f32x2 p = arm_fk(x, dk);
+        const f32x2 d = p - dk.ctr;
+        slot[(size_t)k * T + t] = (int)sr.nearest_d(d.x, d.y);
+        pos[(size_t)k * T + t] = make_float2(p.x, p.y);
     }
 }
 
@@ -889,7 +990,7 @@ int stage_inputs(mppi_ctx* c, const double* x0, const double* window, int W, con
             const double* r = window + 4 * j;
             h->win[j] = make_float4((float)r[0], (float)r[1], (float)r[2], (float)r[3]);
             const double rx = r[0] - cx, ry = r[1] - cy;
-            h->key[j] = make_float4((float)rx, (float)ry, (float)(rx * rx + ry * ry), 0.f);
+            h->key[j] = make_float4((float)(-2.0 * rx), (float)(-2.0 * ry), (float)(rx * rx + ry * ry), 0.f);
         } else {
             h->win[j] = make_float4(0.f, 0.f, 0.f, 0.f);
             h->key[j] = make_float4(0.f, 0.f, kPadKey, 0.f);

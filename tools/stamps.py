@@ -71,6 +71,10 @@ for i in range(steps):
     if d[:, 15].any():
         print(f"         last rho published {us(d[:, 15].max()):5.1f} (loop end of that wg {us(d[np.argmax(d[:, 15]), 1]):5.1f})"
               f" -> final merge done {us(d[last, 11]):5.1f}")
+    st = (d[:, 0] - t0) / 100.0
+    late = np.argsort(st)[-3:][::-1]
+    print("         start offsets: med %.2f p99 %.2f max %.2f us; latest blocks %s (xcc %s)" % (
+        np.median(st), np.percentile(st, 99), st.max(), late.tolist(), (d[late, 9] & 0xF).tolist()))
     if d[:, 12].any():   # loop stamps: prologue, first 4 steps, per-step rate over the second half
         pro = (d[:, 12] - d[:, 0]) / 100.0
         b0 = (d[:, 13] - d[:, 12]) / 100.0
