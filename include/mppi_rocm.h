@@ -31,6 +31,9 @@ extern "C" {
 #define MPPI_E_HIP -2        /* HIP runtime error (message says which call)            */
 #define MPPI_E_SINGULAR -3   /* singular Sigma: the reference raises LinAlgError at   */
                              /* control.py:106 (np.linalg.inv)                          */
+#define MPPI_E_PATH_END -4   /* mppi_dropin_tick: the updated waypoint index reached   */
+                             /* the end of the path (control.py:76-78: the reference   */
+                             /* prints "[ERROR] ..." and raises IndexError)           */
 
 /* rollout flags */
 #define MPPI_FLAG_FUSED_UPDATE 1u  /* last workgroup also runs median filter, u += w_eps, */
@@ -187,6 +190,47 @@ int mppi_wait_outputs(mppi_ctx *ctx, const double *x0, double *u_out, double *tr
 int mppi_step_dropin(mppi_ctx *ctx, const double *x0, const double *window, int W, const double *u,
                      const float *noise_dev, double *S_dev, float *next_noise_dev, unsigned long long seed,
                      unsigned long long next_step, double *u_out, double *traj_out);
+
+/* The drop-in's host buffers, bound once (mppi_dropin_bind) so that a control
+ * step is one call with no arguments to convert (mppi_dropin_tick):
+ *   path, rows, stride  the caller's ref_path (rows of fp64 `stride` apart,
+ *                       columns x, y, dq1, dq2 first — run.py's
+ *                       ref_path[:, 0:4] view is one; read at every tick, so
+ *                       in-place edits are seen as the reference sees them);
+ *   fk_l1, fk_l2        self.l1, self.l2 of _get_nearest_waypoint (control.py:
+ *                       205-206);
+ *   x0                  observed_x (4 fp64), read at every tick;
+ *   idx                 [0] self.prev_waypoints_idx, in and out; [1] out: its
+ *                       value before the tick (the "prev_idx" print);
+ *   u                   self.u_prev (T x 2 fp64): read as this tick's nominal,
+ *                       then overwritten with the shifted nominal (the aliasing
+ *                       return of control.py:152);
+ *   traj                the optimal trajectory (T x 4 fp64) out, or NULL;
+ *   noise_dev, next_noise_dev, S_dev, seed: as mppi_step_dropin. */
+typedef struct {
+    const double *path;
+    int rows, stride;
+    double fk_l1, fk_l2;
+    const double *x0;
+    long long *idx;
+    double *u;
+    double *traj;
+    const float *noise_dev;
+    float *next_noise_dev;
+    double *S_dev;
+    unsigned long long seed;
+} mppi_dropin_binding;
+
+int mppi_dropin_bind(mppi_ctx *ctx, const mppi_dropin_binding *b);
+
+/* One calc_control_input (control.py:67-152) on the bound buffers: the fp64
+ * nearest-waypoint update of control.py:70-74 (_get_nearest_waypoint, :200-232:
+ * forward kinematics, first-occurrence argmin of ((x - rx)^2 + (y - ry)^2) * 100
+ * over ref_path[prev : prev + 30], the same fp64 operations), then
+ * MPPI_E_PATH_END without launching anything if the new index is at the end of
+ * the path (control.py:76-78), else mppi_step_dropin on the window
+ * ref_path[idx : idx + 30] with the next step's noise (seed, next_step). */
+int mppi_dropin_tick(mppi_ctx *ctx, unsigned long long next_step);
 
 /* Counter-based Philox4x32-10 Gaussian noise with covariance Sigma (replaces
  * np.random.multivariate_normal, control.py:163, for device-resident runs; not

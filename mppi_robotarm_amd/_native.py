@@ -18,6 +18,7 @@ MPPI_OK = 0
 MPPI_E_ARG = -1
 MPPI_E_HIP = -2
 MPPI_E_SINGULAR = -3
+MPPI_E_PATH_END = -4
 MPPI_FLAG_FUSED_UPDATE = 1
 MPPI_FLAG_EXCHANGE = 2
 MPPI_FLAG_HOST_OUT = 4
@@ -31,7 +32,7 @@ EXPORTS = (
     "mppi_set_step_inputs", "mppi_rollout", "mppi_merge_partials", "mppi_exchange_handle", "mppi_exchange_attach",
     "mppi_get_weighted_noise",
     "mppi_get_nominal", "mppi_rollout_traj", "mppi_optimal_traj", "mppi_get_step_outputs", "mppi_step_dropin",
-    "mppi_optimal_traj_host", "mppi_wait_outputs",
+    "mppi_optimal_traj_host", "mppi_wait_outputs", "mppi_dropin_bind", "mppi_dropin_tick",
     "mppi_noise_philox",
     "mppi_sync", "mppi_debug_set_buffer",
     "mppi_debug_nearest", "mppi_debug_dropin_times",
@@ -41,6 +42,13 @@ EXPORTS = (
     "mppi_chain_get_weighted_noise", "mppi_chain_get_nominal", "mppi_chain_rollout_traj",
     "mppi_chain_noise_philox", "mppi_chain_sync", "mppi_chain_debug_set_buffer",
 )
+
+
+class DropinBindingC(C.Structure):
+    _fields_ = [("path", C.c_void_p), ("rows", C.c_int), ("stride", C.c_int), ("fk_l1", C.c_double),
+                ("fk_l2", C.c_double), ("x0", C.c_void_p), ("idx", C.c_void_p), ("u", C.c_void_p),
+                ("traj", C.c_void_p), ("noise_dev", C.c_void_p), ("next_noise_dev", C.c_void_p),
+                ("S_dev", C.c_void_p), ("seed", C.c_ulonglong)]
 
 
 class ArmParamsC(C.Structure):
@@ -111,6 +119,8 @@ def open_library(path: str):
         # raw addresses (ints) for every pointer: the per-step hot call skips ctypes pointer objects
         "mppi_step_dropin": ([vp, vp, vp, C.c_int, vp, vp, vp, vp, C.c_ulonglong, C.c_ulonglong, vp, vp], C.c_int),
         "mppi_noise_philox": ([vp, C.c_ulonglong, C.c_ulonglong, fp], C.c_int),
+        "mppi_dropin_bind": ([vp, C.POINTER(DropinBindingC)], C.c_int),
+        "mppi_dropin_tick": ([vp, C.c_ulonglong], C.c_int),
         "mppi_sync": ([vp], C.c_int),
         "mppi_debug_set_buffer": ([vp, vp], C.c_int),
         "mppi_debug_dropin_times": ([vp, dp], C.c_int),

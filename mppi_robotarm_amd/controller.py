@@ -106,6 +106,8 @@ class MPPIControllerForPathTracking:
         self.host_update = bool(host_update) or self.T < 5   # the device median needs T >= 5
         self.keep_costs = False        # set True to keep per-sample S (self.last_S)
         self.last_S = None
+        self._bound = None             # what the engine's drop-in tick is bound to (_bind_key)
+        self._no_trajs = None          # the all-zero sampled_traj_list of a call without sampled trajectories
 
     # ------------------------------------------------------------ engine
     def _shard(self):
@@ -153,6 +155,11 @@ class MPPIControllerForPathTracking:
     # ------------------------------------------------------------ API
     def calc_control_input(self, observed_x: np.ndarray) -> Tuple[float, np.ndarray]:
         """calculate optimal control input (control.py:67-152)"""
+        if (self.noise_source == "device" and not self.host_update and not self.visualze_sampled_trajs
+                and self.process_group is None and self.K >= 1):
+            out = self._tick(observed_x)
+            if out is not None:
+                return out
         u = self.u_prev
         x0 = observed_x
         self._get_nearest_waypoint(x0[0], x0[1], update_prev_idx=True)
@@ -219,6 +226,62 @@ class MPPIControllerForPathTracking:
         self._prefetch_noise(eng)
         return u[0], u, optimal_traj, sampled_traj_list
 
+    def _tick(self, observed_x):
+        """The whole call in one native step (mppi_dropin_tick) when the buffers it
+        binds are plain arrays: the fp64 nearest-waypoint update and end-of-path
+        check of control.py:70-78 (the same operations as _get_nearest_waypoint),
+        then the fused device step of _dropin_step.  None: not applicable, take the
+        general path."""
+        path, u = self.ref_path, self.u_prev
+        if not (isinstance(path, np.ndarray) and path.dtype == np.float64 and path.ndim == 2 and path.shape[1] >= 4
+                and path.strides[1] == 8 and path.strides[0] % 8 == 0 and path.strides[0] >= 32
+                and isinstance(u, np.ndarray) and u.dtype == np.float64
+                and u.shape == (self.T, 2) and u.flags.c_contiguous and u.flags.writeable):
+            return None
+        sig = self.Sigma
+        if not (isinstance(sig, np.ndarray) and sig.shape == (self.dim_u, self.dim_u)):
+            return None                                    # the general path raises as the reference does
+        key = self._engine_key()
+        if self._engine is None or key != self._engine_built_for:
+            return None                                    # (re)build on the general path (LinAlgError order kept)
+        eng = self._engine
+        bkey = (eng, path, u, self.keep_costs, self.visualize_optimal_traj, self.seed, self.l1, self.l2)
+        if self._bound is None or any(a is not b for a, b in zip(bkey, self._bound)):
+            self._x_buf = np.zeros(4)
+            self._idx_buf = np.zeros(2, dtype=np.int64)
+            self._traj_buf = np.zeros((self.T, self.dim_x)) if self.visualize_optimal_traj else None
+            eng.dropin_bind(path, float(self.l1), float(self.l2), self._x_buf, self._idx_buf, u, self._traj_buf,
+                            self._noise_dev, self._noise_dev, self._S_dev if self.keep_costs else None, self.seed)
+            self._bound = bkey
+        self._x_buf[:] = np.asarray(observed_x, dtype=np.float64).ravel()[:4]
+        self._idx_buf[0] = self.prev_waypoints_idx
+        if self._noise_ready != (self.seed, self._step_count):
+            eng.philox_noise(self.seed, self._step_count, out=self._noise_dev)
+        self._step_count += 1
+        rc = eng.dropin_tick(self._step_count)
+        self.prev_waypoints_idx = int(self._idx_buf[0])
+        if self.verbose:
+            print(f"0     prev_idx = {int(self._idx_buf[1])}")
+            print(f"0     nearest_idx = {self.prev_waypoints_idx}")
+            print("======================updated=======================")
+        if rc != 0:                                        # MPPI_E_PATH_END: nothing was launched
+            self._step_count -= 1
+            print("[ERROR] Reached the end of the reference path.")
+            raise IndexError
+        self._noise_ready = (self.seed, self._step_count)
+        if self.keep_costs:
+            self.last_S = self._S_dev.cpu().numpy()
+        traj = self._traj_buf.copy() if self._traj_buf is not None else np.zeros((self.T, self.dim_x))
+        return u[0], u, traj, self._zero_trajs()
+
+    def _zero_trajs(self) -> np.ndarray:
+        """sampled_traj_list when the sampled re-roll is off (control.py:135): all
+        zeros of shape (K, T, 4).  One read-only zero-stride view instead of a fresh
+        134 MB array per call at K = 65536 (writing into it raises)."""
+        if self._no_trajs is None or self._no_trajs.shape != (self.K, self.T, self.dim_x):
+            self._no_trajs = np.broadcast_to(np.zeros(()), (self.K, self.T, self.dim_x))
+        return self._no_trajs
+
     def _dropin_step(self, eng: RolloutEngine, x0, window, u: np.ndarray):
         """control.py:81-152 on one device in one native call (mppi_step_dropin):
         rollouts + soft-min + weighted noise + median filter + u += w_eps + shift in
@@ -236,7 +299,7 @@ class MPPIControllerForPathTracking:
             self.last_S = self._S_dev.cpu().numpy()
         u[:] = u_new                                       # the shifted nominal, in place (aliasing kept)
         optimal_traj = traj if traj is not None else np.zeros((self.T, self.dim_x))
-        return u[0], u, optimal_traj, np.zeros((self.K, self.T, self.dim_x))
+        return u[0], u, optimal_traj, self._zero_trajs()
 
     def _fused_step(self, eng: RolloutEngine, x0, u: np.ndarray, world: int):
         """control.py:81-152 with the update inside the launch (the multi-GPU merge
@@ -332,3 +395,4 @@ class MPPIControllerForPathTracking:
             self._engine = None
         self._noise_ready = None       # the next engine's noise buffer is fresh: draw again
         self._engine_built_for = None
+        self._bound = None

@@ -33,6 +33,7 @@
 #include <stdlib.h>
 #include <string.h>
 
+#include <algorithm>
 #include <chrono>
 #include <string>
 #include <type_traits>
@@ -47,12 +48,18 @@ using namespace mppi;
 
 constexpr int kThreads = 256;
 
-// Device-resident per-step parameter block (ping-pong pair in the context).
-struct alignas(16) DevStep {
+// The observed state and the window of a step: a kernel argument, by value
+// (1 KiB of kernarg), so a control step stages its inputs without a copy call.
+struct alignas(16) StepStatic {
     float4 win[kSlots];   // rx, ry, rdq1, rdq2 of window slot j (lookup after argmin)
     float4 key[kSlots];   // -2 rx', -2 ry', c' = rx'^2 + ry'^2 (centred), 0; pads c' = 1e30
     float4 x0;            // q1, q2, dq1, dq2
     float4 ctr;           // window centre (cx, cy), W, 0
+};
+
+// Device-resident nominal (ping-pong pair in the context): launch n reads one
+// block and its fused update writes the next nominal into the other.
+struct alignas(16) DevStep {
     float4 ua[kMaxT];     // u0, u1, a0, a1 (a = (gamma u_t)^T Sigma^-1), fp32
     double u[kMaxT][2];   // nominal control sequence, fp64 (device closed loop)
 };
@@ -258,8 +265,6 @@ __device__ void nominal_update_block(DevStep* nxt, const KConst& c, Scratch& sm,
             }
         }
     }
-    // win / key / x0 / ctr stay in the static part of the step block (see
-    // mppi_ctx::static_valid), so only the nominal moves here.
     if (ho.p) {
         __threadfence_system();   // this thread's host stores are out before the barrier
         __syncthreads();
@@ -281,7 +286,7 @@ constexpr int kPF = 4;  // noise rows in flight per lane
 // last workgroup to arrive on a counter merges (arrive_last).
 template <int LPS, int NT, bool POLL>
 __global__ __launch_bounds__(NT) void rollout_kernel(
-    const KConst c, const DevStep* __restrict__ st, const float2* __restrict__ noise,
+    const KConst c, const StepStatic ss, const DevStep* __restrict__ st, const float2* __restrict__ noise,
     double* __restrict__ S_out, double* __restrict__ slab, double* __restrict__ gslab,
     unsigned* __restrict__ counters, double* __restrict__ partial_out, double* __restrict__ w_eps_out,
     DevStep* __restrict__ nxt, unsigned flags, const XDesc xd, unsigned* __restrict__ epoch, unsigned* __restrict__ tmo,
@@ -320,11 +325,11 @@ __global__ __launch_bounds__(NT) void rollout_kernel(
     const double u_first = (flags & MPPI_FLAG_FUSED_UPDATE) ? nominal_first(st, tid) : 0.0;
     // window row for the LDS copy: loaded unconditionally (a load inside the
     // tid < kSlots branch would be waited for right there), stored before the barrier
-    const float4 wrow = st->win[tid & (kSlots - 1)];
+    const float4 wrow = ss.win[tid & (kSlots - 1)];
     Search<LPS> sr;
-    sr.load(st->key, st->ctr, tid & (LPS - 1));
+    sr.load(ss.key, ss.ctr, tid & (LPS - 1));
     Arm x;
-    arm_init(x, st->x0);
+    arm_init(x, ss.x0);
     const DynK dk = make_dynk(c, sr.cx, sr.cy);
     // the per-step constants go to LDS: the ring reads them there, so no scalar
     // load shares lgkmcnt with the deferred row lookup below
@@ -618,7 +623,7 @@ __global__ __launch_bounds__(NT) void merge_kernel(const KConst c, const double*
 }
 
 // Trajectory re-roll (control.py:129-145): control(t) = base[(t-1) mod T] (+ eps).
-__global__ __launch_bounds__(kThreads) void traj_kernel(const KConst c, const DevStep* __restrict__ st,
+__global__ __launch_bounds__(kThreads) void traj_kernel(const KConst c, const StepStatic ss,
                                                         const float2* __restrict__ base,
                                                         const float2* __restrict__ noise, int Kn,
                                                         float4* __restrict__ out) {
@@ -627,7 +632,7 @@ __global__ __launch_bounds__(kThreads) void traj_kernel(const KConst c, const De
     const int T = c.T;
     const float exf = noise ? ((c.k_offset + k) < c.k_exploit ? 1.f : 0.f) : 1.f;
     Arm x;
-    arm_init(x, st->x0);
+    arm_init(x, ss.x0);
     const DynK dk = make_dynk(c, 0.f, 0.f);
     for (int t = 0; t < T; ++t) {
         const int ti = t == 0 ? T - 1 : t - 1;
@@ -647,7 +652,8 @@ __global__ __launch_bounds__(kThreads) void traj_kernel(const KConst c, const De
 // sample and step as the rollout evaluates it — the same dyn_step and
 // Search<1>::nearest on the same inputs, so the same fp32 positions and slots —
 // with the end-effector position: slot[k][t], pos[k][t] = (px, py).
-__global__ __launch_bounds__(kThreads) void nearest_debug_kernel(const KConst c, const DevStep* __restrict__ st,
+__global__ __launch_bounds__(kThreads) void nearest_debug_kernel(const KConst c, const StepStatic ss,
+                                                                 const DevStep* __restrict__ st,
                                                                  const float2* __restrict__ noise, int Kn,
                                                                  int* __restrict__ slot, float2* __restrict__ pos) {
     const int k = blockIdx.x * kThreads + threadIdx.x;
@@ -655,9 +661,9 @@ __global__ __launch_bounds__(kThreads) void nearest_debug_kernel(const KConst c,
     const int T = c.T;
     const float exf = (c.k_offset + k) < c.k_exploit ? 1.f : 0.f;
     Search<1> sr;
-    sr.load(st->key, st->ctr, 0);
+    sr.load(ss.key, ss.ctr, 0);
     Arm x;
-    arm_init(x, st->x0);
+    arm_init(x, ss.x0);
     const DynK dk = make_dynk(c, sr.cx, sr.cy);
     for (int t = 0; t < T; ++t) {
         const float4 ua = st->ua[t];
@@ -700,14 +706,15 @@ struct mppi_ctx {
     hipStream_t stream = nullptr;
     int lps = 1, nt = 256, nblocks = 0;
     KConst kc;
-    DevStep* d_step = nullptr;  // [2] ping-pong
+    StepStatic stat{};          // x0 + window of the next launch (a kernel argument)
+    DevStep* d_step = nullptr;  // [2] ping-pong nominal
     int cur = 0;
-    // static part (win, key, x0, ctr) up to date in block i; the drop-in stages
-    // one block per step (one copy), the others fetch it on demand (ensure_static)
-    bool static_valid[2] = {false, false};
-    DevStep* h_step = nullptr;  // pinned staging
+    DevStep* h_step = nullptr;  // pinned staging of an uploaded nominal
     hipEvent_t staged = nullptr;
     bool stage_pending = false;     // a staging copy may still be reading h_step
+    // the current device nominal is the one the last MPPI_FLAG_HOST_OUT launch
+    // published (h_dout): a drop-in step whose u equals it uploads nothing
+    bool nominal_published = false;
     double* h_dout = nullptr;       // coherent host-mapped drop-in outputs (HostOut layout)
     double* d_dout = nullptr;       // its device view
     unsigned dseq = 0;
@@ -726,6 +733,10 @@ struct mppi_ctx {
     float2* d_upd = nullptr;    // updated, unshifted controls of the last fused update (optimal trajectory)
     bool upd_valid = false;
     double* h_out = nullptr;    // pinned: nominal (2T fp64) + optimal trajectory (4T fp32) of mppi_get_step_outputs
+    mppi_dropin_binding bind{};  // mppi_dropin_bind
+    bool bound = false;
+    std::chrono::steady_clock::time_point tick_t0{};   // start of the current mppi_dropin_tick (phase times)
+    bool in_tick = false;
     double sig_inv[4];
     unsigned long long* d_dbg = nullptr;  // diagnostic stamp buffer (MPPI_STAMPS builds)
     // node-level exchange (mppi_exchange_*): inbox, this rank's row, epoch, peer mappings
@@ -968,16 +979,16 @@ int mppi_ctx_info(const mppi_ctx* c, int* lps, int* blocks, int* threads) {
 
 namespace {
 
-// Fill the pinned staging block from the host inputs and copy it to the device
-// (stream-ordered).  both: the static part into both ping-pong blocks and the
-// nominal (if given) into the current one (mppi_set_step_inputs, device loops);
-// otherwise one copy: with a nominal the current block becomes block 0 and
-// takes static part + nominal contiguously (the drop-in's per-step form).
-int stage_inputs(mppi_ctx* c, const double* x0, const double* window, int W, const double* u, bool both) {
+// Stage a step's inputs.  The observed state and the window (with its centred
+// search keys, fp64 on the host then fp32) go into the host copy c->stat, which
+// every launch passes by value: no copy call.  A nominal u, when given, is
+// uploaded into the current ping-pong block (one stream-ordered copy from
+// pinned staging) — unless `skip_same` and u is exactly the nominal the last
+// drop-in launch published, which that launch already left on the device.
+int stage_inputs(mppi_ctx* c, const double* x0, const double* window, int W, const double* u, bool skip_same) {
     if (!x0 || !window) return fail(MPPI_E_ARG, "null argument");
     if (W < 1 || W > MPPI_SEARCH_LEN) return fail(MPPI_E_ARG, "window rows must be in [1, 30]");
-    if (c->stage_pending) HIP_TRY(hipEventSynchronize(c->staged));  // staging block free again
-    DevStep* h = c->h_step;
+    StepStatic& h = c->stat;
     double cx = 0.0, cy = 0.0;
     for (int j = 0; j < W; ++j) {
         cx += window[4 * j];
@@ -988,52 +999,37 @@ int stage_inputs(mppi_ctx* c, const double* x0, const double* window, int W, con
     for (int j = 0; j < kSlots; ++j) {
         if (j < W) {
             const double* r = window + 4 * j;
-            h->win[j] = make_float4((float)r[0], (float)r[1], (float)r[2], (float)r[3]);
+            h.win[j] = make_float4((float)r[0], (float)r[1], (float)r[2], (float)r[3]);
             const double rx = r[0] - cx, ry = r[1] - cy;
-            h->key[j] = make_float4((float)(-2.0 * rx), (float)(-2.0 * ry), (float)(rx * rx + ry * ry), 0.f);
+            h.key[j] = make_float4((float)(-2.0 * rx), (float)(-2.0 * ry), (float)(rx * rx + ry * ry), 0.f);
         } else {
-            h->win[j] = make_float4(0.f, 0.f, 0.f, 0.f);
-            h->key[j] = make_float4(0.f, 0.f, kPadKey, 0.f);
+            h.win[j] = make_float4(0.f, 0.f, 0.f, 0.f);
+            h.key[j] = make_float4(0.f, 0.f, kPadKey, 0.f);
         }
     }
-    h->x0 = make_float4((float)x0[0], (float)x0[1], (float)x0[2], (float)x0[3]);
-    h->ctr = make_float4((float)cx, (float)cy, (float)W, 0.f);
-    size_t bytes = offsetof(DevStep, ua);
-    if (u) {
-        const KConst& k = c->kc;
-        for (int t = 0; t < c->cfg.T; ++t) {
-            const double u0 = u[2 * t], u1 = u[2 * t + 1];
-            const double g0 = k.gamma * u0, g1 = k.gamma * u1;  // ((gamma u^T) Sigma^-1), control.py:106
-            const double a0 = g0 * k.sig_inv[0] + g1 * k.sig_inv[2];
-            const double a1 = g0 * k.sig_inv[1] + g1 * k.sig_inv[3];
-            h->ua[t] = make_float4((float)u0, (float)u1, (float)a0, (float)a1);
-            h->u[t][0] = u0;
-            h->u[t][1] = u1;
-        }
-        bytes = sizeof(DevStep);
+    h.x0 = make_float4((float)x0[0], (float)x0[1], (float)x0[2], (float)x0[3]);
+    h.ctr = make_float4((float)cx, (float)cy, (float)W, 0.f);
+    if (!u) return MPPI_OK;
+    const int T = c->cfg.T;
+    if (skip_same && c->nominal_published && !memcmp(u, c->h_dout + 4, 2 * (size_t)T * sizeof(double)))
+        return MPPI_OK;
+    if (c->stage_pending) HIP_TRY(hipEventSynchronize(c->staged));  // staging block free again
+    DevStep* d = c->h_step;
+    const KConst& k = c->kc;
+    for (int t = 0; t < T; ++t) {
+        const double u0 = u[2 * t], u1 = u[2 * t + 1];
+        const double g0 = k.gamma * u0, g1 = k.gamma * u1;  // ((gamma u^T) Sigma^-1), control.py:106
+        const double a0 = g0 * k.sig_inv[0] + g1 * k.sig_inv[2];
+        const double a1 = g0 * k.sig_inv[1] + g1 * k.sig_inv[3];
+        d->ua[t] = make_float4((float)u0, (float)u1, (float)a0, (float)a1);
+        d->u[t][0] = u0;
+        d->u[t][1] = u1;
     }
-    if (both) {
-        HIP_TRY(hipMemcpyAsync(c->d_step + (c->cur ^ 1), h, offsetof(DevStep, ua), hipMemcpyHostToDevice, c->stream));
-        c->static_valid[c->cur ^ 1] = true;
-    } else {
-        if (u) c->cur = 0;
-        c->static_valid[c->cur ^ 1] = false;
-    }
-    HIP_TRY(hipMemcpyAsync(c->d_step + c->cur, h, bytes, hipMemcpyHostToDevice, c->stream));
-    c->static_valid[c->cur] = true;
+    HIP_TRY(hipMemcpyAsync(c->d_step + c->cur, d, sizeof(DevStep), hipMemcpyHostToDevice, c->stream));
     HIP_TRY(hipEventRecord(c->staged, c->stream));
     c->stage_pending = true;
-    return MPPI_OK;
-}
-
-// The static part of the current block before a kernel reads it: a
-// device-to-device copy from the other block if the drop-in staged only that one.
-int ensure_static(mppi_ctx* c) {
-    if (c->static_valid[c->cur]) return MPPI_OK;
-    if (!c->static_valid[c->cur ^ 1]) return MPPI_OK;   // nothing staged yet: zeros, as before
-    HIP_TRY(hipMemcpyAsync(c->d_step + c->cur, c->d_step + (c->cur ^ 1), offsetof(DevStep, ua),
-                           hipMemcpyDeviceToDevice, c->stream));
-    c->static_valid[c->cur] = true;
+    c->nominal_published = false;
+    c->upd_valid = false;
     return MPPI_OK;
 }
 
@@ -1069,6 +1065,7 @@ int wait_host_out(mppi_ctx* c) {
         __builtin_ia32_pause();
     }
     c->stage_pending = false;   // the launch ran, so every staging copy before it did too
+    c->nominal_published = true;
     return check_timeout(c);
 }
 
@@ -1101,7 +1098,7 @@ extern "C" {
 
 int mppi_set_step_inputs(mppi_ctx* c, const double* x0, const double* window, int W, const double* u) {
     if (!c) return fail(MPPI_E_ARG, "null argument");
-    return stage_inputs(c, x0, window, W, u, true);
+    return stage_inputs(c, x0, window, W, u, false);
 }
 
 int mppi_rollout(mppi_ctx* c, const float* noise_dev, double* S_dev, double* partial_dev, unsigned flags) {
@@ -1123,14 +1120,13 @@ int launch_rollout(mppi_ctx* c, const float* noise_dev, double* S_dev, double* p
         if (partial_dev) return fail(MPPI_E_ARG, "MPPI_FLAG_EXCHANGE merges on device: no partial_out");
         partial_dev = c->d_xrow;
     }
-    if (int rc = ensure_static(c)) return rc;
     const DevStep* cur = c->d_step + c->cur;
     DevStep* nxt = c->d_step + (c->cur ^ 1);
     const float2* nz = reinterpret_cast<const float2*>(noise_dev);
 #define MPPI_LAUNCH(L, NTH, P)                                                                                   \
-    hipLaunchKernelGGL((rollout_kernel<L, NTH, P>), dim3(c->nblocks), dim3(NTH), 0, c->stream, c->kc, cur, nz, S_dev,  \
-                       c->d_slab, c->d_gslab, c->d_counter, partial_dev, c->d_weps, nxt, flags, c->xd, c->d_epoch,       \
-                       c->d_tmo, reinterpret_cast<float*>(c->d_upd), ho, c->d_dbg)
+    hipLaunchKernelGGL((rollout_kernel<L, NTH, P>), dim3(c->nblocks), dim3(NTH), 0, c->stream, c->kc, c->stat, cur, nz, \
+                       S_dev, c->d_slab, c->d_gslab, c->d_counter, partial_dev, c->d_weps, nxt, flags, c->xd,          \
+                       c->d_epoch, c->d_tmo, reinterpret_cast<float*>(c->d_upd), ho, c->d_dbg)
 #define MPPI_LAUNCH_P(L, NTH)                \
     do {                                     \
         if (c->poll) MPPI_LAUNCH(L, NTH, true);  \
@@ -1151,6 +1147,7 @@ int launch_rollout(mppi_ctx* c, const float* noise_dev, double* S_dev, double* p
     if (rc == MPPI_OK && (flags & MPPI_FLAG_FUSED_UPDATE)) {
         c->cur ^= 1;
         c->upd_valid = true;
+        c->nominal_published = false;   // until wait_host_out sees this launch's outputs
     }
     return rc;
 }
@@ -1221,6 +1218,7 @@ int mppi_merge_partials(mppi_ctx* c, const double* partials_dev, int n, unsigned
     if (rc == MPPI_OK && (flags & MPPI_FLAG_FUSED_UPDATE)) {
         c->cur ^= 1;
         c->upd_valid = true;
+        c->nominal_published = false;   // until wait_host_out sees this launch's outputs
     }
     return rc;
 }
@@ -1246,7 +1244,6 @@ int mppi_get_nominal(mppi_ctx* c, double* u_host) {
 
 int mppi_rollout_traj(mppi_ctx* c, const double* base_u, const float* noise_dev, int K, float* out_dev) {
     if (!c || !out_dev || K < 1 || K > c->cfg.K_local) return fail(MPPI_E_ARG, "bad argument");
-    if (int rc = ensure_static(c)) return rc;
     const DevStep* cur = c->d_step + c->cur;
     const float2* base;
     if (base_u) {
@@ -1262,7 +1259,7 @@ int mppi_rollout_traj(mppi_ctx* c, const double* base_u, const float* noise_dev,
         base = c->d_base;
     }
     const int blocks = (K + kThreads - 1) / kThreads;
-    hipLaunchKernelGGL(traj_kernel, dim3(blocks), dim3(kThreads), 0, c->stream, c->kc, cur, base,
+    hipLaunchKernelGGL(traj_kernel, dim3(blocks), dim3(kThreads), 0, c->stream, c->kc, c->stat, base,
                        reinterpret_cast<const float2*>(noise_dev), K, reinterpret_cast<float4*>(out_dev));
     return launch_check("traj_kernel");
 }
@@ -1270,9 +1267,7 @@ int mppi_rollout_traj(mppi_ctx* c, const double* base_u, const float* noise_dev,
 int mppi_optimal_traj(mppi_ctx* c, float* out_dev) {
     if (!c || !out_dev) return fail(MPPI_E_ARG, "null argument");
     if (!c->upd_valid) return fail(MPPI_E_ARG, "mppi_optimal_traj needs a preceding MPPI_FLAG_FUSED_UPDATE launch");
-    if (int rc = ensure_static(c)) return rc;
-    // x0 and the window are in both ping-pong blocks, so the current one serves
-    hipLaunchKernelGGL(traj_kernel, dim3(1), dim3(kThreads), 0, c->stream, c->kc, c->d_step + c->cur, c->d_upd,
+    hipLaunchKernelGGL(traj_kernel, dim3(1), dim3(kThreads), 0, c->stream, c->kc, c->stat, c->d_upd,
                        (const float2*)nullptr, 1, reinterpret_cast<float4*>(out_dev));
     return launch_check("traj_kernel");
 }
@@ -1327,9 +1322,10 @@ int mppi_step_dropin(mppi_ctx* c, const double* x0, const double* window, int W,
     if (c->cfg.T < 5) return fail(MPPI_E_ARG, "device median filter needs T >= 5 (use the host update)");
     if (c->xd.world > 1) return fail(MPPI_E_ARG, "mppi_step_dropin is the single-device path");
     using clk = std::chrono::steady_clock;
-    const auto t0 = clk::now();
+    const auto t0 = c->in_tick ? c->tick_t0 : clk::now();   // a tick's phases include its waypoint update
+    c->in_tick = false;
     auto mark = [&](int i) { c->dropin_us[i] = std::chrono::duration<double, std::micro>(clk::now() - t0).count(); };
-    if (int rc = stage_inputs(c, x0, window, W, u, false)) return rc;
+    if (int rc = stage_inputs(c, x0, window, W, u, true)) return rc;
     mark(0);
     const unsigned fl = MPPI_FLAG_FUSED_UPDATE | MPPI_FLAG_HOST_OUT;
     if (int rc = launch_rollout(c, noise_dev, S_dev, nullptr, fl, next_host_out(c, fl))) return rc;
@@ -1345,6 +1341,62 @@ int mppi_step_dropin(mppi_ctx* c, const double* x0, const double* window, int W,
     if (int rc = mppi_wait_outputs(c, x0, u_out, traj_out)) return rc;   // already published: copies + trajectory
     mark(4);
     return MPPI_OK;
+}
+
+int mppi_dropin_bind(mppi_ctx* c, const mppi_dropin_binding* b) {
+    if (!c || !b) return fail(MPPI_E_ARG, "null argument");
+    if (!b->path || b->rows < 1 || b->stride < 4 || !b->x0 || !b->idx || !b->u || !b->noise_dev)
+        return fail(MPPI_E_ARG, "binding: path (rows >= 1, stride >= 4), x0, idx, u and noise_dev are required");
+    c->bind = *b;
+    c->bound = true;
+    return MPPI_OK;
+}
+
+int mppi_dropin_tick(mppi_ctx* c, unsigned long long next_step) {
+    if (!c) return fail(MPPI_E_ARG, "null context");
+    if (!c->bound) return fail(MPPI_E_ARG, "mppi_dropin_tick before mppi_dropin_bind");
+    const mppi_dropin_binding& b = c->bind;
+    c->tick_t0 = std::chrono::steady_clock::now();
+    c->in_tick = true;
+    // _get_nearest_waypoint(x0[0], x0[1], update_prev_idx=True), control.py:200-232, in the
+    // reference's fp64 operations (NumPy's float64 cos/sin are the C library's)
+    const double q1 = b.x0[0], q2 = b.x0[1];
+    const double x = b.fk_l1 * cos(q1) + b.fk_l2 * cos(q1 + q2);
+    const double y = b.fk_l1 * sin(q1) + b.fk_l2 * sin(q1 + q2);
+    const long long prev = b.idx[0];
+    if (prev < 0 || prev >= b.rows) {
+        c->in_tick = false;
+        return fail(MPPI_E_ARG, "prev_waypoints_idx outside ref_path");
+    }
+    const int n = (int)std::min<long long>(MPPI_SEARCH_LEN, b.rows - prev);
+    int best = 0;
+    double dmin = 0.0;
+    for (int j = 0; j < n; ++j) {   // np.argmin: the first NaN if there is one, else the first minimum
+        const double* r = b.path + (prev + j) * (long long)b.stride;
+        const double dx = x - r[0], dy = y - r[1];
+        const double d = (dx * dx + dy * dy) * 100;
+        if (d != d) {
+            best = j;
+            break;
+        }
+        if (j == 0 || d < dmin) {
+            dmin = d;
+            best = j;
+        }
+    }
+    const long long idx = prev + best;
+    b.idx[1] = prev;
+    b.idx[0] = idx;
+    if (idx >= b.rows - 1) {
+        c->in_tick = false;
+        return fail(MPPI_E_PATH_END, "Reached the end of the reference path.");
+    }
+    // the window ref_path[idx : idx + 30, 0:4] (control.py:203-204, slice-truncated)
+    const int W = (int)std::min<long long>(MPPI_SEARCH_LEN, b.rows - idx);
+    double win[4 * MPPI_SEARCH_LEN];
+    for (int j = 0; j < W; ++j) memcpy(win + 4 * j, b.path + (idx + j) * (long long)b.stride, 4 * sizeof(double));
+    return mppi_step_dropin(c, b.x0, win, W, b.u, b.noise_dev, b.S_dev, b.next_noise_dev, b.seed, next_step, b.u,
+                            b.traj);
 }
 
 int mppi_noise_philox(mppi_ctx* c, unsigned long long seed, unsigned long long step, float* out_dev) {
@@ -1371,9 +1423,8 @@ int mppi_debug_set_buffer(mppi_ctx* c, void* dbg_dev) {
 
 int mppi_debug_nearest(mppi_ctx* c, const float* noise_dev, int K, int* slot_dev, float* pos_dev) {
     if (!c || !noise_dev || !slot_dev || !pos_dev || K < 1 || K > c->cfg.K_local) return fail(MPPI_E_ARG, "bad argument");
-    if (int rc = ensure_static(c)) return rc;
     hipLaunchKernelGGL(nearest_debug_kernel, dim3((K + kThreads - 1) / kThreads), dim3(kThreads), 0, c->stream, c->kc,
-                       c->d_step + c->cur, reinterpret_cast<const float2*>(noise_dev), K, slot_dev,
+                       c->stat, c->d_step + c->cur, reinterpret_cast<const float2*>(noise_dev), K, slot_dev,
                        reinterpret_cast<float2*>(pos_dev));
     return launch_check("nearest_debug_kernel");
 }

@@ -273,6 +273,36 @@ class RolloutEngine:
             self._u_out.ctypes.data, traj.ctypes.data if traj is not None else None), "mppi_step_dropin")
         return self._u_out, traj
 
+    def dropin_bind(self, path: np.ndarray, fk_l1: float, fk_l2: float, x_buf: np.ndarray, idx_buf: np.ndarray,
+                    u: np.ndarray, traj_buf: np.ndarray | None, noise: torch.Tensor,
+                    next_noise: torch.Tensor | None, S_out: torch.Tensor | None, seed: int) -> None:
+        """Bind the host buffers of dropin_tick (mppi_dropin_bind).  path: fp64 (rows, >= 4)
+        with unit column stride (any row stride: run.py's ref_path[:, 0:4] is a view); x_buf: fp64 (4,); idx_buf: int64 (2,); u: C-contiguous fp64 (T, 2),
+        updated in place; traj_buf: fp64 (T, 4) or None.  The arrays must outlive the
+        binding (the caller keeps them)."""
+        self._check_noise(noise)
+        if next_noise is not None:
+            self._check_noise(next_noise)
+        b = N.DropinBindingC()
+        b.path, b.rows, b.stride = path.ctypes.data, path.shape[0], path.strides[0] // 8
+        b.fk_l1, b.fk_l2 = float(fk_l1), float(fk_l2)
+        b.x0, b.idx, b.u = x_buf.ctypes.data, idx_buf.ctypes.data, u.ctypes.data
+        b.traj = traj_buf.ctypes.data if traj_buf is not None else None
+        b.noise_dev = noise.data_ptr()
+        b.next_noise_dev = next_noise.data_ptr() if next_noise is not None else None
+        b.S_dev = S_out.data_ptr() if S_out is not None else None
+        b.seed = int(seed) & 0xFFFFFFFFFFFFFFFF
+        N.check(self._lib.mppi_dropin_bind(self._ctx, C.byref(b)), "mppi_dropin_bind")
+
+    def dropin_tick(self, next_step: int) -> int:
+        """One bound drop-in step (mppi_dropin_tick): MPPI_OK, or MPPI_E_PATH_END
+        (nothing launched); any other failure raises."""
+        self._sync_stream()
+        rc = self._lib.mppi_dropin_tick(self._ctx, next_step)
+        if rc != N.MPPI_OK and rc != N.MPPI_E_PATH_END:
+            N.check(rc, "mppi_dropin_tick")
+        return rc
+
     def dropin_times(self) -> np.ndarray:
         """Diagnostics: phase ends (us) of the last step_dropin (mppi_debug_dropin_times)."""
         out = np.zeros(5)

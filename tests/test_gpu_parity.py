@@ -616,3 +616,55 @@ def test_sigma_and_lambda_reread_per_call(paths):
     eps = np.random.multivariate_normal(np.zeros(2), sig2, (4096, 32)).astype(np.float32).astype(np.float64)
     want = oc.calc_control_input(X0, epsilon=eps)[1]
     assert _urel(got, want) < U_TOL
+
+
+def test_bound_tick_equals_general_dropin(paths):
+    """The one-call tick (mppi_dropin_tick: native nearest-waypoint update, no
+    input copy when u_prev is the nominal the last step published) against the
+    general drop-in path on the same device noise, bit for bit: u, the aliasing,
+    prev_waypoints_idx and the optimal trajectory, over ticks that move along the
+    path, an in-place edit of u_prev and of ref_path between ticks (both must be
+    seen), and the end of the path (IndexError at the same index, nothing run)."""
+    from mppi_robotarm_amd.controller import MPPIControllerForPathTracking
+    base = paths["xydq_circle"][:60].copy()
+    kw = dict(delta_t=0.006, horizon_step_T=16, number_of_samples_K=2048, verbose=False, noise="device", seed=3,
+              device=0, **RUNPY)
+    fast = MPPIControllerForPathTracking(ref_path=base[:, 0:4], **kw)          # strided view, like run.py
+    slow = MPPIControllerForPathTracking(ref_path=base[:, 0:4].tolist(), **kw)  # not an ndarray: general path
+    slow.ref_path = np.array(slow.ref_path)[:, :4].copy(order="F")             # column-major: no tick either
+    assert fast._tick is not None
+    x = X0.copy()
+    for tick in range(40):
+        if tick == 4:
+            for c in (fast, slow):
+                c.u_prev += 0.25                    # caller edits the nominal in place
+        if tick == 6:
+            base[10:40, 0] += 1e-3                  # caller edits the path in place (the view sees it)
+            slow.ref_path[10:40, 0] += 1e-3
+        outs = []
+        for c in (fast, slow):
+            u_prev = c.u_prev
+            try:
+                u0, u_seq, opt, samp = c.calc_control_input(x)
+            except IndexError:
+                outs.append(None)
+                continue
+            assert u_seq is u_prev and np.shares_memory(u0, u_prev)
+            assert samp.shape == (2048, 16, 4) and not samp.any()
+            outs.append((u_seq.copy(), opt.copy(), c.prev_waypoints_idx))
+        if outs[0] is None or outs[1] is None:
+            assert outs[0] is None and outs[1] is None, tick
+            assert fast.prev_waypoints_idx == slow.prev_waypoints_idx >= 58
+            break
+        (ua, oa, ia), (ub, ob, ib) = outs
+        assert ia == ib and np.array_equal(ua, ub) and np.array_equal(oa, ob), tick
+        x = oa[4].copy()                            # move along the planned trajectory
+        if tick >= 8:                               # then jump to the last waypoint (2-link IK, elbow as X0)
+            px, py = base[59, 0], base[59, 1]
+            q2 = -np.arccos((px * px + py * py - 2.0) / 2.0)
+            x = np.array([np.arctan2(py, px) - np.arctan2(np.sin(q2), 1.0 + np.cos(q2)), q2, 0.0, 0.0])
+    else:
+        raise AssertionError("the path end was never reached")
+    assert fast._bound is not None                  # the fast controller really took the tick
+    fast.close()
+    slow.close()

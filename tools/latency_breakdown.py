@@ -1,15 +1,16 @@
 """Where the drop-in's control-step latency goes (diagnostic tool, not product).
 
 MPPIControllerForPathTracking.calc_control_input at the bench's K, T with device
-noise, on the fused single-call path (mppi_step_dropin):
+noise, on the one-call tick (mppi_dropin_tick: native waypoint update, inputs
+staged as kernel arguments, fused launch, wait, host trajectory, next noise):
 
   * closed loop: run.py's driver (harness), plant work between ticks — the
     bench's control_step_latency_ms;
   * back to back: calls with nothing in between (the next step's Philox draw,
     queued behind each call, is then paid by the following call);
-  * phases of one call: Python before the native call (waypoint update, checks,
-    engine lookup), the native call (stage + launch + wait + host trajectory +
-    queue the next noise), Python after; the device work alone (one fused
+  * phases of one call: Python before the native call (checks, engine lookup,
+    buffer binding check), the native call (waypoint update + stage + launch +
+    queue the next noise + wait + host trajectory), Python after; the device work alone (one fused
     rollout launch, and one Philox draw, HIP-event timed on the stream).
 
     python tools/latency_breakdown.py [K T calls]
@@ -51,7 +52,7 @@ def main():
         c.prev_waypoints_idx = 0
     eng = c._get_engine()
     stamps = []
-    native = eng.step_dropin
+    native = eng.dropin_tick
 
     def timed(*args, **kwargs):
         t0 = time.perf_counter()
@@ -59,7 +60,7 @@ def main():
         stamps.append((t0, time.perf_counter()))
         return out
 
-    eng.step_dropin = timed
+    eng.dropin_tick = timed
     whole, pre, nat, post = [], [], [], []
     for _ in range(n):
         c.prev_waypoints_idx = 0
@@ -71,7 +72,7 @@ def main():
         pre.append(t1 - t0)
         nat.append(t2 - t1)
         post.append(t3 - t2)
-    eng.step_dropin = native
+    eng.dropin_tick = native
     phases = []
     for _ in range(n):
         c.prev_waypoints_idx = 0
@@ -94,13 +95,13 @@ def main():
         phil.append(ev[1].elapsed_time(ev[2]) * 1e-3)
     c.close()
 
-    print(f"K={K} T={T}, device noise, fused single-call drop-in (mppi_step_dropin), {n} calls")
+    print(f"K={K} T={T}, device noise, one-call drop-in tick (mppi_dropin_tick), {n} calls")
     print(f"  closed loop (run.py driver, plant between ticks) {us(closed)}")
     print(f"  back to back (no work between calls)             {us(whole)}")
     print(f"    Python before the native call                  {us(pre)}")
     print(f"    native call (stage, launch, wait, traj, noise) {us(nat)}")
     print(f"    Python after                                   {us(post)}")
-    names = ["stage inputs (host keys + H2D copy issued)", "launch fused rollout", "queue next Philox draw",
+    names = ["waypoint update + stage inputs (host keys)", "launch fused rollout", "queue next Philox draw",
              "wait for the rollout's outputs", "copy outputs + fp64 optimal trajectory"]
     prev = np.zeros(len(phases))
     for i, nm in enumerate(names):
