@@ -394,6 +394,7 @@ struct MergeScratch {
     double weps[MAXV];
     double unew[MAXV];
     double rho[kDirectRows];  // direct merge: the rows' rho, polled by wave 0
+    double part[2 * kDirectRows];  // direct merge: per row-group column sums (one group per ncol threads)
     int nrel;
 };
 
@@ -662,7 +663,14 @@ __device__ __forceinline__ bool direct_merge(__amdgpu_buffer_rsrc_t rows, int n,
         rel[j] = __ballot(s_l[j] != 0.0);
         nrel += __popcll(rel[j]);
     }
-    if (nrel > kDirectMax) return false;
+    // Phase 2 spreads the weighted rows over row groups when the merged columns
+    // fill less than the workgroup (one column chunk: G = NT / ncol groups of
+    // ncol threads, group g taking every G-th row), so one batch of loads covers
+    // kDirectMax * G rows; up to two batches (and 64 rows, one lane each) stay
+    // direct.  With one group (config 3's 129 columns) the measured optimum is
+    // one batch of 16 rows (the group mergers' overlap wins beyond it).
+    const int G = MAXCH == 1 ? max(1, NT / ncol) : 1;
+    if (nrel > (G > 1 ? min(64, 2 * kDirectMax * G) : kDirectMax)) return false;
     // lane k < nrel: the k-th weighted row (ascending) and its factor
     int k = lane, row = 0;
     bool found = false;
@@ -688,45 +696,102 @@ __device__ __forceinline__ bool direct_merge(__amdgpu_buffer_rsrc_t rows, int n,
     double acc[MAXCH], eta = 0.0, eta_k = 0.0;
 #pragma unroll
     for (int ch = 0; ch < MAXCH; ++ch) acc[ch] = 0.0;
-    for (int b0 = 0; b0 < nrel; b0 += RB) {
-        double v[LB];
-        if constexpr (GRAN) {
-            u32x4 ge, gv[LB];
-            for (unsigned spins = 0;; ++spins) {
-                asm volatile("" ::: "memory");
-                ge = ld_gran(rows, (b0 == 0 && mine) ? row * stride + 1 : kOffRange);
-                bool ok = !(b0 == 0 && mine) || gran_ok(ge, tag);
+    if (G == 1) {
+        // one group: the rows of a batch are wave-uniform (v_readlane); eta as a
+        // scalar in the same row order as column 0
+        for (int b0 = 0; b0 < nrel; b0 += RB) {
+            double v[LB];
+            if constexpr (GRAN) {
+                u32x4 ge, gv[LB];
+                for (unsigned spins = 0;; ++spins) {
+                    asm volatile("" ::: "memory");
+                    ge = ld_gran(rows, (b0 == 0 && mine) ? row * stride + 1 : kOffRange);
+                    bool ok = !(b0 == 0 && mine) || gran_ok(ge, tag);
+#pragma unroll
+                    for (int j = 0; j < LB; ++j) {
+                        const int i = b0 + j / MAXCH, col = tid + (j % MAXCH) * NT;
+                        const bool on = i < nrel && col < ncol;
+                        gv[j] = ld_gran(rows, on ? __builtin_amdgcn_readlane(row, i) * stride + 1 + col : kOffRange);
+                        ok = ok && (!on || gran_ok(gv[j], tag));
+                    }
+                    if (__all(ok)) break;
+                    MPPI_SPIN_OR_GIVE_UP(spins, tmo, lane);
+                }
+                if (b0 == 0) eta_k = gran_val(ge);
+#pragma unroll
+                for (int j = 0; j < LB; ++j) v[j] = gran_val(gv[j]);
+            } else {
+                if (b0 == 0) eta_k = ld_wt(rows, mine ? row * stride + 1 : kOffRange);
 #pragma unroll
                 for (int j = 0; j < LB; ++j) {
                     const int i = b0 + j / MAXCH, col = tid + (j % MAXCH) * NT;
-                    const bool on = i < nrel && col < ncol;
-                    gv[j] = ld_gran(rows, on ? __builtin_amdgcn_readlane(row, i) * stride + 1 + col : kOffRange);
-                    ok = ok && (!on || gran_ok(gv[j], tag));
+                    v[j] = ld_wt(rows, (i < nrel && col < ncol) ? __builtin_amdgcn_readlane(row, i) * stride + 1 + col
+                                                                 : kOffRange);
                 }
-                if (__all(ok)) break;
-                MPPI_SPIN_OR_GIVE_UP(spins, tmo, lane);
             }
-            if (b0 == 0) eta_k = gran_val(ge);
-#pragma unroll
-            for (int j = 0; j < LB; ++j) v[j] = gran_val(gv[j]);
-        } else {
-            if (b0 == 0) eta_k = ld_wt(rows, mine ? row * stride + 1 : kOffRange);
 #pragma unroll
             for (int j = 0; j < LB; ++j) {
-                const int i = b0 + j / MAXCH, col = tid + (j % MAXCH) * NT;
-                v[j] = ld_wt(rows, (i < nrel && col < ncol) ? __builtin_amdgcn_readlane(row, i) * stride + 1 + col
-                                                             : kOffRange);
+                const int i = b0 + j / MAXCH, ch = j % MAXCH;
+                if (i < nrel) {
+                    const double s = readlane_f64(sk, i);
+                    acc[ch] = fma(s, v[j], acc[ch]);
+                    if (ch == 0) eta = fma(s, readlane_f64(eta_k, i), eta);
+                }
             }
         }
+    } else {
+        // G groups of ncol threads (one column chunk), group g taking weighted rows
+        // g, g + G, ...: the row of a load varies by lane and comes through
+        // ds_bpermute, read for every lane before any per-lane test (a cross-lane
+        // read returns nothing from a lane the EXEC mask has off)
+        const int grp = tid / ncol, gcol = tid - grp * ncol;
+        const bool active = grp < G;
+        for (int b0 = 0; b0 < nrel; b0 += RB * G) {
+            double v[LB], sf[LB];
+            int roff[LB];
+            bool on[LB];
 #pragma unroll
-        for (int j = 0; j < LB; ++j) {
-            const int i = b0 + j / MAXCH, ch = j % MAXCH;
-            if (i < nrel) {
-                const double s = readlane_f64(sk, i);
-                acc[ch] = fma(s, v[j], acc[ch]);
-                if (ch == 0) eta = fma(s, readlane_f64(eta_k, i), eta);
+            for (int j = 0; j < LB; ++j) {
+                const int i = b0 + grp + G * j;
+                on[j] = active && i < nrel;
+                const int r = __builtin_amdgcn_ds_bpermute(min(i, 63) << 2, row);
+                sf[j] = __shfl(sk, min(i, 63));
+                roff[j] = on[j] ? r * stride + 1 + gcol : kOffRange;
             }
+            if constexpr (GRAN) {
+                u32x4 gv[LB];
+                for (unsigned spins = 0;; ++spins) {
+                    asm volatile("" ::: "memory");
+                    bool ok = true;
+#pragma unroll
+                    for (int j = 0; j < LB; ++j) {
+                        gv[j] = ld_gran(rows, roff[j]);
+                        ok = ok && (!on[j] || gran_ok(gv[j], tag));
+                    }
+                    if (__all(ok)) break;
+                    MPPI_SPIN_OR_GIVE_UP(spins, tmo, lane);
+                }
+#pragma unroll
+                for (int j = 0; j < LB; ++j) v[j] = gran_val(gv[j]);
+            } else {
+#pragma unroll
+                for (int j = 0; j < LB; ++j) v[j] = ld_wt(rows, roff[j]);
+            }
+#pragma unroll
+            for (int j = 0; j < LB; ++j)
+                if (on[j]) acc[0] = fma(sf[j], v[j], acc[0]);
         }
+        // fold the groups' column sums in group order; eta is column 0
+        if (active) sm.part[tid] = acc[0];
+        __syncthreads();
+        if (grp == 0) {
+            double a = sm.part[gcol];
+            for (int g = 1; g < G; ++g) a += sm.part[g * ncol + gcol];
+            acc[0] = a;
+            if (tid == 0) sm.red[0] = a;
+        }
+        __syncthreads();
+        eta = sm.red[0];
     }
     STAMP(14, NOW());
     put_final<NT, MAXCH>(rho, acc, eta, nrel, geo, sm, out_row, w_eps_out);

@@ -1079,8 +1079,9 @@ void host_F(const mppi_arm_params& a, double dt, double* x, double u1, double u2
     const double M22 = a.m2 * a.lc2 * a.lc2 + a.l2;
     const double M12 = a.m2 * a.l1 * a.lc2 * c2 + a.m2 * a.lc2 * a.lc2 + a.l2;
     const double h = a.m2 * a.l1 * a.lc2 * sin(q2);
-    const double g1 = a.m1 * a.lc1 * a.g * cos(q1) + a.m2 * a.g * (a.lc2 * cos(q1 + q2) + a.l1 * cos(q1));
-    const double g2 = a.m2 * a.lc2 * a.g * cos(q1 + q2);
+    const double c1 = cos(q1), c12 = cos(q1 + q2);   // each evaluated once (the reference evaluates them twice)
+    const double g1 = a.m1 * a.lc1 * a.g * c1 + a.m2 * a.g * (a.lc2 * c12 + a.l1 * c1);
+    const double g2 = a.m2 * a.lc2 * a.g * c12;
     const double r1 = u1 - ((-h * dq2) * dq1 + (-h * dq1 - h * dq2) * dq2) - g1;
     const double r2 = u2 - ((h * dq1) * dq1 + 0.0 * dq2) - g2;
     const double det = M11 * M22 - M12 * M12;

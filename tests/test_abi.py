@@ -86,10 +86,25 @@ int main(void) {
                     N.CHAIN_MAX_DOF]
 
 
+def test_dropin_binding_layout_matches_header(tmp_path):
+    from mppi_robotarm_amd import _native as N
+    probe = tmp_path / "probe_bind.c"
+    fields = [f for f, _ in N.DropinBindingC._fields_]
+    probe.write_text("#include <stddef.h>\n#include <stdio.h>\n#include \"mppi_rocm.h\"\nint main(void) {\n"
+                     + "".join(f'  printf("%zu ", offsetof(mppi_dropin_binding, {f}));\n' for f in fields)
+                     + '  printf("%zu\\n", sizeof(mppi_dropin_binding));\n  return 0;\n}\n')
+    exe = tmp_path / "probe_bind"
+    subprocess.run(["gcc", "-I", os.path.dirname(HEADER), str(probe), "-o", str(exe)], check=True)
+    vals = [int(v) for v in subprocess.run([str(exe)], capture_output=True, text=True, check=True).stdout.split()]
+    B = N.DropinBindingC
+    assert vals == [getattr(B, f).offset for f in fields] + [C.sizeof(B)]
+
+
 def test_constants_match_header():
     from mppi_robotarm_amd import _native as N
     text = open(HEADER).read()
-    for name in ("MPPI_MAX_T", "MPPI_SEARCH_LEN", "MPPI_OK", "MPPI_E_ARG", "MPPI_E_HIP", "MPPI_E_SINGULAR"):
+    for name in ("MPPI_MAX_T", "MPPI_SEARCH_LEN", "MPPI_OK", "MPPI_E_ARG", "MPPI_E_HIP", "MPPI_E_SINGULAR",
+                 "MPPI_E_PATH_END"):
         m = re.search(rf"#define {name}\s+(-?\d+)", text)
         assert m and int(m.group(1)) == getattr(N, name), name
     assert re.search(r"#define MPPI_FLAG_FUSED_UPDATE\s+1u", text) and N.MPPI_FLAG_FUSED_UPDATE == 1
