@@ -14,6 +14,8 @@ WL=${2:-c3}
 B="python3 bench.py --workload $WL --steps 1000 --warmup 100 --cpu-seconds 0"
 BP="python3 bench.py --workload $WL --steps 40 --warmup 4 --settle-ms 0 --cpu-seconds 0"
 if [ "$WL" = c5 ]; then KR=chain_rollout; CA=4; else KR=rollout; CA=8; fi
+# the calibration kernel is a git-ignored build product: compile it on the box
+[ -x tools/calib_fetch ] || hipcc --offload-arch=gfx950 -O3 tools/calib_fetch.hip -o tools/calib_fetch 2>/dev/null || exit 3
 step() { local n=$1; shift; timeout -k 10 400 "$@" > $O/$n.log 2>&1; local rc=$?; echo "$n rc=$rc"; [ $rc -le 1 ] || exit $rc; }
 step stats rocprofv3 --kernel-trace --stats --output-format csv -d $O/stats -o run -- $B
 step fetch rocprofv3 --pmc FETCH_SIZE --kernel-include-regex $KR --output-format csv -d $O/fetch -o p -- $BP
