@@ -344,7 +344,7 @@ __global__ __launch_bounds__(kCT) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
     const float* __restrict__ noise, double* __restrict__ S_out, double* __restrict__ slab, double* __restrict__ gslab,
     unsigned* __restrict__ counters, double* __restrict__ partial_out, double* __restrict__ w_eps_out,
     ChainStep* __restrict__ nxt, unsigned flags, const XDesc xd, unsigned* __restrict__ epoch, unsigned* __restrict__ tmo,
-    unsigned long long* __restrict__ dbg) {
+    unsigned long long* __restrict__ runmin, unsigned long long* __restrict__ dbg) {
     static_assert(N <= kCMax && N >= 2, "links");
     __shared__ float4 s_win[kSlots];
     __shared__ KeyPair s_keys[kKeyPairs];
@@ -353,6 +353,7 @@ __global__ __launch_bounds__(kCT) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
     __shared__ int s_k[kCT];
     __shared__ float s_e[kCT];
     __shared__ unsigned s_flag, s_parity;
+    __shared__ double s_run;
     __shared__ CScratch sm;
 
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -473,7 +474,19 @@ __global__ __launch_bounds__(kCT) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
         s_cnt[wave] = __popcll(bal);
         s_redf[wave] = esum;
     }
+    // The running minimum of the workgroups' rho_b so far (one 64-bit atomic min
+    // on an order-preserving key; reset by the final merger).  The final rho is at
+    // most this value, so a workgroup whose rho_b is 2^-64 or more below it in
+    // weight can carry no weight in any merge: it publishes rho_b = +inf and skips
+    // the gather of its weighted samples' noise — each of those is T n scattered
+    // 4-B reads, one cache line apiece (1.14x the algorithmic bytes at config 5).
+    if (tid == 0) {
+        const unsigned long long key = ord_key(rho_b);
+        const unsigned long long old = __hip_atomic_fetch_min(runmin, key, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        s_run = ord_val(old < key ? old : key);
+    }
     __syncthreads();
+    const bool skip = exp((s_run - rho_b) * c.inv_lambda) < kMergeFloor;   // uniform
     int off = 0, nl = 0;
     double eta_b = 0.0;
 #pragma unroll
@@ -503,11 +516,13 @@ __global__ __launch_bounds__(kCT) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
     };
     // rho_b and eta_b leave first (see rollout_kernel in mppi_rocm.hip)
     if (tid == 0) {
-        publish(blockIdx.x * stride, rho_b);
+        publish(blockIdx.x * stride, skip ? INFINITY : rho_b);
         publish(blockIdx.x * stride + 1, eta_b);
     }
     nl = __builtin_amdgcn_readfirstlane(nl);
-    if (nl <= kSparseMax) {
+    if (skip) {
+        // no merge reads this row past rho
+    } else if (nl <= kSparseMax) {
         // column (t, d) = t N + d of the noise is the row noise[col K : col K + K]
         for (int col = tid; col < nval; col += kCT) {
             const float* base = noise + (size_t)col * K;
@@ -564,7 +579,10 @@ __global__ __launch_bounds__(kCT) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
             merge_rows_block<kCT, kCMaxCh, true, true>(gslab_r, 0, ngroups, geo, c.inv_lambda, sm, nullptr, 0,
                                                        partial_out, w_eps_out, tag, tmo);
         }
-        if (threadIdx.x == 0) __hip_atomic_store(epoch, tag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (threadIdx.x == 0) {
+            __hip_atomic_store(epoch, tag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            __hip_atomic_store(runmin, ~0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);   // every row is in
+        }
     } else {
         if (!arrive_last(counters + g, (unsigned)gsz, &s_flag, c.acquire != 0)) return;
         STAMP(3, NOW());
@@ -578,6 +596,7 @@ __global__ __launch_bounds__(kCT) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
                                                 nullptr)))
             merge_rows_block<kCT, kCMaxCh, true, false>(gslab_r, 0, ngroups, geo, c.inv_lambda, sm, nullptr, 0,
                                                         partial_out, w_eps_out, 0u, nullptr);
+        if (threadIdx.x == 0) __hip_atomic_store(runmin, ~0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
     STAMP(11, NOW());
     STAMP(6, (unsigned long long)sm.nrel);
@@ -684,6 +703,7 @@ struct mppi_chain_ctx {
     double* d_gslab = nullptr;
     unsigned* d_counter = nullptr;
     unsigned* d_epoch = nullptr;
+    unsigned long long* d_runmin = nullptr;   // running minimum of the workgroups' rho_b (ord_key), ~0 between launches
     double* d_weps = nullptr;
     double* h_buf = nullptr;
     float* d_base = nullptr;
@@ -710,7 +730,7 @@ template <int N, bool P>
 void launch_rollout(mppi_chain_ctx* c, const ChainStep* cur, const float* noise, double* S, double* part, ChainStep* nxt,
                     unsigned flags) {
     hipLaunchKernelGGL((chain_rollout_kernel<N, P>), dim3(c->nblocks), dim3(kCT), 0, c->stream, c->kc, cur, c->d_dyn, noise, S,
-                       c->d_slab, c->d_gslab, c->d_counter, part, c->d_weps, nxt, flags, c->xd, c->d_epoch, c->d_tmo,
+                       c->d_slab, c->d_gslab, c->d_counter, part, c->d_weps, nxt, flags, c->xd, c->d_epoch, c->d_tmo, c->d_runmin,
                        c->d_dbg);
 }
 
@@ -729,6 +749,8 @@ void launch_rollout(mppi_chain_ctx* c, const ChainStep* cur, const float* noise,
 int check_tmo(mppi_chain_ctx* c) {
     if (c->h_tmo && __atomic_load_n(c->h_tmo, __ATOMIC_ACQUIRE)) {
         *c->h_tmo = 0;
+        // an aborted merge left the running minimum set: clear it for the next launch
+        (void)hipMemsetAsync(c->d_runmin, 0xFF, sizeof(unsigned long long), c->stream);
         return fail(MPPI_E_HIP, "in-launch hand-off timed out (workgroups not co-resident?); results invalid");
     }
     return MPPI_OK;
@@ -857,6 +879,7 @@ int mppi_chain_ctx_create(const mppi_chain_config* cfg, int device, void* stream
     if ((e = hipMalloc(&c->d_step, 2 * sizeof(ChainStep))) != hipSuccess ||
         (e = hipMalloc(&c->d_slab, slab)) != hipSuccess || (e = hipMalloc(&c->d_gslab, gslab)) != hipSuccess ||
         (e = hipMalloc(&c->d_counter, ctr_bytes)) != hipSuccess ||
+        (e = hipMalloc(&c->d_runmin, 256)) != hipSuccess || (e = hipMemset(c->d_runmin, 0xFF, 256)) != hipSuccess ||
         (e = hipMalloc(&c->d_weps, kCMaxVals * sizeof(double))) != hipSuccess ||
         (e = hipMalloc(&c->d_base, kCMaxVals * sizeof(float))) != hipSuccess ||
         (e = hipMalloc(&c->d_chol, sizeof(chol))) != hipSuccess ||
@@ -890,6 +913,7 @@ void mppi_chain_ctx_destroy(mppi_chain_ctx* c) {
     (void)hipFree(c->d_slab);
     (void)hipFree(c->d_gslab);
     (void)hipFree(c->d_counter);
+    (void)hipFree(c->d_runmin);
     (void)hipFree(c->d_weps);
     (void)hipFree(c->d_base);
     (void)hipFree(c->d_chol);

@@ -386,6 +386,16 @@ __device__ __forceinline__ void report_timeout(unsigned* tmo) {
     }                                                 \
     __builtin_amdgcn_s_sleep(1)
 
+// Order-preserving 64-bit key of a double (unsigned order == numeric order; NaN
+// above +inf) for integer atomic min / max, and its inverse.
+__device__ __forceinline__ unsigned long long ord_key(double x) {
+    const unsigned long long b = (unsigned long long)__double_as_longlong(x);
+    return (b >> 63) ? ~b : (b | (1ull << 63));
+}
+__device__ __forceinline__ double ord_val(unsigned long long k) {
+    return __longlong_as_double((long long)((k >> 63) ? (k & ~(1ull << 63)) : ~k));
+}
+
 // ------------------------------------------------------------ merge scratch
 
 template <int MAXV>

@@ -82,10 +82,16 @@ def test_chain_at_n2_reproduces_reference_steps(name, paths):
     c.close()
 
 
-@pytest.mark.parametrize("K,T,lam,s99", [(4096, 32, 100.0, 5e-4), (4096, 32, 1.0e9, 1e-5),
-                                        (131072, 128, 100.0, 1e-3), (3000, 7, 100.0, 2e-5)])
+@pytest.mark.parametrize("K,T,lam,s99", [(4096, 32, 100.0, 2e-4), (4096, 32, 1.0e9, 1e-7),
+                                        (131072, 128, 100.0, 2e-4), (3000, 7, 100.0, 1e-5)])
 def test_chain_n7_against_c_oracle(K, T, lam, s99, paths):
-    """Config 5 (K=131072 T=128) and smaller shapes: S and the weighted noise vs fp64."""
+    """Config 5 (K=131072 T=128) and smaller shapes: S and the weighted noise vs fp64.
+
+    Achieved on MI355X (r08): at config 5, S rel-err p50 1.9e-6, p99 1.0e-4, max
+    1.8e-3 (2.8e-4 of the samples above 1e-3), same argmin, w_eps exact; K=4096
+    T=32: p99 7.8e-5, max 8.9e-4.  The fp32 trajectories of the undamped-looking
+    7-link chain drift from fp64 over 128 steps (the 2-link arm stays below 5e-5);
+    the bounds are ~2x the achieved figures."""
     P, x0, sig, ug = _c5()
     eng = _engine(K, T, lam)
     win = paths["xydq_circle"][:30]
@@ -100,10 +106,13 @@ def test_chain_n7_against_c_oracle(K, T, lam, s99, paths):
     Sr = coracle.chain_rollout_costs(x0, u, nz, win, 0.006, lam, 0.98, sig, W, TW, CO.ChainParams(), layout="TNK")
     _, wr = coracle.chain_weighted_noise(Sr, nz, lam, layout="TNK")
     rel = np.abs(S - Sr) / np.abs(Sr)
+    print(f"chain n=7 K={K} T={T} lam={lam:g}: S rel-err p50 {np.median(rel):.2e} p99 {np.percentile(rel, 99):.2e} "
+          f"max {rel.max():.2e}, frac > 1e-3 {np.mean(rel > 1e-3):.2e}, w_eps rel-err {_urel(w, wr):.2e}")
     assert np.all(np.isfinite(S))
     assert int(np.argmin(S)) == int(np.argmin(Sr))
     assert float(np.percentile(rel, 99)) < s99
-    assert float(np.mean(rel > 1e-3)) < 0.01
+    assert float(np.mean(rel > 1e-3)) < 1e-3
+    assert float(rel.max()) < 5e-3
     assert _urel(w, wr) < U_TOL
     eng.close()
 
