@@ -460,7 +460,20 @@ __global__ __launch_bounds__(NT) void rollout_kernel(
     if (S_out && owner) S_out[k] = S;
 
     // ---- workgroup partial: rho_b, eta_b, N_b (control.py:112-118 over this block)
+    const int stride = 2 + 2 * T;
+    const RowGeo geo(2 * T);   // 2T + 1 merged columns <= NT: one column chunk (host keeps T <= 127 at NT = 256)
+    const int nrows = c.nblocks;
+    const int ngroups = (nrows + kGroup - 1) / kGroup;
+    constexpr int kValBytes = POLL ? 16 : 8;
+    const __amdgpu_buffer_rsrc_t slab_r = rows_rsrc(slab, nrows * stride * kValBytes);
+    const __amdgpu_buffer_rsrc_t gslab_r = rows_rsrc(gslab, ngroups * stride * kValBytes);
+    const unsigned tag = __builtin_amdgcn_readfirstlane(tag_v);
+    auto publish = [&](int idx, double v) {
+        if constexpr (POLL) st_gran(slab_r, idx, v, tag);
+        else st_wt(slab_r, idx, v);
+    };
     const double rho_b = block_min_f64<NT>(owner ? S : INFINITY, sm);
+    if (tid == 0) publish(blockIdx.x * stride, rho_b);   // the merger's first need, out at once
     // weights below 2^-64 of the block's best are dropped (see kMergeFloor)
     const float wgt = owner ? __expf((float)((rho_b - S) * c.inv_lambda)) : 0.f;
     const bool nz = wgt >= 5.421010862e-20f;
@@ -485,24 +498,10 @@ __global__ __launch_bounds__(NT) void rollout_kernel(
         s_e[pos] = wgt;
     }
     __syncthreads();
-    const int stride = 2 + 2 * T;
-    const RowGeo geo(2 * T);   // 2T + 1 merged columns <= NT: one column chunk (host keeps T <= 127 at NT = 256)
-    const int nrows = c.nblocks;
-    const int ngroups = (nrows + kGroup - 1) / kGroup;
-    constexpr int kValBytes = POLL ? 16 : 8;
-    const __amdgpu_buffer_rsrc_t slab_r = rows_rsrc(slab, nrows * stride * kValBytes);
-    const __amdgpu_buffer_rsrc_t gslab_r = rows_rsrc(gslab, ngroups * stride * kValBytes);
-    const unsigned tag = __builtin_amdgcn_readfirstlane(tag_v);
-    auto publish = [&](int idx, double v) {
-        if constexpr (POLL) st_gran(slab_r, idx, v, tag);
-        else st_wt(slab_r, idx, v);
-    };
-    // rho_b and eta_b leave first: a poll merger learns the global minimum and
-    // which rows carry weight before the slowest workgroup's gather is done
-    if (tid == 0) {
-        publish(blockIdx.x * stride, rho_b);
-        publish(blockIdx.x * stride + 1, eta_b);
-    }
+    // eta_b leaves next (rho_b left right after the block minimum): a poll merger
+    // learns the global minimum and which rows carry weight before the slowest
+    // workgroup's gather is done
+    if (tid == 0) publish(blockIdx.x * stride + 1, eta_b);
     STAMP(15, NOW());
     nl = __builtin_amdgcn_readfirstlane(nl);
     if (nl <= kSparseMax) {
