@@ -17,6 +17,10 @@ xydq_circle.txt, noise N(0, Sigma) from the device Philox generator, 10
 distinct buffers rotated so their total (335 MB at K=65536 T=64) exceeds the
 256 MiB Infinity Cache.  Everything is resident in HBM before timing starts.
 
+``--workload c2``: BASELINE config 2's size on the same 2-DoF path (K=4096
+T=32, 10 noise buffers of 1 MiB: they stay in the Infinity Cache, as a
+controller's one redrawn buffer would).  ``c3`` remains the headline line.
+
 ``--workload c5``: BASELINE config 5 instead — the 7-DoF chain
 (mppi_robotarm_amd/chain.py, build-defined model) at K=131072 T=128, strong
 scaling (K fixed, split over the ranks), 28 B of noise per state-step, the
@@ -83,15 +87,16 @@ def parse():
     p.add_argument("--settle-ms", type=float, default=200.0,
                    help="untimed steps for this long before the W warmup steps: the GPU clock takes ~0.1 s of "
                         "load to ramp (measured: 33.4 us/step after 20 warmup steps, 30.9 after 2000)")
-    p.add_argument("--workload", choices=("c3", "c5"), default="c3",
-                   help="c3: 2-DoF arm, K per GPU (BASELINE metric); c5: 7-DoF chain, K total (config 5)")
-    p.add_argument("--K", type=int, default=None, help="c3: samples per GPU (65536); c5: samples in total (131072)")
-    p.add_argument("--T", type=int, default=None, help="horizon (c3: 64, c5: 128)")
+    p.add_argument("--workload", choices=("c3", "c2", "c5"), default="c3",
+                   help="c3: 2-DoF arm, K per GPU (BASELINE metric); c2: same path at config 2's K=4096 T=32; "
+                        "c5: 7-DoF chain, K total (config 5)")
+    p.add_argument("--K", type=int, default=None, help="c3: samples per GPU (65536); c2: 4096; c5: samples in total (131072)")
+    p.add_argument("--T", type=int, default=None, help="horizon (c3: 64, c2: 32, c5: 128)")
     p.add_argument("--nbuf", type=int, default=None, help="rotated noise buffers (c3: 10, c5: 4)")
     p.add_argument("--lps", type=int, default=0, help="lanes per sample (0 = auto)")
     p.add_argument("--cpu-seconds", type=float, default=10.0, help="CPU baseline budget (0 = skip)")
     p.add_argument("--traffic-json", default=None,
-                   help="measured HBM bytes per launch (default profiles/traffic.json, c5: profiles/traffic_c5.json)")
+                   help="measured HBM bytes per launch (default profiles/traffic.json, c2/c5: profiles/traffic_<workload>.json)")
     p.add_argument("--launch", choices=("eager", "graph"), default="eager",
                    help="N = 1: back-to-back launches from the host loop (default) or replay of a captured HIP graph")
     p.add_argument("--backend", default=None,
@@ -254,13 +259,14 @@ def main():
         sys.exit(launch_ranks(args))
     c5 = args.workload == "c5"
     if args.K is None:
-        args.K = 131072 if c5 else 65536
+        args.K = {"c5": 131072, "c2": 4096}.get(args.workload, 65536)
     if args.T is None:
-        args.T = 128 if c5 else 64
+        args.T = {"c5": 128, "c2": 32}.get(args.workload, 64)
     if args.nbuf is None:
         args.nbuf = 4 if c5 else 10
     if args.traffic_json is None:
-        args.traffic_json = os.path.join(ROOT, "profiles", "traffic_c5.json" if c5 else "traffic.json")
+        name = "traffic.json" if args.workload == "c3" else f"traffic_{args.workload}.json"
+        args.traffic_json = os.path.join(ROOT, "profiles", name)
     rank = int(os.environ.get("RANK", "0"))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))

@@ -86,7 +86,7 @@ def main():
         # whole-device VALU wave-instructions per launch (bench.py's "valu" roofline)
         out["valu_insts_per_launch"] = sq["SQ_INSTS_VALU"]
         out["waves_per_launch"] = sq.get("SQ_WAVES")
-    name = "traffic_c5.json" if workload == "c5" else "traffic.json"
+    name = "traffic.json" if workload == "c3" else f"traffic_{workload}.json"
     json.dump(out, open(os.path.join(os.path.dirname(dst.rstrip('/')), name), "w"), indent=1)
     if sq:
         gr = {}
