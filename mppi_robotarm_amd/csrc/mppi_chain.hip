@@ -348,10 +348,10 @@ __global__ __launch_bounds__(kCT) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
     static_assert(N <= kCMax && N >= 2, "links");
     __shared__ float4 s_win[kSlots];
     __shared__ KeyPair s_keys[kKeyPairs];
-    __shared__ float s_redf[kCT / 64];
+    __shared__ double s_redd[kCT / 64];
     __shared__ int s_cnt[kCT / 64];
     __shared__ int s_k[kCT];
-    __shared__ float s_e[kCT];
+    __shared__ double s_e[kCT];
     __shared__ unsigned s_flag, s_parity;
     __shared__ double s_run;
     __shared__ CScratch sm;
@@ -466,13 +466,17 @@ __global__ __launch_bounds__(kCT) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
 
     // ---- workgroup partial: rho_b, eta_b, N_b (control.py:112-118 over this block)
     const double rho_b = block_min_f64<kCT>(valid ? S : INFINITY, sm);
-    const float wgt = valid ? __expf((float)((rho_b - S) * c.inv_lambda)) : 0.f;
-    const bool nz = wgt >= 5.421010862e-20f;
+    // fp64, like the reference's weights; a wave whose samples all lie below the
+    // floor (exp(-44.4) = 2^-64: the usual case, S spread >> lambda) skips the exp
+    const double warg = (rho_b - S) * c.inv_lambda;
+    double wgt = 0.0;
+    if (__any(valid && warg >= -45.0)) wgt = valid ? exp(warg) : 0.0;
+    const bool nz = wgt >= kMergeFloor;
     const unsigned long long bal = __ballot(nz);
-    const float esum = wave_sum_f32(nz ? wgt : 0.f);
+    const double esum = wave_sum_f64(nz ? wgt : 0.0);
     if (lane == 0) {
         s_cnt[wave] = __popcll(bal);
-        s_redf[wave] = esum;
+        s_redd[wave] = esum;
     }
     // The running minimum of the workgroups' rho_b so far (one 64-bit atomic min
     // on an order-preserving key; reset by the final merger).  The final rho is at
@@ -493,7 +497,7 @@ __global__ __launch_bounds__(kCT) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
     for (int w = 0; w < kCT / 64; ++w) {
         off += (w < wave) ? s_cnt[w] : 0;
         nl += s_cnt[w];
-        eta_b += (double)s_redf[w];
+        eta_b += s_redd[w];
     }
     if (nz) {
         const int pos = off + lanes_below(bal);
@@ -532,13 +536,13 @@ __global__ __launch_bounds__(kCT) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
         constexpr int PER = kCT / 64;
         constexpr int kRowBatch = 4;
         const int k0 = blockIdx.x * kCT;
-        s_e[tid] = 0.f;
+        s_e[tid] = 0.0;
         __syncthreads();
         if (nz) s_e[k - k0] = wgt;
         __syncthreads();
         double w[PER];
 #pragma unroll
-        for (int i = 0; i < PER; ++i) w[i] = (k0 + lane + 64 * i < K) ? (double)s_e[lane + 64 * i] : 0.0;
+        for (int i = 0; i < PER; ++i) w[i] = (k0 + lane + 64 * i < K) ? s_e[lane + 64 * i] : 0.0;
         for (int cb = wave * kRowBatch; cb < nval; cb += (kCT / 64) * kRowBatch) {
             float e[kRowBatch][PER];
 #pragma unroll

@@ -244,6 +244,7 @@ struct Search {
         }
         if (LPS >= 2) best = min_raw(best, dpp_f32<0xB1>(best));  // quad_perm xor 1
         if (LPS >= 4) best = min_raw(best, dpp_f32<0x4E>(best));  // quad_perm xor 2
+        if (LPS >= 8) best = min_raw(best, dpp_f32<0x141>(best));  // row_half_mirror: the other quad of 8
         return __float_as_uint(best) & 31u;
     }
 };
@@ -300,7 +301,7 @@ struct SearchLDS {
 // issued together.  NL is a compile-time bucket >= nl, so a workgroup with one
 // weighted sample issues one load per column, not kSparseMax.
 template <int NL>
-__device__ __forceinline__ double gather_col_n(const float* base, int kstride, const int* s_k, const float* s_e,
+__device__ __forceinline__ double gather_col_n(const float* base, int kstride, const int* s_k, const double* s_e,
                                                int nl) {
     float e[NL];
 #pragma unroll
@@ -308,11 +309,11 @@ __device__ __forceinline__ double gather_col_n(const float* base, int kstride, c
     double acc = 0.0;
 #pragma unroll
     for (int l = 0; l < NL; ++l)
-        if (l < nl) acc = fma((double)s_e[l], (double)e[l], acc);
+        if (l < nl) acc = fma(s_e[l], (double)e[l], acc);
     return acc;
 }
 // nl: wave-uniform, <= kSparseMax
-__device__ __forceinline__ double gather_col(const float* base, int kstride, const int* s_k, const float* s_e,
+__device__ __forceinline__ double gather_col(const float* base, int kstride, const int* s_k, const double* s_e,
                                              int nl) {
     static_assert(kSparseMax == 16, "buckets");
     if (nl <= 1) return gather_col_n<1>(base, kstride, s_k, s_e, nl);

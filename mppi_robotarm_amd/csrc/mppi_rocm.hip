@@ -7,7 +7,7 @@
 // -> terminal cost (control.py:109) -> soft-min weights (control.py:297-314)
 // -> weighted noise sum (control.py:115-118)), written for CDNA4 directly:
 //
-//  * rollout_kernel<LPS>: LPS lanes of a 64-wide wave per sample (1, 2 or 4).
+//  * rollout_kernel<LPS>: LPS lanes of a 64-wide wave per sample (1, 2, 4 or 8).
 //    The serial T loop runs per lane in fp32 registers; the 30-waypoint
 //    argmin is split over the LPS lanes of a sample and closed with DPP
 //    quad_perm min (no LDS, no MFMA: the work is element-wise VALU).  The
@@ -293,10 +293,10 @@ __global__ __launch_bounds__(NT) void rollout_kernel(
     float* __restrict__ upd, const HostOut ho, unsigned long long* __restrict__ dbg) {
     __shared__ float4 s_win[kSlots];
     __shared__ float4 s_ua[kMaxT + kPF];   // per-step constants (u_t, a_t); rows >= T repeat row T - 1
-    __shared__ float s_redf[NT / 64];
+    __shared__ double s_redd[NT / 64];
     __shared__ int s_cnt[NT / 64];
     __shared__ int s_k[NT];
-    __shared__ float s_e[NT];
+    __shared__ double s_e[NT];
     __shared__ unsigned s_flag;
     __shared__ Scratch sm;
 
@@ -475,13 +475,17 @@ __global__ __launch_bounds__(NT) void rollout_kernel(
     const double rho_b = block_min_f64<NT>(owner ? S : INFINITY, sm);
     if (tid == 0) publish(blockIdx.x * stride, rho_b);   // the merger's first need, out at once
     // weights below 2^-64 of the block's best are dropped (see kMergeFloor)
-    const float wgt = owner ? __expf((float)((rho_b - S) * c.inv_lambda)) : 0.f;
-    const bool nz = wgt >= 5.421010862e-20f;
+    // fp64, like the reference's weights; a wave whose samples all lie below the
+    // floor (exp(-44.4) = 2^-64: the usual case, S spread >> lambda) skips the exp
+    const double warg = (rho_b - S) * c.inv_lambda;
+    double wgt = 0.0;
+    if (__any(owner && warg >= -45.0)) wgt = owner ? exp(warg) : 0.0;
+    const bool nz = wgt >= kMergeFloor;
     const unsigned long long bal = __ballot(nz);
-    const float esum = wave_sum_f32(nz ? wgt : 0.f);
+    const double esum = wave_sum_f64(nz ? wgt : 0.0);
     if (lane == 0) {
         s_cnt[wave] = __popcll(bal);
-        s_redf[wave] = esum;
+        s_redd[wave] = esum;
     }
     __syncthreads();
     int off = 0, nl = 0;
@@ -490,7 +494,7 @@ __global__ __launch_bounds__(NT) void rollout_kernel(
     for (int w = 0; w < NT / 64; ++w) {
         off += (w < wave) ? s_cnt[w] : 0;
         nl += s_cnt[w];
-        eta_b += (double)s_redf[w];
+        eta_b += s_redd[w];
     }
     if (nz) {
         const int pos = off + lanes_below(bal);
@@ -521,7 +525,7 @@ __global__ __launch_bounds__(NT) void rollout_kernel(
         constexpr int PER = (NS + 63) / 64;
         constexpr int kRowBatch = 4;
         const int k0 = blockIdx.x * NS;
-        if (tid < NS) s_e[tid] = 0.f;
+        if (tid < NS) s_e[tid] = 0.0;
         __syncthreads();
         if (nz) s_e[k - k0] = wgt;
         __syncthreads();
@@ -529,7 +533,7 @@ __global__ __launch_bounds__(NT) void rollout_kernel(
 #pragma unroll
         for (int i = 0; i < PER; ++i) {
             const int ks = lane + 64 * i;
-            w[i] = (ks < NS && k0 + ks < K) ? (double)s_e[ks] : 0.0;
+            w[i] = (ks < NS && k0 + ks < K) ? s_e[ks] : 0.0;
         }
         for (int tb = wave * kRowBatch; tb < T; tb += (NT / 64) * kRowBatch) {
             float2 e[kRowBatch][PER];
@@ -792,12 +796,17 @@ int auto_lps(int K_local) {
     // issues a VALU op every ~6-8 cycles, 2 waves/SIMD ~4.4, 4 waves ~3.0.
     // Splitting the window search over LPS lanes multiplies the instructions
     // per sample by ~1.6 (LPS=2) / ~2.7 (LPS=4); at K = 65536 (one wave per
-    // SIMD) one lane per sample won (37 vs 45 us span), so split only when the
-    // grid would leave SIMDs empty.
+    // SIMD) one lane per sample won (37 vs 45 us span), so split only while
+    // the grid would leave SIMDs empty, up to one wave per SIMD
+    // (tools/gpu_lps_sweep.sh, us per fused step, LPS 2 / 4 / 8:
+    // K=2048 T=32 16.0 / 15.3 / 14.6; K=4096 T=32 17.3 / 15.7 / 15.5;
+    // K=8192 T=64 23.4 / 20.1 / 20.4; K=16384 T=64 23.3 / 20.2 / 26.9;
+    // K=32768 T=64 23.9 / 29.5 / 53.0).
     const long long waves1 = ((long long)K_local + 63) / 64;
     if (waves1 >= 1024) return 1;
-    if (waves1 >= 256) return 2;
-    return 4;
+    if (waves1 >= 512) return 2;
+    if (waves1 >= 128) return 4;
+    return 8;
 }
 }  // namespace
 
@@ -824,9 +833,9 @@ int mppi_ctx_create(const mppi_config* cfg, int device, void* stream, mppi_ctx**
     c->sig_inv[2] = -S[2] / det;
     c->sig_inv[3] = S[0] / det;
     int lps = cfg->lanes_per_sample > 0 ? cfg->lanes_per_sample : auto_lps(cfg->K_local);
-    if (lps != 1 && lps != 2 && lps != 4) {
+    if (lps != 1 && lps != 2 && lps != 4 && lps != 8) {
         delete c;
-        return fail(MPPI_E_ARG, "lanes_per_sample must be 0, 1, 2 or 4");
+        return fail(MPPI_E_ARG, "lanes_per_sample must be 0, 1, 2, 4 or 8");
     }
     c->lps = lps;
     // 512-thread workgroups when the grid fills every CU with one of them (8 waves:
@@ -887,8 +896,12 @@ int mppi_ctx_create(const mppi_config* cfg, int device, void* stream, mppi_ctx**
         return cleanup_fail(fail(MPPI_E_HIP, std::string("device attributes: ") + hipGetErrorString(e)));
     {
         int rc = 0;
-        if (c->nt == 512) rc = lps == 1 ? occupancy<1, 512>(&per_cu) : lps == 2 ? occupancy<2, 512>(&per_cu) : occupancy<4, 512>(&per_cu);
-        else rc = lps == 1 ? occupancy<1, 256>(&per_cu) : lps == 2 ? occupancy<2, 256>(&per_cu) : occupancy<4, 256>(&per_cu);
+        if (c->nt == 512)
+            rc = lps == 1 ? occupancy<1, 512>(&per_cu) : lps == 2 ? occupancy<2, 512>(&per_cu)
+               : lps == 4 ? occupancy<4, 512>(&per_cu) : occupancy<8, 512>(&per_cu);
+        else
+            rc = lps == 1 ? occupancy<1, 256>(&per_cu) : lps == 2 ? occupancy<2, 256>(&per_cu)
+               : lps == 4 ? occupancy<4, 256>(&per_cu) : occupancy<8, 256>(&per_cu);
         if (rc != 0) per_cu = 0;
     }
     c->poll = per_cu >= 1 && c->nblocks <= ncu;
@@ -1135,11 +1148,13 @@ int launch_rollout(mppi_ctx* c, const float* noise_dev, double* S_dev, double* p
     if (c->nt == 512) {
         if (c->lps == 1) MPPI_LAUNCH_P(1, 512);
         else if (c->lps == 2) MPPI_LAUNCH_P(2, 512);
-        else MPPI_LAUNCH_P(4, 512);
+        else if (c->lps == 4) MPPI_LAUNCH_P(4, 512);
+        else MPPI_LAUNCH_P(8, 512);
     } else {
         if (c->lps == 1) MPPI_LAUNCH_P(1, 256);
         else if (c->lps == 2) MPPI_LAUNCH_P(2, 256);
-        else MPPI_LAUNCH_P(4, 256);
+        else if (c->lps == 4) MPPI_LAUNCH_P(4, 256);
+        else MPPI_LAUNCH_P(8, 256);
     }
 #undef MPPI_LAUNCH_P
 #undef MPPI_LAUNCH
