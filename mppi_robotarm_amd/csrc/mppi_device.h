@@ -173,6 +173,25 @@ __device__ __forceinline__ float min_raw(float a, float b) {
 
 // ------------------------------------------------------------ window search
 
+// Minimum of N packed keys as a tree of v_min3 (depth ceil(log3 N))
+template <int N>
+__device__ __forceinline__ float min_tree(const float (&k)[N]) {
+    if constexpr (N == 1) {
+        return k[0];
+    } else {
+        constexpr int M = (N + 2) / 3;
+        float r[M];
+#pragma unroll
+        for (int g = 0; g < M; ++g) {
+            const int a = 3 * g;
+            if (a + 2 < N) r[g] = min3_raw(k[a], k[a + 1], k[a + 2]);
+            else if (a + 1 < N) r[g] = min_raw(k[a], k[a + 1]);
+            else r[g] = k[a];
+        }
+        return min_tree<M>(r);
+    }
+}
+
 // Nearest waypoint of the shared window (control.py:200-232): the window is
 // uploaded as centred keys (-2 rx', -2 ry', rx'^2 + ry'^2; pads 1e30 — the
 // factor -2 is exact, so it costs nothing to fold it into the table), and
@@ -230,7 +249,11 @@ struct Search {
         const f32x2 ax2 = {dx, dx}, ay2 = {dy, dy};
         const float pp = fmaf(dx, dx, dy * dy);
         const f32x2 pp2 = {pp, pp};
+#ifdef MPPI_MIN_CHAIN
         float best = 3.0e38f;
+#else
+        float kk[2 * SP];
+#endif
 #pragma unroll
         for (int i = 0; i < SP; ++i) {
             f32x2 key = __builtin_elementwise_fma(ax2, krx[i], __builtin_elementwise_fma(ay2, kry[i], kc[i]));
@@ -240,8 +263,18 @@ struct Search {
             const unsigned j = (unsigned)(sub * SL + 2 * i);
             const float k0 = __uint_as_float((__float_as_uint(key.x) & ~31u) | j);
             const float k1 = __uint_as_float((__float_as_uint(key.y) & ~31u) | (j + 1));
+#ifdef MPPI_MIN_CHAIN
             best = min3_raw(best, k0, k1);
+#else
+            kk[2 * i] = k0;
+            kk[2 * i + 1] = k1;
+#endif
         }
+#ifndef MPPI_MIN_CHAIN
+        // the same v_min3 count as a running minimum, but 4 levels deep instead of
+        // 15 (the keys carry distinct indices, so the order of the minima is free)
+        float best = min_tree<2 * SP>(kk);
+#endif
         if (LPS >= 2) best = min_raw(best, dpp_f32<0xB1>(best));  // quad_perm xor 1
         if (LPS >= 4) best = min_raw(best, dpp_f32<0x4E>(best));  // quad_perm xor 2
         if (LPS >= 8) best = min_raw(best, dpp_f32<0x141>(best));  // row_half_mirror: the other quad of 8
