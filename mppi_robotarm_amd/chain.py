@@ -393,11 +393,8 @@ class ChainMPPIController:
         if self.visualze_sampled_trajs:
             tr = eng.trajectories(base_u=None, noise=self._noise_dev)
             if world > 1:
-                import torch.distributed as dist
-                parts = [None] * world
-                dist.all_gather_object(parts, (eng.k_offset, tr.cpu().numpy()), group=self.process_group)
-                for off, arr in parts:
-                    sampled[off:off + arr.shape[0]] = arr
+                from .distributed import gather_trajectories
+                gather_trajectories(tr, self.K, sampled, self.process_group)
             else:
                 sampled[:] = tr.double().cpu().numpy()
         self.u_prev[:-1] = u[1:]

@@ -213,11 +213,8 @@ class MPPIControllerForPathTracking:
         if self.visualze_sampled_trajs:
             tr = eng.trajectories(base_u=None, noise=self._noise_dev)   # pre-update u, v[k, t-1]
             if world > 1:
-                import torch.distributed as dist
-                parts = [None] * world
-                dist.all_gather_object(parts, (eng.k_offset, tr.cpu().numpy()), group=self.process_group)
-                for off, arr in parts:
-                    sampled_traj_list[off:off + arr.shape[0]] = arr
+                from .distributed import gather_trajectories
+                gather_trajectories(tr, self.K, sampled_traj_list, self.process_group)
             else:
                 sampled_traj_list[:] = tr.double().cpu().numpy()
 
@@ -324,11 +321,8 @@ class MPPIControllerForPathTracking:
             self.last_S = self._S_dev.cpu().numpy()
         if tr is not None:
             if world > 1:
-                import torch.distributed as dist
-                parts = [None] * world
-                dist.all_gather_object(parts, (eng.k_offset, tr.cpu().numpy()), group=self.process_group)
-                for off, arr in parts:
-                    sampled_traj_list[off:off + arr.shape[0]] = arr
+                from .distributed import gather_trajectories
+                gather_trajectories(tr, self.K, sampled_traj_list, self.process_group)
             else:
                 sampled_traj_list[:] = tr.double().cpu().numpy()
         # next step's noise after the last read-back: the draw overlaps the caller's

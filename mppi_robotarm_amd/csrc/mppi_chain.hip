@@ -14,7 +14,7 @@
 //    [T][N][K] fp32: N coalesced 4-B-per-lane rows per step.  Same epilogue,
 //    in-launch merges and fused update as the 2-link engine (mppi_device.h),
 //    with T*N columns per partial row (MAXCH = 4 column chunks).
-//  * chain_traj_kernel<N>, chain_philox_kernel: trajectory re-roll and
+//  * chain_traj_kernel<N, NOISE>, chain_philox_kernel: trajectory re-roll and
 //    counter-based Gaussian noise with an n x n Cholesky factor.
 //
 // C ABI: include/mppi_rocm.h (mppi_chain_*).
@@ -629,33 +629,72 @@ __global__ __launch_bounds__(kCT) void chain_merge_kernel(const ChainConst c, co
 }
 
 // Trajectory re-roll (control.py:129-145 with the chain): control(t) =
-// base[(t-1) mod T] (+ eps); out[k][t][2N] = (q, dq) after step t.
-template <int N>
+// base[(t-1) mod T] (+ eps); out[k][t][2N] = (q, dq) after step t.  As in
+// traj_kernel, the states of kChainTB steps go through an LDS tile and each
+// flush writes every sample's kChainTB * 2N floats as one contiguous run.
+constexpr int kChainTB = 2;
+// LDS-only barrier (see traj_kernel)
+#define CHAIN_LDS_BARRIER() asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory")
+template <int N, bool NOISE>
 __global__ __launch_bounds__(kCT) void chain_traj_kernel(const ChainConst c, const ChainStep* __restrict__ st,
                                                          const float* __restrict__ base,
                                                          const float* __restrict__ noise, int Kn,
                                                          float* __restrict__ out) {
-    const int k = blockIdx.x * kCT + threadIdx.x;
-    if (k >= Kn) return;
+    constexpr int W = 2 * N;   // floats per state
+    __shared__ float tile[kChainTB][W][kCT];
+    const int tid = threadIdx.x;
+    const int k0 = blockIdx.x * kCT;
+    const int k = min(k0 + tid, Kn - 1);   // lanes past Kn recompute the last sample, never stored
+    const int nk = min(kCT, Kn - k0);
     const int T = c.T;
-    const float exf = noise ? ((c.k_offset + k) < c.k_exploit ? 1.f : 0.f) : 1.f;
+    const float exf = NOISE ? ((c.k_offset + k) < c.k_exploit ? 1.f : 0.f) : 1.f;
     ChainState<N> x;
     x.load(st->x0);
-    for (int t = 0; t < T; ++t) {
-        const int ti = t == 0 ? T - 1 : t - 1;
-        float v[N];
+    // a tile's noise is loaded one tile ahead (see traj_kernel)
+    auto load_tile = [&](int t0, float (&e)[kChainTB][N]) {
 #pragma unroll
-        for (int d = 0; d < N; ++d) {
-            v[d] = base[ti * N + d];
-            if (noise) v[d] = fmaf(exf, v[d], noise[((size_t)ti * N + d) * c.K_local + k]);
-        }
-        x.step(v, DynArg{c.dyn});
-        float* o = out + ((size_t)k * T + t) * 2 * N;
+        for (int j = 0; j < kChainTB; ++j) {
+            const int t = min(t0 + j, T - 1);
+            const int ti = t == 0 ? T - 1 : t - 1;
 #pragma unroll
-        for (int a = 0; a < N; ++a) {
-            o[a] = x.qa(a);
-            o[N + a] = x.dqa(a);
+            for (int d = 0; d < N; ++d) e[j][d] = NOISE ? noise[((size_t)ti * N + d) * c.K_local + k] : 0.f;
         }
+    };
+    float cur[kChainTB][N];
+    load_tile(0, cur);
+    for (int t0 = 0; t0 < T; t0 += kChainTB) {
+        const int nt = min(kChainTB, T - t0);
+        float nxt[kChainTB][N];
+        load_tile(t0 + kChainTB, nxt);
+#pragma unroll
+        for (int j = 0; j < kChainTB; ++j) {
+            if (j >= nt) break;
+            const int t = t0 + j;
+            const int ti = t == 0 ? T - 1 : t - 1;
+            float v[N];
+#pragma unroll
+            for (int d = 0; d < N; ++d) {
+                v[d] = base[ti * N + d];
+                if (NOISE) v[d] = fmaf(exf, v[d], cur[j][d]);
+            }
+            x.step(v, DynArg{c.dyn});
+#pragma unroll
+            for (int a = 0; a < N; ++a) {
+                tile[j][a][tid] = x.qa(a);
+                tile[j][N + a][tid] = x.dqa(a);
+            }
+        }
+        CHAIN_LDS_BARRIER();
+        const int run = nt * W;   // floats of one sample in this flush
+        for (int i = tid; i < nk * run; i += kCT) {
+            const int s = i / run, r = i - s * run;
+            out[((size_t)(k0 + s) * T + t0) * W + r] = tile[r / W][r % W][s];
+        }
+        CHAIN_LDS_BARRIER();
+#pragma unroll
+        for (int j = 0; j < kChainTB; ++j)
+#pragma unroll
+            for (int d = 0; d < N; ++d) cur[j][d] = nxt[j][d];
     }
 }
 
@@ -1125,9 +1164,15 @@ int mppi_chain_rollout_traj(mppi_chain_ctx* c, const double* base_u, const float
             return fail(MPPI_E_HIP, "base copy");
     }
     const int blocks = (K + kCT - 1) / kCT;
-#define MPPI_T(N)                                                                                                  \
-    hipLaunchKernelGGL(chain_traj_kernel<N>, dim3(blocks), dim3(kCT), 0, c->stream, c->kc, cur, c->d_base, noise_dev, \
-                       K, out_dev)
+#define MPPI_T(N)                                                                                                \
+    do {                                                                                                         \
+        if (noise_dev)                                                                                           \
+            hipLaunchKernelGGL((chain_traj_kernel<N, true>), dim3(blocks), dim3(kCT), 0, c->stream, c->kc, cur,  \
+                               c->d_base, noise_dev, K, out_dev);                                                \
+        else                                                                                                     \
+            hipLaunchKernelGGL((chain_traj_kernel<N, false>), dim3(blocks), dim3(kCT), 0, c->stream, c->kc, cur, \
+                               c->d_base, noise_dev, K, out_dev);                                                \
+    } while (0)
     MPPI_CHAIN_DISPATCH(n, MPPI_T)
 #undef MPPI_T
     const hipError_t e = hipGetLastError();

@@ -626,28 +626,79 @@ __global__ __launch_bounds__(NT) void merge_kernel(const KConst c, const double*
 }
 
 // Trajectory re-roll (control.py:129-145): control(t) = base[(t-1) mod T] (+ eps).
+// The output is the reference's [K][T][4] order: a sample's states are
+// contiguous, so a lane writing its own state each step would scatter 16 B per
+// lane at a T * 16 B stride.  The states go through an LDS tile of kTrajTB steps
+// instead, and each flush writes whole kTrajTB * 16 B runs per sample (eight
+// steps = one 128 B line), lane-contiguous.
+constexpr int kTrajTB = 8;
+// LDS-only barrier: __syncthreads() would also drain the tile's stores and the
+// next tile's noise loads (vmcnt(0) on gfx9: loads and stores share the counter)
+#define LDS_BARRIER() asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory")
+// base: the controls, float2 elements bstride apart (1: a plain [T][2] array;
+// 2: the (u, a) float4 rows of a DevStep, read in place)
+template <bool NOISE>
 __global__ __launch_bounds__(kThreads) void traj_kernel(const KConst c, const StepStatic ss,
-                                                        const float2* __restrict__ base,
+                                                        const float2* __restrict__ base, int bstride,
                                                         const float2* __restrict__ noise, int Kn,
                                                         float4* __restrict__ out) {
-    const int k = blockIdx.x * kThreads + threadIdx.x;
-    if (k >= Kn) return;
+    __shared__ float4 tile[kTrajTB][kThreads];
+    const int tid = threadIdx.x;
+    const int k0 = blockIdx.x * kThreads;
+    const int k = min(k0 + tid, Kn - 1);   // lanes past Kn recompute the last sample, never stored
+    const int nk = min(kThreads, Kn - k0);
     const int T = c.T;
-    const float exf = noise ? ((c.k_offset + k) < c.k_exploit ? 1.f : 0.f) : 1.f;
+    const float exf = NOISE ? ((c.k_offset + k) < c.k_exploit ? 1.f : 0.f) : 1.f;
     Arm x;
     arm_init(x, ss.x0);
     const DynK dk = make_dynk(c, 0.f, 0.f);
-    for (int t = 0; t < T; ++t) {
-        const int ti = t == 0 ? T - 1 : t - 1;
-        const float2 b = base[ti];
-        f32x2 v = {b.x, b.y};
-        if (noise) {
-            const float2 e = noise[(size_t)ti * c.K_local + k];
-            v = __builtin_elementwise_fma(splat(exf), v, f32x2{e.x, e.y});
+    // the noise of a whole tile is loaded two tiles ahead (a lane's per-step load
+    // would otherwise be waited for every step: one wave per SIMD hides nothing)
+    auto load_tile = [&](int t0, float2 (&d)[kTrajTB]) {
+#pragma unroll
+        for (int j = 0; j < kTrajTB; ++j) {
+            const int t = min(t0 + j, T - 1);
+            const int ti = t == 0 ? T - 1 : t - 1;
+            d[j] = NOISE ? noise[(size_t)ti * c.K_local + k] : make_float2(0.f, 0.f);
         }
-        arm_step(x, v, dk);
-        const f32x2 q = x.Q * 6.283185307179586f;
-        out[(size_t)k * T + t] = make_float4(q.x, q.y, x.dq.x, x.dq.y);
+    };
+    // one tile: its 8 steps, the states into the LDS tile, one coalesced flush
+    auto tile_steps = [&](const float2 (&cur)[kTrajTB], int t0) {
+        const int nt = min(kTrajTB, T - t0);
+#pragma unroll
+        for (int j = 0; j < kTrajTB; ++j) {
+            if (j >= nt) break;
+            const int t = t0 + j;
+            const int ti = t == 0 ? T - 1 : t - 1;
+            const float2 b = base[ti * bstride];
+            f32x2 v = {b.x, b.y};
+            if (NOISE) v = __builtin_elementwise_fma(splat(exf), v, f32x2{cur[j].x, cur[j].y});
+            arm_step(x, v, dk);
+            const f32x2 q = x.Q * 6.283185307179586f;
+            tile[j][tid] = make_float4(q.x, q.y, x.dq.x, x.dq.y);
+        }
+        LDS_BARRIER();
+        // flush: element i of the block's nk * nt states -> sample i / nt, step i % nt
+        for (int i = tid; i < nk * nt; i += kThreads) {
+            const int s = i / nt, j = i - s * nt;
+            out[(size_t)(k0 + s) * T + t0 + j] = tile[j][s];
+        }
+        LDS_BARRIER();
+    };
+    // three register tiles in rotation, compile-time slots: tile i + 2's noise
+    // is issued before tile i is stepped (~2 tiles of dynamics ahead of its use)
+    float2 ta[kTrajTB], tb[kTrajTB], tc[kTrajTB];
+    load_tile(0, ta);
+    load_tile(kTrajTB, tb);
+    for (int t0 = 0; t0 < T; t0 += 3 * kTrajTB) {
+        load_tile(t0 + 2 * kTrajTB, tc);
+        tile_steps(ta, t0);
+        if (t0 + kTrajTB >= T) break;
+        load_tile(t0 + 3 * kTrajTB, ta);
+        tile_steps(tb, t0 + kTrajTB);
+        if (t0 + 2 * kTrajTB >= T) break;
+        load_tile(t0 + 4 * kTrajTB, tb);
+        tile_steps(tc, t0 + 2 * kTrajTB);
     }
 }
 
@@ -1261,6 +1312,7 @@ int mppi_rollout_traj(mppi_ctx* c, const double* base_u, const float* noise_dev,
     if (!c || !out_dev || K < 1 || K > c->cfg.K_local) return fail(MPPI_E_ARG, "bad argument");
     const DevStep* cur = c->d_step + c->cur;
     const float2* base;
+    int bstride = 1;
     if (base_u) {
         HIP_TRY(hipEventSynchronize(c->staged));
         for (int t = 0; t < c->cfg.T; ++t) c->h_base[t] = make_float2((float)base_u[2 * t], (float)base_u[2 * t + 1]);
@@ -1268,21 +1320,25 @@ int mppi_rollout_traj(mppi_ctx* c, const double* base_u, const float* noise_dev,
         HIP_TRY(hipEventRecord(c->staged, c->stream));
         base = c->d_base;
     } else {
-        // nominal u0,u1 of the current step block: ua[t].xy, read with stride 16 B
-        HIP_TRY(hipMemcpy2DAsync(c->d_base, sizeof(float2), (const char*)cur + offsetof(DevStep, ua), sizeof(float4),
-                                 sizeof(float2), c->cfg.T, hipMemcpyDeviceToDevice, c->stream));
-        base = c->d_base;
+        // the current nominal in place: ua[t].xy, every other float2 (stream order
+        // keeps the next launch's write of this block behind the re-roll)
+        base = reinterpret_cast<const float2*>(reinterpret_cast<const char*>(cur) + offsetof(DevStep, ua));
+        bstride = 2;
     }
     const int blocks = (K + kThreads - 1) / kThreads;
-    hipLaunchKernelGGL(traj_kernel, dim3(blocks), dim3(kThreads), 0, c->stream, c->kc, c->stat, base,
-                       reinterpret_cast<const float2*>(noise_dev), K, reinterpret_cast<float4*>(out_dev));
+    if (noise_dev)
+        hipLaunchKernelGGL(traj_kernel<true>, dim3(blocks), dim3(kThreads), 0, c->stream, c->kc, c->stat, base, bstride,
+                           reinterpret_cast<const float2*>(noise_dev), K, reinterpret_cast<float4*>(out_dev));
+    else
+        hipLaunchKernelGGL(traj_kernel<false>, dim3(blocks), dim3(kThreads), 0, c->stream, c->kc, c->stat, base,
+                           bstride, (const float2*)nullptr, K, reinterpret_cast<float4*>(out_dev));
     return launch_check("traj_kernel");
 }
 
 int mppi_optimal_traj(mppi_ctx* c, float* out_dev) {
     if (!c || !out_dev) return fail(MPPI_E_ARG, "null argument");
     if (!c->upd_valid) return fail(MPPI_E_ARG, "mppi_optimal_traj needs a preceding MPPI_FLAG_FUSED_UPDATE launch");
-    hipLaunchKernelGGL(traj_kernel, dim3(1), dim3(kThreads), 0, c->stream, c->kc, c->stat, c->d_upd,
+    hipLaunchKernelGGL(traj_kernel<false>, dim3(1), dim3(kThreads), 0, c->stream, c->kc, c->stat, c->d_upd, 1,
                        (const float2*)nullptr, 1, reinterpret_cast<float4*>(out_dev));
     return launch_check("traj_kernel");
 }

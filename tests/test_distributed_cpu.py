@@ -212,3 +212,35 @@ def test_attach_exchange_is_collective_safe(tmp_path, bad, where):
     assert r[0][0] == r[1][0] == (1 if bad < 0 else 0)
     if bad < 0:
         assert r[0][1:].tolist() == r[1][1:].tolist() == [0, 1]   # handles in rank order
+
+
+def _traj_worker(rank, world, port, K, T, out_path):
+    import sys
+    sys.path.insert(0, ROOT)
+    from mppi_robotarm_amd.distributed import gather_trajectories, shard_geometry
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        n, off = shard_geometry(K, world, rank)
+        # this rank's shard of a known (K, T, 4) array, fp32 like the device re-roll
+        full = np.arange(K * T * 4, dtype=np.float32).reshape(K, T, 4)
+        out = np.zeros((K, T, 4))
+        gather_trajectories(torch.from_numpy(full[off:off + n].copy()), K, out)
+        np.save(f"{out_path}.{rank}.npy", out)
+        with pytest.raises(ValueError):
+            gather_trajectories(torch.zeros((n + 1, T, 4)), K, out)
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("K,world", [(10, 3), (12, 2)])
+def test_gather_trajectories_uneven_shards(tmp_path, K, world):
+    """Sampled trajectories (control.py:136-145, run.py:36) of uneven shards come
+    back in sample order on every rank (tensor all-gather, padded shards)."""
+    T = 5
+    out = str(tmp_path / "traj")
+    mp.start_processes(_traj_worker, args=(world, _free_port(), K, T, out), nprocs=world, join=True,
+                       start_method="spawn")
+    ref = np.arange(K * T * 4, dtype=np.float32).reshape(K, T, 4).astype(np.float64)
+    for r in range(world):
+        assert np.array_equal(np.load(f"{out}.{r}.npy"), ref)
