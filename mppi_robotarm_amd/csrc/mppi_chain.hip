@@ -633,8 +633,6 @@ __global__ __launch_bounds__(kCT) void chain_merge_kernel(const ChainConst c, co
 // traj_kernel, the states of kChainTB steps go through an LDS tile and each
 // flush writes every sample's kChainTB * 2N floats as one contiguous run.
 constexpr int kChainTB = 2;
-// LDS-only barrier (see traj_kernel)
-#define CHAIN_LDS_BARRIER() asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory")
 template <int N, bool NOISE>
 __global__ __launch_bounds__(kCT) void chain_traj_kernel(const ChainConst c, const ChainStep* __restrict__ st,
                                                          const float* __restrict__ base,
@@ -684,13 +682,13 @@ __global__ __launch_bounds__(kCT) void chain_traj_kernel(const ChainConst c, con
                 tile[j][N + a][tid] = x.dqa(a);
             }
         }
-        CHAIN_LDS_BARRIER();
+        __syncthreads();
         const int run = nt * W;   // floats of one sample in this flush
         for (int i = tid; i < nk * run; i += kCT) {
             const int s = i / run, r = i - s * run;
             out[((size_t)(k0 + s) * T + t0) * W + r] = tile[r / W][r % W][s];
         }
-        CHAIN_LDS_BARRIER();
+        __syncthreads();
 #pragma unroll
         for (int j = 0; j < kChainTB; ++j)
 #pragma unroll

@@ -632,9 +632,6 @@ __global__ __launch_bounds__(NT) void merge_kernel(const KConst c, const double*
 // instead, and each flush writes whole kTrajTB * 16 B runs per sample (eight
 // steps = one 128 B line), lane-contiguous.
 constexpr int kTrajTB = 8;
-// LDS-only barrier: __syncthreads() would also drain the tile's stores and the
-// next tile's noise loads (vmcnt(0) on gfx9: loads and stores share the counter)
-#define LDS_BARRIER() asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory")
 // base: the controls, float2 elements bstride apart (1: a plain [T][2] array;
 // 2: the (u, a) float4 rows of a DevStep, read in place)
 template <bool NOISE>
@@ -677,13 +674,13 @@ __global__ __launch_bounds__(kThreads) void traj_kernel(const KConst c, const St
             const f32x2 q = x.Q * 6.283185307179586f;
             tile[j][tid] = make_float4(q.x, q.y, x.dq.x, x.dq.y);
         }
-        LDS_BARRIER();
+        __syncthreads();
         // flush: element i of the block's nk * nt states -> sample i / nt, step i % nt
         for (int i = tid; i < nk * nt; i += kThreads) {
             const int s = i / nt, j = i - s * nt;
             out[(size_t)(k0 + s) * T + t0 + j] = tile[j][s];
         }
-        LDS_BARRIER();
+        __syncthreads();
     };
     // three register tiles in rotation, compile-time slots: tile i + 2's noise
     // is issued before tile i is stepped (~2 tiles of dynamics ahead of its use)
