@@ -976,7 +976,10 @@ __device__ __forceinline__ void exchange_merge(const XDesc& x, const RowGeo& geo
 // 2^kPrioShift ticks (100 MHz: ~41 us), the phase flipped by the ticket parity.
 // Priority steers scheduling only; no result depends on it.
 constexpr int kCuSlots = 2048;   // (XCC, SE, SH, CU) keys
-constexpr int kPrioShift = 12;
+#ifndef MPPI_PRIO_SHIFT
+#define MPPI_PRIO_SHIFT 12
+#endif
+constexpr int kPrioShift = MPPI_PRIO_SHIFT;
 __device__ __forceinline__ unsigned cu_key() {
     const unsigned hw = __builtin_amdgcn_s_getreg(0xF804);    // HW_ID
     const unsigned xcc = __builtin_amdgcn_s_getreg(0xF814);   // XCC_ID
