@@ -676,3 +676,50 @@ def test_bound_tick_equals_general_dropin(paths):
     assert fast._bound is not None                  # the fast controller really took the tick
     fast.close()
     slow.close()
+
+
+def _random_cases(n=24, seed=2024):
+    rng = np.random.default_rng(seed)
+    cases = []
+    for i in range(n):
+        K = int(rng.choice([1, 7, 64, 100, 777, 2048, 4096, 5000, 12345, 20000]))
+        T = int(rng.integers(1, 129))
+        lam = float(10 ** rng.uniform(0, 7))
+        lps = int(rng.choice([0, 1, 2, 4, 8]))
+        expl = float(rng.choice([0.0, 0.0, 0.1, 0.5]))
+        prev = int(rng.integers(0, 200)) if i % 4 else int(rng.integers(0, 4000))
+        cases.append((i, K, T, lam, lps, expl, prev))
+    return cases
+
+
+@pytest.mark.parametrize("i,K,T,lam,lps,expl,prev", _random_cases())
+def test_random_configs_against_c_oracle(i, K, T, lam, lps, expl, prev, paths):
+    """Seeded random sweep (control.py:91-118): K from 1 to 20000, T from 1 to 128, lambda over seven
+    decades, every lanes-per-sample split, exploration fractions, windows anywhere on the path
+    (truncated ones at its end), a random SPD Sigma and start pose.  S to 5e-5, the argmin (or a
+    near-tie at fp32 resolution), the weighted noise to 1e-4 against the C fp64 oracle."""
+    rng = np.random.default_rng(1000 + i)
+    A = rng.normal(0, 1, (2, 2))
+    sigma = A @ A.T + np.eye(2) * rng.uniform(2.0, 20.0)
+    path = paths["xydq_circle"]
+    prev = min(prev, len(path) - 1)
+    win = path[prev:prev + 30]
+    x0 = X0 + np.concatenate([rng.normal(0, 0.05, 2), rng.normal(0, 0.5, 2)])
+    u = np.array([[10.0, -2.0]] * T) + rng.normal(0, 2.0, (T, 2))
+    eng = _engine(K, T, lps=lps, param_lambda=lam, param_exploration=expl, sigma=sigma)
+    eng.set_step_inputs(x0, win, u)
+    noise = eng.philox_noise(11 + i, i)
+    S_dev = torch.empty(K, dtype=torch.float64, device="cuda")
+    eng.rollout(noise, S_out=S_dev)
+    w_eps = eng.weighted_noise()
+    S = S_dev.cpu().numpy()
+    eps_tk = noise.cpu().numpy()
+    ref_S = coracle.rollout_costs(x0, u, eps_tk, win, 0.006, lam, 0.98, sigma, RUNPY["stage_cost_weight"],
+                                  RUNPY["terminal_cost_weight"], O.ArmParams(),
+                                  k_exploit=math.ceil((1.0 - expl) * K), layout="TK")
+    assert float(np.max(np.abs(S - ref_S) / np.abs(ref_S))) < S_TOL
+    j, j_ref = int(np.argmin(S)), int(np.argmin(ref_S))
+    assert j == j_ref or abs(ref_S[j] - ref_S[j_ref]) <= 1e-6 * abs(ref_S[j_ref])
+    _, ref_weps = coracle.weighted_noise(ref_S, eps_tk, lam, layout="TK")
+    assert _urel(w_eps, ref_weps) < U_TOL
+    eng.close()
