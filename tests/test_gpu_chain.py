@@ -224,3 +224,48 @@ def test_chain_errors():
     with pytest.raises(ValueError):
         ChainEngine(256, 8, 0.006, 100.0, 0.98, np.eye(8), W, TW, chain=ChainParams(*(tuple([1.0] * 8),) * 7),
                     device=0)
+
+
+def _uniform_chain(mod, n):
+    """n uniform slender links of 1 kg and 2 m total reach (config 5's arm at n = 7)."""
+    L = 2.0 / n
+    return mod.ChainParams(m=(1.0,) * n, l=(L,) * n, lc=(L / 2,) * n, I=(L * L / 12.0,) * n, fk=(L,) * n,
+                           J=(0.1,) * n, b=(1.0,) * n)
+
+
+@pytest.mark.parametrize("n,K,T,lam", [(3, 256, 16, 100.0), (4, 3000, 24, 100.0), (5, 777, 32, 1.0e4),
+                                       (6, 2048, 20, 100.0), (7, 1000, 9, 1.0e8), (2, 513, 40, 100.0)])
+def test_chain_every_link_count_against_c_oracle(n, K, T, lam, paths):
+    """Every compiled chain length (chain_rollout_kernel<N>, N = 2..7) against the C fp64 chain oracle, with a
+    random SPD Sigma, gravity-holding nominal plus noise, and a window away from the path start."""
+    from mppi_robotarm_amd.chain import ChainEngine, ChainParams, gravity_torque
+    rng = np.random.default_rng(n * 100 + T)
+    import mppi_robotarm_amd.chain as chain_mod
+    P, Po = _uniform_chain(chain_mod, n), _uniform_chain(CO, n)
+    assert isinstance(P, ChainParams)
+    q = np.array([1.4] + [-2.2 / (n - 1)] * (n - 1)) if n > 1 else np.array([1.4])
+    x0 = np.concatenate([q, rng.normal(0, 0.2, n)])
+    A = rng.normal(0, 1, (n, n))
+    sig = A @ A.T / n + np.diag(np.linspace(8.0, 1.0, n))
+    u = np.tile(gravity_torque(q, P), (T, 1)) + rng.normal(0, 0.3, (T, n))
+    eng = ChainEngine(K, T, 0.006, lam, 0.98, sig, W, TW, 0.0, P, device=0)
+    win = paths["xydq_circle"][40:70]
+    eng.set_step_inputs(x0, win, u)
+    noise = eng.philox_noise(3 + n, 1)
+    S_dev = torch.empty(K, dtype=torch.float64, device="cuda")
+    eng.rollout(noise, S_out=S_dev)
+    w = eng.weighted_noise()
+    S = S_dev.cpu().numpy()
+    nz = noise.cpu().numpy()
+    Sr = coracle.chain_rollout_costs(x0, u, nz, win, 0.006, lam, 0.98, sig, W, TW, Po, layout="TNK")
+    _, wr = coracle.chain_weighted_noise(Sr, nz, lam, layout="TNK")
+    rel = np.abs(S - Sr) / np.abs(Sr)
+    print(f"chain n={n} K={K} T={T}: S rel-err p99 {np.percentile(rel, 99):.2e} max {rel.max():.2e}, "
+          f"w_eps {_urel(w, wr):.2e}")
+    assert np.all(np.isfinite(S))
+    j, jr = int(np.argmin(S)), int(np.argmin(Sr))
+    assert j == jr or abs(Sr[j] - Sr[jr]) <= 1e-5 * abs(Sr[jr])
+    assert float(np.percentile(rel, 99)) < 2e-4
+    assert float(rel.max()) < 5e-3
+    assert _urel(w, wr) < U_TOL
+    eng.close()
