@@ -76,6 +76,9 @@ def valu_roofline(tj, kern_ms):
     if waves_per_simd <= 1.0:
         # a lone wave cannot use the SIMD's full rate: its own ceiling is one instruction per 4 cycles
         out["frac_one_wave_ceiling"] = achieved * LONE_WAVE_ISSUE_CYC
+    for key in ("valu_active_frac_of_wave_time", "cycles_per_valu_inst"):
+        if tj.get(key) is not None:
+            out[key] = tj[key]   # SQ_ACTIVE_INST_VALU of the committed PMC pass (how busy the VALU is)
     return out
 
 

@@ -86,6 +86,11 @@ def main():
         # whole-device VALU wave-instructions per launch (bench.py's "valu" roofline)
         out["valu_insts_per_launch"] = sq["SQ_INSTS_VALU"]
         out["waves_per_launch"] = sq.get("SQ_WAVES")
+        if "SQ_ACTIVE_INST_VALU" in sq and "SQ_WAVE_CYCLES" in sq:
+            # both in quad-cycles: the share of a wave's lifetime its VALU is executing, and
+            # the cycles one VALU instruction occupies it (4 = the wave64 issue cadence)
+            out["valu_active_frac_of_wave_time"] = sq["SQ_ACTIVE_INST_VALU"] / sq["SQ_WAVE_CYCLES"]
+            out["cycles_per_valu_inst"] = 4.0 * sq["SQ_ACTIVE_INST_VALU"] / sq["SQ_INSTS_VALU"]
     name = "traffic.json" if workload == "c3" else f"traffic_{workload}.json"
     json.dump(out, open(os.path.join(os.path.dirname(dst.rstrip('/')), name), "w"), indent=1)
     if sq:
