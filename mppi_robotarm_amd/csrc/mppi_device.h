@@ -92,6 +92,20 @@ __device__ __forceinline__ float readlane_f32(float v, int l) {
     return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), l));
 }
 
+// v_min_f64 / v_max_f64 issued directly: fmin()/fmax() make hipcc canonicalise
+// both operands first (a v_max_f64 x, x each).  Same results for every input
+// but signalling NaNs (IEEE minNum / maxNum, like fmin / fmax).
+__device__ __forceinline__ double min_raw_f64(double a, double b) {
+    double r;
+    asm("v_min_f64 %0, %1, %2" : "=v"(r) : "v"(a), "v"(b));
+    return r;
+}
+__device__ __forceinline__ double max_raw_f64(double a, double b) {
+    double r;
+    asm("v_max_f64 %0, %1, %2" : "=v"(r) : "v"(a), "v"(b));
+    return r;
+}
+
 // Whole-wave reductions (all 64 lanes active), result wave-uniform: DPP
 // quad_perm xor 1 / xor 2, row_half_mirror, row_mirror reduce each row of 16
 // in registers, then the four row results are combined from v_readlane — no
@@ -114,7 +128,7 @@ __device__ __forceinline__ T wave_reduce(T v, Op op) {
     }
 }
 struct OpMin {
-    __device__ double operator()(double a, double b) const { return fmin(a, b); }
+    __device__ double operator()(double a, double b) const { return min_raw_f64(a, b); }
 };
 struct OpAdd {
     template <class T>
@@ -452,7 +466,7 @@ __device__ __forceinline__ double block_min_f64(double v, SM& sm) {
     __syncthreads();
     double r = sm.red[0];
 #pragma unroll
-    for (int w = 1; w < NT / 64; ++w) r = fmin(r, sm.red[w]);
+    for (int w = 1; w < NT / 64; ++w) r = min_raw_f64(r, sm.red[w]);
     return r;
 }
 
@@ -550,7 +564,7 @@ __device__ __forceinline__ void merge_rows_block(__amdgpu_buffer_rsrc_t rows, in
             }
         }
         const double rho_l = lane < nr ? rho_r : INFINITY;
-        const double rnew = fmin(rho, wave_min_f64(rho_l));
+        const double rnew = min_raw_f64(rho, wave_min_f64(rho_l));
         double s_l = 0.0;
         if (lane < nr) {
             const double s = exp((rnew - rho_l) * inv_lambda);
@@ -695,7 +709,7 @@ __device__ __forceinline__ bool direct_merge(__amdgpu_buffer_rsrc_t rows, int n,
     }
     double m = rho_l[0];
 #pragma unroll
-    for (int j = 1; j < P; ++j) m = fmin(m, rho_l[j]);
+    for (int j = 1; j < P; ++j) m = min_raw_f64(m, rho_l[j]);
     const double rho = wave_min_f64(m);
     double s_l[P];
     unsigned long long rel[P];
@@ -867,7 +881,7 @@ __device__ __forceinline__ bool arrive_last(unsigned* counter, unsigned expected
 // Upper median of 10 (rank 5): a 29-comparator sorting network (verified on all
 // 2^10 0/1 inputs), the element scipy.ndimage.median_filter(size=10) returns.
 __device__ __forceinline__ double median10(double* v) {
-#define CX(i, j) { const double lo = fmin(v[i], v[j]), hi = fmax(v[i], v[j]); v[i] = lo; v[j] = hi; }
+#define CX(i, j) { const double lo = min_raw_f64(v[i], v[j]), hi = max_raw_f64(v[i], v[j]); v[i] = lo; v[j] = hi; }
     CX(4, 9) CX(3, 8) CX(2, 7) CX(1, 6) CX(0, 5) CX(1, 4) CX(6, 9) CX(0, 3) CX(5, 8) CX(0, 2)
     CX(3, 6) CX(7, 9) CX(0, 1) CX(2, 4) CX(5, 7) CX(8, 9) CX(1, 2) CX(4, 6) CX(7, 8) CX(3, 5)
     CX(2, 5) CX(6, 8) CX(1, 3) CX(4, 7) CX(2, 3) CX(6, 7) CX(3, 4) CX(5, 6) CX(4, 5)
