@@ -71,6 +71,12 @@ for i in range(steps):
     if d[:, 15].any():
         print(f"         last rho published {us(d[:, 15].max()):5.1f} (loop end of that wg {us(d[np.argmax(d[:, 15]), 1]):5.1f})"
               f" -> final merge done {us(d[last, 11]):5.1f}")
+    gm = d[:, 10][d[:, 10] > 0]
+    if len(gm) and (np.arange(len(d)) != last).any():
+        others = [b for b in range(len(d)) if b != last and d[b, 10] > 0]
+        if others:
+            print(f"         level-1 group mergers: {len(others)}, last done {us(max(d[b, 10] for b in others)):5.1f} "
+                  f"(final workgroup's update done {us(d[last, 7]):5.1f})")
     st = (d[:, 0] - t0) / 100.0
     late = np.argsort(st)[-3:][::-1]
     print("         start offsets: med %.2f p99 %.2f max %.2f us; latest blocks %s (xcc %s)" % (
