@@ -69,7 +69,7 @@ typedef struct {
     double stage_cost_weight[4];
     double terminal_cost_weight[4];
     mppi_arm_params arm;
-    int lanes_per_sample;      /* 0 = auto; 1, 2, 4 or 8 lanes of a wave per sample   */
+    int lanes_per_sample;      /* 0 = auto; 1, 2, 4, 8 or 16 lanes of a wave per sample */
 } mppi_config;
 
 typedef struct mppi_ctx mppi_ctx;

@@ -292,6 +292,7 @@ struct Search {
         if (LPS >= 2) best = min_raw(best, dpp_f32<0xB1>(best));  // quad_perm xor 1
         if (LPS >= 4) best = min_raw(best, dpp_f32<0x4E>(best));  // quad_perm xor 2
         if (LPS >= 8) best = min_raw(best, dpp_f32<0x141>(best));  // row_half_mirror: the other quad of 8
+        if (LPS >= 16) best = min_raw(best, dpp_f32<0x128>(best));  // row_ror:8: the other half of the row
         return __float_as_uint(best) & 31u;
     }
 };

@@ -7,7 +7,7 @@
 // -> terminal cost (control.py:109) -> soft-min weights (control.py:297-314)
 // -> weighted noise sum (control.py:115-118)), written for CDNA4 directly:
 //
-//  * rollout_kernel<LPS>: LPS lanes of a 64-wide wave per sample (1, 2, 4 or 8).
+//  * rollout_kernel<LPS>: LPS lanes of a 64-wide wave per sample (1, 2, 4, 8 or 16).
 //    The serial T loop runs per lane in fp32 registers; the 30-waypoint
 //    argmin is split over the LPS lanes of a sample and closed with DPP
 //    quad_perm min (no LDS, no MFMA: the work is element-wise VALU).  The
@@ -849,12 +849,15 @@ int auto_lps(int K_local) {
     // (tools/gpu_lps_sweep.sh, us per fused step, LPS 2 / 4 / 8:
     // K=2048 T=32 16.0 / 15.3 / 14.6; K=4096 T=32 17.3 / 15.7 / 15.5;
     // K=8192 T=64 23.4 / 20.1 / 20.4; K=16384 T=64 23.3 / 20.2 / 26.9;
-    // K=32768 T=64 23.9 / 29.5 / 53.0).
+    // K=32768 T=64 23.9 / 29.5 / 53.0; LPS 4 / 8 / 16: K=2048 T=32 15.2 / 14.7 /
+    // 14.4; K=4096 T=32 15.3 / 15.2 / 15.5; K=4096 T=64 19.5 / 19.1 / 19.0;
+    // K=8192 T=32 16.4 / 16.7 / 19.9).
     const long long waves1 = ((long long)K_local + 63) / 64;
     if (waves1 >= 1024) return 1;
     if (waves1 >= 512) return 2;
     if (waves1 >= 128) return 4;
-    return 8;
+    if (waves1 >= 64) return 8;
+    return 16;
 }
 }  // namespace
 
@@ -881,9 +884,9 @@ int mppi_ctx_create(const mppi_config* cfg, int device, void* stream, mppi_ctx**
     c->sig_inv[2] = -S[2] / det;
     c->sig_inv[3] = S[0] / det;
     int lps = cfg->lanes_per_sample > 0 ? cfg->lanes_per_sample : auto_lps(cfg->K_local);
-    if (lps != 1 && lps != 2 && lps != 4 && lps != 8) {
+    if (lps != 1 && lps != 2 && lps != 4 && lps != 8 && lps != 16) {
         delete c;
-        return fail(MPPI_E_ARG, "lanes_per_sample must be 0, 1, 2, 4 or 8");
+        return fail(MPPI_E_ARG, "lanes_per_sample must be 0, 1, 2, 4, 8 or 16");
     }
     c->lps = lps;
     // 512-thread workgroups when the grid fills every CU with one of them (8 waves:
@@ -946,10 +949,12 @@ int mppi_ctx_create(const mppi_config* cfg, int device, void* stream, mppi_ctx**
         int rc = 0;
         if (c->nt == 512)
             rc = lps == 1 ? occupancy<1, 512>(&per_cu) : lps == 2 ? occupancy<2, 512>(&per_cu)
-               : lps == 4 ? occupancy<4, 512>(&per_cu) : occupancy<8, 512>(&per_cu);
+               : lps == 4 ? occupancy<4, 512>(&per_cu) : lps == 8 ? occupancy<8, 512>(&per_cu)
+               : occupancy<16, 512>(&per_cu);
         else
             rc = lps == 1 ? occupancy<1, 256>(&per_cu) : lps == 2 ? occupancy<2, 256>(&per_cu)
-               : lps == 4 ? occupancy<4, 256>(&per_cu) : occupancy<8, 256>(&per_cu);
+               : lps == 4 ? occupancy<4, 256>(&per_cu) : lps == 8 ? occupancy<8, 256>(&per_cu)
+               : occupancy<16, 256>(&per_cu);
         if (rc != 0) per_cu = 0;
     }
     c->poll = per_cu >= 1 && c->nblocks <= ncu;
@@ -1197,12 +1202,14 @@ int launch_rollout(mppi_ctx* c, const float* noise_dev, double* S_dev, double* p
         if (c->lps == 1) MPPI_LAUNCH_P(1, 512);
         else if (c->lps == 2) MPPI_LAUNCH_P(2, 512);
         else if (c->lps == 4) MPPI_LAUNCH_P(4, 512);
-        else MPPI_LAUNCH_P(8, 512);
+        else if (c->lps == 8) MPPI_LAUNCH_P(8, 512);
+        else MPPI_LAUNCH_P(16, 512);
     } else {
         if (c->lps == 1) MPPI_LAUNCH_P(1, 256);
         else if (c->lps == 2) MPPI_LAUNCH_P(2, 256);
         else if (c->lps == 4) MPPI_LAUNCH_P(4, 256);
-        else MPPI_LAUNCH_P(8, 256);
+        else if (c->lps == 8) MPPI_LAUNCH_P(8, 256);
+        else MPPI_LAUNCH_P(16, 256);
     }
 #undef MPPI_LAUNCH_P
 #undef MPPI_LAUNCH
