@@ -400,7 +400,12 @@ def main():
     else:
         kern_ms = sum(a.elapsed_time(b) for a, b in ev) / steps
     ranks_seen = 1
+    n_dev = 1
     if world > 1:
+        import socket
+        where = [None] * world
+        dist.all_gather_object(where, (socket.gethostname(), local_rank))
+        n_dev = len(set(where))                        # distinct GPUs (a rehearsal puts ranks on one)
         dev = eng.device if args.backend == "nccl" else "cpu"
         tt = torch.tensor([elapsed, kern_ms], dtype=torch.float64, device=dev)
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
@@ -433,7 +438,9 @@ def main():
                        if c5 else f"MPPI rollouts/sec (K×T state-steps/s) + control-step latency, K={K} T={T}"),
             "value": value,
             "unit": "state-steps/s",
-            "n_gpus": dist.get_world_size() if world > 1 else 1,
+            "n_gpus": n_dev,
+            "ranks": world,
+            "ranks_per_gpu": world / n_dev,
             "ranks_seen": ranks_seen,
             "steps": args.steps,
             "warmup": args.warmup, "settle_ms": args.settle_ms,
@@ -455,9 +462,11 @@ def main():
                        "K_total": K_total, "K_per_gpu": K, "T": T,
                        "lanes_per_sample": 1 if c5 else eng.lanes_per_sample,
                        "exchange": xmode, "backend": args.backend if world > 1 else None,
-                       "parallelism": (f"samples sharded x{world}, " + (
-                           "partial rows exchanged inside the rollout launch (IPC inboxes over xGMI)"
-                           if xmode == "launch" else "RCCL all_gather of partials + merge launch")) if world > 1
+                       "parallelism": (f"samples sharded x{world} ranks on {n_dev} GPU(s), " + (
+                           ("partial rows exchanged inside the rollout launch (IPC inboxes"
+                            + (" over xGMI)" if n_dev == world else "; shared GPU: no xGMI link crossed)"))
+                           if xmode == "launch" else "all_gather of partials + merge launch"
+                           + (" (RCCL)" if args.backend == "nccl" else f" ({args.backend})"))) if world > 1
                        else "single device, fused update" + (f", HIP graph of {chunk} steps" if use_graph
                                                                else ", back-to-back launches")},
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",

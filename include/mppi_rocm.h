@@ -70,6 +70,8 @@ typedef struct {
     double terminal_cost_weight[4];
     mppi_arm_params arm;
     int lanes_per_sample;      /* 0 = auto; 1, 2, 4, 8 or 16 lanes of a wave per sample */
+    double param_gamma;        /* gamma of the control cost (control.py:106), used as   */
+                               /* given; NaN: lambda (1 - alpha) as control.py:45       */
 } mppi_config;
 
 typedef struct mppi_ctx mppi_ctx;
@@ -92,9 +94,12 @@ int mppi_ctx_handoff(const mppi_ctx *ctx, int *poll);
 
 /* Per control step inputs (control.py:70-75): observed state x0[4], the search
  * window ref_path[prev:prev+W, 0:4] (W = min(30, N - prev), row-major W x 4),
- * and the nominal control sequence u[T][2] (self.u_prev).  Async H2D on the
- * context stream from a pinned staging block.  u may be NULL to keep the
- * device-resident nominal (device closed loop, MPPI_FLAG_FUSED_UPDATE). */
+ * and the nominal control sequence u[T][2] (self.u_prev).  x0 and the window
+ * (with its centred search keys) are copied into the context on the host and
+ * reach the next launch by value, as a kernel argument (no copy call); u is
+ * uploaded with one stream-ordered copy from a pinned staging block.  u may be
+ * NULL to keep the device-resident nominal (device closed loop,
+ * MPPI_FLAG_FUSED_UPDATE). */
 int mppi_set_step_inputs(mppi_ctx *ctx, const double *x0, const double *window, int W,
                          const double *u);
 
@@ -186,7 +191,10 @@ int mppi_wait_outputs(mppi_ctx *ctx, const double *x0, double *u_out, double *tr
  * after the rollout launch (stream-ordered behind it: the draw runs once the
  * rollout has read noise_dev, which may be the same buffer), so it overlaps the
  * host's remaining work and the caller's.  Needs T >= 5
- * (device median filter) and a single device (no exchange attached). */
+ * (device median filter).  With an exchange attached (mppi_exchange_attach) the
+ * launch also trades and merges every rank's partial row (MPPI_FLAG_EXCHANGE),
+ * so one call per rank is one multi-GPU control step; every rank must then make
+ * the same sequence of calls. */
 int mppi_step_dropin(mppi_ctx *ctx, const double *x0, const double *window, int W, const double *u,
                      const float *noise_dev, double *S_dev, float *next_noise_dev, unsigned long long seed,
                      unsigned long long next_step, double *u_out, double *traj_out);
@@ -231,6 +239,15 @@ int mppi_dropin_bind(mppi_ctx *ctx, const mppi_dropin_binding *b);
  * the path (control.py:76-78), else mppi_step_dropin on the window
  * ref_path[idx : idx + 30] with the next step's noise (seed, next_step). */
 int mppi_dropin_tick(mppi_ctx *ctx, unsigned long long next_step);
+
+/* mppi_dropin_tick in two halves, so the caller can do host work while the
+ * launch runs (the drop-in allocates the call's fresh sampled_traj_list,
+ * control.py:135, in between): _launch does everything up to and including the
+ * launch (MPPI_E_PATH_END as mppi_dropin_tick, nothing launched); _wait waits
+ * for the published outputs and writes u and traj.  Every successful _launch
+ * must be followed by one _wait before the next _launch. */
+int mppi_dropin_tick_launch(mppi_ctx *ctx, unsigned long long next_step);
+int mppi_dropin_tick_wait(mppi_ctx *ctx);
 
 /* Counter-based Philox4x32-10 Gaussian noise with covariance Sigma (replaces
  * np.random.multivariate_normal, control.py:163, for device-resident runs; not

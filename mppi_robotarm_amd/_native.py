@@ -33,6 +33,7 @@ EXPORTS = (
     "mppi_get_weighted_noise",
     "mppi_get_nominal", "mppi_rollout_traj", "mppi_optimal_traj", "mppi_get_step_outputs", "mppi_step_dropin",
     "mppi_optimal_traj_host", "mppi_wait_outputs", "mppi_dropin_bind", "mppi_dropin_tick",
+    "mppi_dropin_tick_launch", "mppi_dropin_tick_wait",
     "mppi_noise_philox",
     "mppi_sync", "mppi_debug_set_buffer",
     "mppi_debug_nearest", "mppi_debug_dropin_times",
@@ -61,8 +62,13 @@ class ConfigC(C.Structure):
         ("delta_t", C.c_double), ("param_lambda", C.c_double), ("param_alpha", C.c_double),
         ("param_exploration", C.c_double), ("sigma", C.c_double * 4),
         ("stage_cost_weight", C.c_double * 4), ("terminal_cost_weight", C.c_double * 4),
-        ("arm", ArmParamsC), ("lanes_per_sample", C.c_int),
+        ("arm", ArmParamsC), ("lanes_per_sample", C.c_int), ("param_gamma", C.c_double),
     ]
+
+    def __init__(self, *args, **kw):
+        super().__init__(*args, **kw)
+        if "param_gamma" not in kw and len(args) < len(self._fields_):
+            self.param_gamma = float("nan")   # gamma = lambda (1 - alpha), control.py:45
 
 
 CHAIN_MAX_DOF = 8
@@ -121,6 +127,8 @@ def open_library(path: str):
         "mppi_noise_philox": ([vp, C.c_ulonglong, C.c_ulonglong, fp], C.c_int),
         "mppi_dropin_bind": ([vp, C.POINTER(DropinBindingC)], C.c_int),
         "mppi_dropin_tick": ([vp, C.c_ulonglong], C.c_int),
+        "mppi_dropin_tick_launch": ([vp, C.c_ulonglong], C.c_int),
+        "mppi_dropin_tick_wait": ([vp], C.c_int),
         "mppi_sync": ([vp], C.c_int),
         "mppi_debug_set_buffer": ([vp, vp], C.c_int),
         "mppi_debug_dropin_times": ([vp, dp], C.c_int),

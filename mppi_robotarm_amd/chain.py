@@ -23,7 +23,8 @@ import torch
 from scipy.ndimage import median_filter
 
 from . import _native as N
-from .distributed import exchange_partials, shard_geometry
+from .controller import first_min_index
+from .distributed import attach_exchange, check_exchange, exchange_partials, same_on_all_ranks, shard_geometry
 
 SEARCH_IDX_LEN = 30  # control.py:203
 
@@ -283,7 +284,7 @@ class ChainMPPIController:
                  terminal_cost_weight: np.ndarray = np.array([5.0, 5.0, 50.0, 50.0]),
                  visualize_optimal_traj=True, visualze_sampled_trajs=False, *, chain: ChainParams = ChainParams(),
                  u_init=None, device: int | None = None, verbose: bool = False, noise: str = "numpy", seed: int = 0,
-                 process_group=None) -> None:
+                 process_group=None, exchange: str = "auto") -> None:
         self.chain = chain
         self.dim_u, self.dim_x = chain.n, 2 * chain.n
         self.T, self.K = horizon_step_T, number_of_samples_K
@@ -300,6 +301,10 @@ class ChainMPPIController:
             raise ValueError("noise must be 'numpy' or 'device'")
         self.verbose, self.noise_source, self.seed = verbose, noise, int(seed)
         self.process_group = process_group
+        if exchange not in ("auto", "launch", "rccl"):
+            raise ValueError("exchange must be 'auto', 'launch' or 'rccl'")
+        self.exchange = exchange      # multi-GPU: as MPPIControllerForPathTracking
+        self._xmode = None
         self._device = device
         self._engine = None
         self._step_count = 0
@@ -326,7 +331,24 @@ class ChainMPPIController:
             if world > 1:
                 self._gathered = torch.empty(world * self._engine.partial_len, dtype=torch.float64,
                                              device=self._engine.device)
+            self._xmode = None
         return self._engine
+
+    def _multi_setup(self, eng: ChainEngine, noise_check) -> None:
+        """As MPPIControllerForPathTracking._multi_setup: the ranks agree on the noise
+        stream; the in-launch exchange if its self-check passes, else RCCL."""
+        pg = self.process_group
+        if not same_on_all_ranks((self.K, self.T, self.noise_source, self.seed, noise_check), pg):
+            raise RuntimeError("ranks disagree on the noise stream: every rank must seed np.random identically "
+                               "(and pass the same seed / K / T)")
+        mode = "rccl"
+        if self.exchange != "rccl":
+            ok = attach_exchange(eng, pg)
+            ok = ok and check_exchange(eng, self._noise_dev, self._partial, self._gathered, pg)
+            if not ok and self.exchange == "launch":
+                raise RuntimeError("the in-launch exchange failed its self-check (exchange='launch')")
+            mode = "launch" if ok else "rccl"
+        self._xmode = mode
 
     def _effector(self, q):
         th = np.cumsum(q)
@@ -337,7 +359,7 @@ class ChainMPPIController:
         """control.py:200-232 on the end-effector position, host fp64"""
         prev_idx = self.prev_waypoints_idx
         win = self.ref_path[prev_idx:(prev_idx + SEARCH_IDX_LEN)]
-        nearest_idx = int(np.argmin(((x - win[:, 0]) ** 2 + (y - win[:, 1]) ** 2) * 100)) + prev_idx
+        nearest_idx = first_min_index(((x - win[:, 0]) ** 2 + (y - win[:, 1]) ** 2) * 100) + prev_idx
         if update_prev_idx:
             if self.verbose:
                 print(f"0     prev_idx = {prev_idx}")
@@ -374,10 +396,15 @@ class ChainMPPIController:
         window = self.ref_path[self.prev_waypoints_idx:(self.prev_waypoints_idx + SEARCH_IDX_LEN)]
         eng.set_step_inputs(x0, window, u)
         world, _ = self._shard()
+        S_out = self._S_dev if self.keep_costs else None
+        if world > 1 and self._xmode is None:
+            self._multi_setup(eng, float(epsilon[0, 0, 0] + epsilon[-1, -1, -1]) if epsilon is not None else None)
         if world == 1:
-            eng.rollout(self._noise_dev, S_out=self._S_dev if self.keep_costs else None)
+            eng.rollout(self._noise_dev, S_out=S_out)
+        elif self._xmode == "launch":
+            eng.rollout(self._noise_dev, S_out=S_out, exchange=True)      # one launch: rows traded in-launch
         else:
-            eng.rollout(self._noise_dev, S_out=self._S_dev if self.keep_costs else None, partial_out=self._partial)
+            eng.rollout(self._noise_dev, S_out=S_out, partial_out=self._partial)
             exchange_partials(self._partial, self._gathered, self.process_group)
             eng.merge(self._gathered, world)
         w_epsilon = eng.weighted_noise()
@@ -405,3 +432,4 @@ class ChainMPPIController:
         if self._engine is not None:
             self._engine.close()
             self._engine = None
+        self._xmode = None

@@ -25,10 +25,20 @@ spelling), same ``calc_control_input(observed_x)`` contract (control.py:67-152):
 Extra keyword arguments (all optional): ``device``, ``verbose`` (the three
 progress prints of control.py:227-229, on by default like the reference),
 ``noise`` ("numpy" = reference RNG stream, or "device" = on-device Philox),
-``seed`` (device noise), ``lanes_per_sample``, ``arm`` (ArmParams),
-``process_group`` (shard the samples over the ranks of a torch.distributed
-group; one RCCL all-gather of the per-device partials per step) and
+``seed`` (device noise), ``lanes_per_sample``, ``arm`` (ArmParams; its
+``fk_l1``/``fk_l2`` start ``self.l1``/``self.l2``, which the engine follows
+from then on), ``process_group`` (shard the samples over the ranks of a
+torch.distributed group), ``exchange`` (with a process group: "auto" = the
+in-launch exchange, one launch per rank per step, when its one-step self-check
+against the all-gather passes, else one RCCL all-gather of the per-device
+partials plus a merge launch per step; "launch" or "rccl" force one) and
 ``host_update`` (force the host update path).
+
+Multi-GPU: every rank constructs the controller with the same arguments and
+calls ``calc_control_input`` with the same ``observed_x`` in the same order
+(run.py's loop, replicated); with NumPy noise every rank draws the reference's
+full (K, T, 2) stream from the same seed and keeps its slice (checked once,
+at the first step).
 """
 from __future__ import annotations
 
@@ -38,11 +48,23 @@ import numpy as np
 import torch
 from scipy.ndimage import median_filter
 
-from .distributed import exchange_partials, shard_geometry
+import dataclasses
+
+from .distributed import attach_exchange, check_exchange, exchange_partials, same_on_all_ranks, shard_geometry
 from .engine import RolloutEngine
 from .params import ArmParams
 
 SEARCH_IDX_LEN = 30  # control.py:203
+
+
+def first_min_index(d: np.ndarray) -> int:
+    """``d.index(min(d))`` of control.py:213-215 on a 1-D array: Python's min()
+    keeps d[0] and replaces it only on a strict '<', so a NaN at j > 0 is never
+    chosen and a NaN at j = 0 is (np.argmin would return the first NaN)."""
+    j = int(np.argmin(d))
+    if d[j] != d[j]:                                   # a NaN somewhere: Python's rule
+        j = 0 if d[0] != d[0] else int(np.nanargmin(d))
+    return j
 
 
 class MPPIControllerForPathTracking:
@@ -68,6 +90,7 @@ class MPPIControllerForPathTracking:
             lanes_per_sample: int = 0,
             arm: ArmParams | None = None,
             process_group=None,
+            exchange: str = "auto",
             host_update: bool = False,
     ) -> None:
         self.dim_x = 4
@@ -95,8 +118,14 @@ class MPPIControllerForPathTracking:
         self.verbose = verbose
         self.noise_source = noise
         self.seed = int(seed)
+        if arm is not None:                # the cost's kinematics lengths (control.py:55-56)
+            self.l1, self.l2 = arm.fk_l1, arm.fk_l2
         self.arm = ArmParams(fk_l1=float(self.l1), fk_l2=float(self.l2)) if arm is None else arm
         self.process_group = process_group
+        if exchange not in ("auto", "launch", "rccl"):
+            raise ValueError("exchange must be 'auto', 'launch' or 'rccl'")
+        self.exchange = exchange
+        self._xmode = None             # multi-GPU exchange in use: "launch" / "rccl" (decided at the first step)
         self._lanes_per_sample = lanes_per_sample
         self._device = device
         self._engine = None
@@ -107,7 +136,6 @@ class MPPIControllerForPathTracking:
         self.keep_costs = False        # set True to keep per-sample S (self.last_S)
         self.last_S = None
         self._bound = None             # what the engine's drop-in tick is bound to (_bind_key)
-        self._no_trajs = None          # the all-zero sampled_traj_list of a call without sampled trajectories
 
     # ------------------------------------------------------------ engine
     def _shard(self):
@@ -119,11 +147,12 @@ class MPPIControllerForPathTracking:
     def _engine_key(self):
         """Everything the engine bakes in at creation that the reference reads on
         every call (Sigma at control.py:84,106; lambda :112; gamma :106; the cost
-        weights :185,198; the exploration split :98; delta_t :256-259)."""
+        weights :185,198; the exploration split :98; delta_t :256-259; the
+        kinematics lengths self.l1/l2 of :178-179,205-206; the arm constants)."""
         return (np.asarray(self.Sigma, dtype=np.float64).tobytes(), float(self.param_lambda),
                 float(self.param_gamma), np.asarray(self.stage_cost_weight, dtype=np.float64).tobytes(),
                 np.asarray(self.terminal_cost_weight, dtype=np.float64).tobytes(), float(self.param_exploration),
-                float(self.delta_t))
+                float(self.delta_t), float(self.l1), float(self.l2), self.arm)
 
     def _get_engine(self, key=None) -> RolloutEngine:
         key = self._engine_key() if key is None else key
@@ -134,14 +163,13 @@ class MPPIControllerForPathTracking:
             K_local, k_offset = shard_geometry(self.K, world, rank)
             device = self._device if self._device is not None else torch.cuda.current_device()
             # gamma is fixed at construction in the reference (control.py:45) while lambda is
-            # re-read per call; the engine takes (lambda, alpha), so carry gamma through alpha
-            alpha = self.param_alpha
-            if self.param_lambda * (1.0 - alpha) != self.param_gamma and self.param_lambda != 0:
-                alpha = 1.0 - self.param_gamma / self.param_lambda
+            # re-read per call: the engine takes gamma as given; the cost's kinematics follow self.l1/l2
+            arm = dataclasses.replace(self.arm, fk_l1=float(self.l1), fk_l2=float(self.l2))
             self._engine = RolloutEngine(
-                K_local, self.T, self.delta_t, self.param_lambda, alpha, self.Sigma,
-                self.stage_cost_weight, self.terminal_cost_weight, self.param_exploration, self.arm,
-                K_total=self.K, k_offset=k_offset, device=device, lanes_per_sample=self._lanes_per_sample)
+                K_local, self.T, self.delta_t, self.param_lambda, self.param_alpha, self.Sigma,
+                self.stage_cost_weight, self.terminal_cost_weight, self.param_exploration, arm,
+                K_total=self.K, k_offset=k_offset, device=device, lanes_per_sample=self._lanes_per_sample,
+                param_gamma=self.param_gamma)
             self._engine_built_for = key
             self._noise_dev = self._engine.new_noise()
             self._partial = self._engine.new_partial()
@@ -150,13 +178,44 @@ class MPPIControllerForPathTracking:
             if world > 1:
                 self._gathered = torch.empty(world * self._engine.partial_len, dtype=torch.float64,
                                              device=self._engine.device)
+            self._xmode = None
         return self._engine
+
+    def _multi_setup(self, eng: RolloutEngine, noise_check) -> None:
+        """First multi-GPU step of an engine (collective, every rank): check that the
+        ranks agree on the noise stream, then pick the exchange — the in-launch one
+        (distributed.attach_exchange) if its one-step self-check against the
+        all-gather + merge passes (distributed.check_exchange), else RCCL."""
+        pg = self.process_group
+        if not same_on_all_ranks((self.K, self.T, self.noise_source, self.seed, noise_check), pg):
+            raise RuntimeError("ranks disagree on the noise stream: every rank must seed np.random identically "
+                               "(and pass the same seed / K / T)")
+        mode = "rccl"
+        if self.exchange != "rccl":
+            ok = attach_exchange(eng, pg)
+            ok = ok and check_exchange(eng, self._noise_dev, self._partial, self._gathered, pg)
+            if not ok and self.exchange == "launch":
+                raise RuntimeError("the in-launch exchange failed its self-check (exchange='launch')")
+            mode = "launch" if ok else "rccl"
+        self._xmode = mode
+
+    def _multi_rollout(self, eng: RolloutEngine, S_out, fused: bool) -> None:
+        """control.py:81-118 over every rank's shard, the rows merged on every rank:
+        one launch with the in-launch exchange, or rollout + RCCL all-gather + merge
+        launch.  fused: the update of control.py:120-149 too, published for wait_outputs."""
+        if self._xmode == "launch":
+            eng.rollout(self._noise_dev, S_out=S_out, fused_update=fused, exchange=True, host_out=fused)
+            return
+        world, _ = self._shard()
+        eng.rollout(self._noise_dev, S_out=S_out, partial_out=self._partial)
+        exchange_partials(self._partial, self._gathered, self.process_group)
+        eng.merge(self._gathered, world, fused_update=fused, host_out=fused)
 
     # ------------------------------------------------------------ API
     def calc_control_input(self, observed_x: np.ndarray) -> Tuple[float, np.ndarray]:
         """calculate optimal control input (control.py:67-152)"""
         if (self.noise_source == "device" and not self.host_update and not self.visualze_sampled_trajs
-                and self.process_group is None and self.K >= 1):
+                and (self.process_group is None or self._xmode == "launch") and self.K >= 1):
             out = self._tick(observed_x)
             if out is not None:
                 return out
@@ -190,14 +249,16 @@ class MPPIControllerForPathTracking:
         if not self.host_update and world == 1 and not self.visualze_sampled_trajs:
             return self._dropin_step(eng, x0, window, u)
         eng.set_step_inputs(np.asarray(x0, dtype=np.float64), window, u)
+        if world > 1 and self._xmode is None:
+            check = float(epsilon[0, 0, 0] + epsilon[-1, -1, -1]) if epsilon is not None else None
+            self._multi_setup(eng, check)
         if not self.host_update:
             return self._fused_step(eng, x0, u, world)
+        S_out = self._S_dev if self.keep_costs else None
         if world == 1:
-            eng.rollout(self._noise_dev, S_out=self._S_dev if self.keep_costs else None)
+            eng.rollout(self._noise_dev, S_out=S_out)
         else:
-            eng.rollout(self._noise_dev, S_out=self._S_dev if self.keep_costs else None, partial_out=self._partial)
-            exchange_partials(self._partial, self._gathered, self.process_group)
-            eng.merge(self._gathered, world)
+            self._multi_rollout(eng, S_out, fused=False)
         w_epsilon = eng.weighted_noise()
         if self.keep_costs:
             self.last_S = self._S_dev.cpu().numpy()
@@ -255,7 +316,7 @@ class MPPIControllerForPathTracking:
         if self._noise_ready != (self.seed, self._step_count):
             eng.philox_noise(self.seed, self._step_count, out=self._noise_dev)
         self._step_count += 1
-        rc = eng.dropin_tick(self._step_count)
+        rc = eng.dropin_tick_launch(self._step_count)
         self.prev_waypoints_idx = int(self._idx_buf[0])
         if self.verbose:
             print(f"0     prev_idx = {int(self._idx_buf[1])}")
@@ -265,19 +326,13 @@ class MPPIControllerForPathTracking:
             self._step_count -= 1
             print("[ERROR] Reached the end of the reference path.")
             raise IndexError
+        sampled = np.zeros((self.K, self.T, self.dim_x))   # control.py:135, allocated while the launch runs
+        eng.dropin_tick_wait()
         self._noise_ready = (self.seed, self._step_count)
         if self.keep_costs:
             self.last_S = self._S_dev.cpu().numpy()
         traj = self._traj_buf.copy() if self._traj_buf is not None else np.zeros((self.T, self.dim_x))
-        return u[0], u, traj, self._zero_trajs()
-
-    def _zero_trajs(self) -> np.ndarray:
-        """sampled_traj_list when the sampled re-roll is off (control.py:135): all
-        zeros of shape (K, T, 4).  One read-only zero-stride view instead of a fresh
-        134 MB array per call at K = 65536 (writing into it raises)."""
-        if self._no_trajs is None or self._no_trajs.shape != (self.K, self.T, self.dim_x):
-            self._no_trajs = np.broadcast_to(np.zeros(()), (self.K, self.T, self.dim_x))
-        return self._no_trajs
+        return u[0], u, traj, sampled
 
     def _dropin_step(self, eng: RolloutEngine, x0, window, u: np.ndarray):
         """control.py:81-152 on one device in one native call (mppi_step_dropin):
@@ -296,7 +351,7 @@ class MPPIControllerForPathTracking:
             self.last_S = self._S_dev.cpu().numpy()
         u[:] = u_new                                       # the shifted nominal, in place (aliasing kept)
         optimal_traj = traj if traj is not None else np.zeros((self.T, self.dim_x))
-        return u[0], u, optimal_traj, self._zero_trajs()
+        return u[0], u, optimal_traj, np.zeros((self.K, self.T, self.dim_x))
 
     def _fused_step(self, eng: RolloutEngine, x0, u: np.ndarray, world: int):
         """control.py:81-152 with the update inside the launch (the multi-GPU merge
@@ -309,9 +364,7 @@ class MPPIControllerForPathTracking:
         if world == 1:
             eng.rollout(self._noise_dev, S_out=S_out, fused_update=True, host_out=True)
         else:
-            eng.rollout(self._noise_dev, S_out=S_out, partial_out=self._partial)
-            exchange_partials(self._partial, self._gathered, self.process_group)
-            eng.merge(self._gathered, world, fused_update=True, host_out=True)
+            self._multi_rollout(eng, S_out, fused=True)
         sampled_traj_list = np.zeros((self.K, self.T, self.dim_x))
         tr = None
         if self.visualze_sampled_trajs:
@@ -363,7 +416,7 @@ class MPPIControllerForPathTracking:
         y = self.l1 * np.sin(q1) + self.l2 * np.sin(q1 + q2)
         win = self.ref_path[prev_idx:(prev_idx + SEARCH_IDX_LEN)]
         d = ((x - win[:, 0]) ** 2 + (y - win[:, 1]) ** 2) * 100
-        nearest_idx = int(np.argmin(d)) + prev_idx
+        nearest_idx = first_min_index(d) + prev_idx
         ref_x = self.ref_path[nearest_idx, 0]
         ref_y = self.ref_path[nearest_idx, 1]
         ref_dq1 = self.ref_path[nearest_idx, 2]
@@ -390,3 +443,4 @@ class MPPIControllerForPathTracking:
         self._noise_ready = None       # the next engine's noise buffer is fresh: draw again
         self._engine_built_for = None
         self._bound = None
+        self._xmode = None

@@ -788,6 +788,8 @@ struct mppi_ctx {
     bool bound = false;
     std::chrono::steady_clock::time_point tick_t0{};   // start of the current mppi_dropin_tick (phase times)
     bool in_tick = false;
+    bool tick_launched = false;     // mppi_dropin_tick_launch done, mppi_dropin_tick_wait pending
+    std::chrono::steady_clock::time_point step_t0{};   // start of the current drop-in step (phase times)
     double sig_inv[4];
     unsigned long long* d_dbg = nullptr;  // diagnostic stamp buffer (MPPI_STAMPS builds)
     // node-level exchange (mppi_exchange_*): inbox, this rank's row, epoch, peer mappings
@@ -929,7 +931,8 @@ int mppi_ctx_create(const mppi_config* cfg, int device, void* stream, mppi_ctx**
     }
     k.lambda = cfg->param_lambda;
     k.inv_lambda = 1.0 / cfg->param_lambda;
-    k.gamma = cfg->param_lambda * (1.0 - cfg->param_alpha);  // control.py:45
+    // control.py:45 fixes gamma at construction; the caller passes it as given
+    k.gamma = isnan(cfg->param_gamma) ? cfg->param_lambda * (1.0 - cfg->param_alpha) : cfg->param_gamma;
     for (int i = 0; i < 4; ++i) k.sig_inv[i] = c->sig_inv[i];
 
     auto cleanup_fail = [&](int rc) {
@@ -1390,19 +1393,23 @@ int mppi_wait_outputs(mppi_ctx* c, const double* x0, double* u_out, double* traj
     return MPPI_OK;
 }
 
-int mppi_step_dropin(mppi_ctx* c, const double* x0, const double* window, int W, const double* u,
-                     const float* noise_dev, double* S_dev, float* next_noise_dev, unsigned long long seed,
-                     unsigned long long next_step, double* u_out, double* traj_out) {
-    if (!c || !x0 || !window || !noise_dev || !u_out) return fail(MPPI_E_ARG, "null argument");
+}  // extern "C"
+
+namespace {
+// The launch half of mppi_step_dropin: stage, fused launch, next noise queued.
+int dropin_launch(mppi_ctx* c, const double* x0, const double* window, int W, const double* u, const float* noise_dev,
+                  double* S_dev, float* next_noise_dev, unsigned long long seed, unsigned long long next_step) {
+    if (!c || !x0 || !window || !noise_dev) return fail(MPPI_E_ARG, "null argument");
     if (c->cfg.T < 5) return fail(MPPI_E_ARG, "device median filter needs T >= 5 (use the host update)");
-    if (c->xd.world > 1) return fail(MPPI_E_ARG, "mppi_step_dropin is the single-device path");
     using clk = std::chrono::steady_clock;
     const auto t0 = c->in_tick ? c->tick_t0 : clk::now();   // a tick's phases include its waypoint update
     c->in_tick = false;
+    c->step_t0 = t0;
     auto mark = [&](int i) { c->dropin_us[i] = std::chrono::duration<double, std::micro>(clk::now() - t0).count(); };
     if (int rc = stage_inputs(c, x0, window, W, u, true)) return rc;
     mark(0);
-    const unsigned fl = MPPI_FLAG_FUSED_UPDATE | MPPI_FLAG_HOST_OUT;
+    // with an exchange attached the launch also trades rows with the other ranks
+    const unsigned fl = MPPI_FLAG_FUSED_UPDATE | MPPI_FLAG_HOST_OUT | (c->xd.world >= 1 ? MPPI_FLAG_EXCHANGE : 0u);
     if (int rc = launch_rollout(c, noise_dev, S_dev, nullptr, fl, next_host_out(c, fl))) return rc;
     mark(1);
     // the next step's noise, queued behind this step's rollout (stream order: the
@@ -1411,11 +1418,32 @@ int mppi_step_dropin(mppi_ctx* c, const double* x0, const double* window, int W,
     if (next_noise_dev)
         if (int rc = mppi_noise_philox(c, seed, next_step, next_noise_dev)) return rc;
     mark(2);
+    return MPPI_OK;
+}
+
+// The wait half: the launch's published outputs, then the host trajectory.
+int dropin_finish(mppi_ctx* c, const double* x0, double* u_out, double* traj_out) {
+    if (!u_out) return fail(MPPI_E_ARG, "null argument");
+    using clk = std::chrono::steady_clock;
+    auto mark = [&](int i) {
+        c->dropin_us[i] = std::chrono::duration<double, std::micro>(clk::now() - c->step_t0).count();
+    };
     if (int rc = wait_host_out(c)) return rc;
     mark(3);
     if (int rc = mppi_wait_outputs(c, x0, u_out, traj_out)) return rc;   // already published: copies + trajectory
     mark(4);
     return MPPI_OK;
+}
+}  // namespace
+
+extern "C" {
+
+int mppi_step_dropin(mppi_ctx* c, const double* x0, const double* window, int W, const double* u,
+                     const float* noise_dev, double* S_dev, float* next_noise_dev, unsigned long long seed,
+                     unsigned long long next_step, double* u_out, double* traj_out) {
+    if (!u_out) return fail(MPPI_E_ARG, "null argument");
+    if (int rc = dropin_launch(c, x0, window, W, u, noise_dev, S_dev, next_noise_dev, seed, next_step)) return rc;
+    return dropin_finish(c, x0, u_out, traj_out);
 }
 
 int mppi_dropin_bind(mppi_ctx* c, const mppi_dropin_binding* b) {
@@ -1428,8 +1456,21 @@ int mppi_dropin_bind(mppi_ctx* c, const mppi_dropin_binding* b) {
 }
 
 int mppi_dropin_tick(mppi_ctx* c, unsigned long long next_step) {
+    if (int rc = mppi_dropin_tick_launch(c, next_step)) return rc;
+    return mppi_dropin_tick_wait(c);
+}
+
+int mppi_dropin_tick_wait(mppi_ctx* c) {
+    if (!c) return fail(MPPI_E_ARG, "null context");
+    if (!c->tick_launched) return fail(MPPI_E_ARG, "mppi_dropin_tick_wait without a launched tick");
+    c->tick_launched = false;
+    return dropin_finish(c, c->bind.x0, c->bind.u, c->bind.traj);
+}
+
+int mppi_dropin_tick_launch(mppi_ctx* c, unsigned long long next_step) {
     if (!c) return fail(MPPI_E_ARG, "null context");
     if (!c->bound) return fail(MPPI_E_ARG, "mppi_dropin_tick before mppi_dropin_bind");
+    if (c->tick_launched) return fail(MPPI_E_ARG, "a launched tick was not waited for (mppi_dropin_tick_wait)");
     const mppi_dropin_binding& b = c->bind;
     c->tick_t0 = std::chrono::steady_clock::now();
     c->in_tick = true;
@@ -1446,14 +1487,10 @@ int mppi_dropin_tick(mppi_ctx* c, unsigned long long next_step) {
     const int n = (int)std::min<long long>(MPPI_SEARCH_LEN, b.rows - prev);
     int best = 0;
     double dmin = 0.0;
-    for (int j = 0; j < n; ++j) {   // np.argmin: the first NaN if there is one, else the first minimum
+    for (int j = 0; j < n; ++j) {   // min(d) then d.index(min_d) (control.py:213-215): d[0], replaced on a strict '<'
         const double* r = b.path + (prev + j) * (long long)b.stride;
         const double dx = x - r[0], dy = y - r[1];
         const double d = (dx * dx + dy * dy) * 100;
-        if (d != d) {
-            best = j;
-            break;
-        }
         if (j == 0 || d < dmin) {
             dmin = d;
             best = j;
@@ -1470,8 +1507,9 @@ int mppi_dropin_tick(mppi_ctx* c, unsigned long long next_step) {
     const int W = (int)std::min<long long>(MPPI_SEARCH_LEN, b.rows - idx);
     double win[4 * MPPI_SEARCH_LEN];
     for (int j = 0; j < W; ++j) memcpy(win + 4 * j, b.path + (idx + j) * (long long)b.stride, 4 * sizeof(double));
-    return mppi_step_dropin(c, b.x0, win, W, b.u, b.noise_dev, b.S_dev, b.next_noise_dev, b.seed, next_step, b.u,
-                            b.traj);
+    const int rc = dropin_launch(c, b.x0, win, W, b.u, b.noise_dev, b.S_dev, b.next_noise_dev, b.seed, next_step);
+    c->tick_launched = rc == MPPI_OK;
+    return rc;
 }
 
 int mppi_noise_philox(mppi_ctx* c, unsigned long long seed, unsigned long long step, float* out_dev) {

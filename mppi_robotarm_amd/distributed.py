@@ -8,7 +8,10 @@ is ONE all-gather of those 2 + 2T doubles (1 KB at T = 64) over the process
 group; every rank then merges the gathered rows on device in rank order
 (deterministic, identical on all ranks) and continues with the same w_eps.
 An all-gather (not an all-reduce) keeps the merge exact: rows carry their own
-rho, so no prior MIN collective is needed.
+rho, so no prior MIN collective is needed.  The preferred form does without
+the collective call: attach_exchange maps every rank's inbox once, and each
+launch then trades the rows itself (include/mppi_rocm.h mppi_exchange_*);
+check_exchange is its one-step self-check against the all-gather.
 """
 from __future__ import annotations
 
@@ -115,6 +118,13 @@ def check_exchange(engine, noise, partial, gathered, group=None) -> bool:
     except Exception:  # noqa: BLE001
         ok = False
     return _all_ranks(ok, group)
+
+
+def same_on_all_ranks(obj, group=None) -> bool:
+    """True on every rank iff every rank passed an equal (picklable) `obj`."""
+    objs = [None] * dist.get_world_size(group)
+    dist.all_gather_object(objs, obj, group=group)
+    return all(o == objs[0] for o in objs)
 
 
 def _all_ranks(ok: bool, group=None) -> bool:

@@ -34,7 +34,8 @@ class RolloutEngine:
     def __init__(self, K_local: int, T: int, delta_t: float, param_lambda: float, param_alpha: float,
                  sigma, stage_cost_weight, terminal_cost_weight, param_exploration: float = 0.0,
                  arm: ArmParams = ArmParams(), K_total: int | None = None, k_offset: int = 0,
-                 device: int | torch.device | None = None, lanes_per_sample: int = 0):
+                 device: int | torch.device | None = None, lanes_per_sample: int = 0,
+                 param_gamma: float | None = None):
         self._lib = N.load()
         if device is None:
             device = torch.cuda.current_device()
@@ -57,6 +58,8 @@ class RolloutEngine:
         for f in ("m1", "m2", "l1", "l2", "lc1", "lc2", "g", "fk_l1", "fk_l2"):
             setattr(cfg.arm, f, float(getattr(arm, f)))
         cfg.lanes_per_sample = int(lanes_per_sample)
+        # gamma as given (control.py:45 fixes it at construction); None: lambda (1 - alpha)
+        cfg.param_gamma = float("nan") if param_gamma is None else float(param_gamma)
         self.sigma = sig
         self.param_lambda = float(param_lambda)
         with torch.cuda.device(self.device):
@@ -302,6 +305,19 @@ class RolloutEngine:
         if rc != N.MPPI_OK and rc != N.MPPI_E_PATH_END:
             N.check(rc, "mppi_dropin_tick")
         return rc
+
+    def dropin_tick_launch(self, next_step: int) -> int:
+        """The launch half of dropin_tick (mppi_dropin_tick_launch): MPPI_OK or
+        MPPI_E_PATH_END (nothing launched); dropin_tick_wait() must follow an OK."""
+        self._sync_stream()
+        rc = self._lib.mppi_dropin_tick_launch(self._ctx, next_step)
+        if rc != N.MPPI_OK and rc != N.MPPI_E_PATH_END:
+            N.check(rc, "mppi_dropin_tick_launch")
+        return rc
+
+    def dropin_tick_wait(self) -> None:
+        """The wait half (mppi_dropin_tick_wait): u and traj of the binding written."""
+        N.check(self._lib.mppi_dropin_tick_wait(self._ctx), "mppi_dropin_tick_wait")
 
     def dropin_times(self) -> np.ndarray:
         """Diagnostics: phase ends (us) of the last step_dropin (mppi_debug_dropin_times)."""

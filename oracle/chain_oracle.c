@@ -123,7 +123,7 @@ static double chain_cost(const double *x, const double *win, int W, const double
     for (int j = 0; j < W; ++j) {
         const double dx = px - win[4 * j], dy = py - win[4 * j + 1];
         const double d = (dx * dx + dy * dy) * 100;
-        if (d < dmin) { dmin = d; jmin = j; }
+        if (j == 0 || d < dmin) { dmin = d; jmin = j; }   /* control.py:213-215, as mppi_oracle.c */
     }
     const double *r = win + 4 * jmin;
     const double ex = px - r[0], ey = py - r[1], e1 = x[M->n] - r[2], e2 = x[M->n + 1] - r[3];

@@ -122,10 +122,10 @@ def chain_fk(q, P: ChainParams):
 
 
 def nearest_waypoint_xy(x, y, ref_path, prev_idx):
-    """control.py:200-232 on an end-effector position (first-occurrence argmin)."""
+    """control.py:200-232 on an end-effector position (d.index(min(d)), O.first_min_index)."""
     win = ref_path[prev_idx:prev_idx + O.SEARCH_IDX_LEN]
     d = ((np.asarray(x)[..., None] - win[:, 0]) ** 2 + (np.asarray(y)[..., None] - win[:, 1]) ** 2) * 100
-    idx = np.argmin(d, axis=-1) + prev_idx
+    idx = O.first_min_index(d) + prev_idx
     return idx, ref_path[idx, 0], ref_path[idx, 1], ref_path[idx, 2], ref_path[idx, 3]
 
 

@@ -66,7 +66,7 @@ static inline double oracle_cost(const double x[4], const double *win, int W, co
     for (int j = 0; j < W; ++j) {
         const double dx = px - win[4 * j], dy = py - win[4 * j + 1];
         const double d = (dx * dx + dy * dy) * 100;
-        if (d < dmin) { dmin = d; jmin = j; } /* first occurrence, list.index(min) */
+        if (j == 0 || d < dmin) { dmin = d; jmin = j; } /* min(d): d[0], replaced on a strict <; list.index */
     }
     const double *r = win + 4 * jmin;
     const double ex = px - r[0], ey = py - r[1], e1 = x[2] - r[2], e2 = x[3] - r[3];

@@ -102,11 +102,24 @@ def forward_kinematics(q, p: ArmParams = ArmParams()):
     return x1, y1, x2, y2
 
 
+def first_min_index(d):
+    """``d.index(min(d))`` (control.py:213-215) along the last axis.  Python's
+    min() keeps d[0] and replaces it only on a strict '<': a NaN at j > 0 is
+    never chosen, a NaN at j = 0 always is (np.argmin returns the first NaN)."""
+    j = np.argmin(d, axis=-1)
+    nan = np.isnan(np.take_along_axis(d, np.asarray(j)[..., None], axis=-1)[..., 0])
+    if np.any(nan):
+        alt = np.argmin(np.where(np.isnan(d), np.inf, d), axis=-1)   # the first minimum of the numbers
+        alt = np.where(np.isnan(d[..., 0]), 0, alt)
+        j = np.where(nan, alt, j)
+    return j
+
+
 def nearest_waypoint(q1, q2, ref_path, prev_idx, p: ArmParams):
     """``_get_nearest_waypoint`` (control.py:200-232) vectorised over samples.
 
     Window ``ref_path[prev:prev+30]`` (slice-truncated at the path end),
-    first-occurrence argmin of ``((x-rx)^2 + (y-ry)^2) * 100``.
+    ``d.index(min(d))`` of ``((x-rx)^2 + (y-ry)^2) * 100`` (control.py:212-215).
     Returns (nearest_idx, ref_x, ref_y, ref_dq1, ref_dq2).
     """
     x = p.fk_l1 * np.cos(q1) + p.fk_l2 * np.cos(q1 + q2)
@@ -115,7 +128,7 @@ def nearest_waypoint(q1, q2, ref_path, prev_idx, p: ArmParams):
     dx = np.asarray(x)[..., None] - win[:, 0]
     dy = np.asarray(y)[..., None] - win[:, 1]
     d = (dx ** 2 + dy ** 2) * 100
-    j = np.argmin(d, axis=-1)
+    j = first_min_index(d)
     idx = j + prev_idx
     return idx, ref_path[idx, 0], ref_path[idx, 1], ref_path[idx, 2], ref_path[idx, 3]
 

@@ -26,6 +26,17 @@ STEP_FIXTURES = sorted(os.path.basename(f)[5:-4] for f in glob.glob(os.path.join
 LOOP_FIXTURES = sorted(os.path.basename(f)[5:-4] for f in glob.glob(os.path.join(GOLDEN, "loop_*.npz")))
 
 
+def record(kind, **vals):
+    """Append one achieved-accuracy record (JSON line) to $MPPI_PARITY_RECORD when
+    set: the GPU runs that DESIGN.md's parity tables quote write them there."""
+    path = os.environ.get("MPPI_PARITY_RECORD")
+    if path:
+        import json
+        with open(path, "a") as f:
+            f.write(json.dumps({"kind": kind, **{k: (float(v) if isinstance(v, (float, np.floating)) else v)
+                                                 for k, v in vals.items()}}) + "\n")
+
+
 def load_step(name):
     return dict(np.load(os.path.join(GOLDEN, f"step_{name}.npz")))
 

@@ -45,10 +45,10 @@ def test_struct_layout_matches_header(tmp_path):
 #include <stdio.h>
 #include "mppi_rocm.h"
 int main(void) {
-  printf("%zu %zu %zu %zu %zu %zu %zu %zu\n", sizeof(mppi_config), sizeof(mppi_arm_params),
+  printf("%zu %zu %zu %zu %zu %zu %zu %zu %zu\n", sizeof(mppi_config), sizeof(mppi_arm_params),
          offsetof(mppi_config, delta_t), offsetof(mppi_config, sigma), offsetof(mppi_config, stage_cost_weight),
          offsetof(mppi_config, terminal_cost_weight), offsetof(mppi_config, arm),
-         offsetof(mppi_config, lanes_per_sample));
+         offsetof(mppi_config, lanes_per_sample), offsetof(mppi_config, param_gamma));
   return 0;
 }
 ''')
@@ -58,7 +58,7 @@ int main(void) {
     Cc = N.ConfigC
     assert vals == [C.sizeof(Cc), C.sizeof(N.ArmParamsC), Cc.delta_t.offset, Cc.sigma.offset,
                     Cc.stage_cost_weight.offset, Cc.terminal_cost_weight.offset, Cc.arm.offset,
-                    Cc.lanes_per_sample.offset]
+                    Cc.lanes_per_sample.offset, Cc.param_gamma.offset]
 
 
 def test_chain_struct_layout_matches_header(tmp_path):

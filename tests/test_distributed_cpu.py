@@ -244,3 +244,37 @@ def test_gather_trajectories_uneven_shards(tmp_path, K, world):
     ref = np.arange(K * T * 4, dtype=np.float32).reshape(K, T, 4).astype(np.float64)
     for r in range(world):
         assert np.array_equal(np.load(f"{out}.{r}.npy"), ref)
+
+
+def _setup_worker(rank, world, port, seeds_differ, out_path):
+    import sys
+    sys.path.insert(0, ROOT)
+    from mppi_robotarm_amd.controller import MPPIControllerForPathTracking
+    from mppi_robotarm_amd.distributed import same_on_all_ranks
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        res = [int(same_on_all_ranks(("k", 3), None)), int(same_on_all_ranks(("k", rank), None))]
+        c = MPPIControllerForPathTracking(ref_path=np.zeros((40, 4)), verbose=False, noise="device",
+                                          seed=rank if seeds_differ else 7, process_group=dist.group.WORLD,
+                                          exchange="rccl")
+        try:
+            c._multi_setup(None, None)          # the engine is not touched on the RCCL path
+            res.append(1 if c._xmode == "rccl" else -1)
+        except RuntimeError:
+            res.append(0)
+        np.save(f"{out_path}.{rank}.npy", np.array(res))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("seeds_differ", [False, True])
+def test_multi_gpu_controller_checks_the_noise_stream(tmp_path, seeds_differ):
+    """The multi-GPU drop-in's first step: ranks that would draw different noise
+    streams stop on every rank (RuntimeError), instead of merging inconsistent shards."""
+    world = 2
+    out = str(tmp_path / "setup")
+    mp.start_processes(_setup_worker, args=(world, _free_port(), seeds_differ, out), nprocs=world, join=True,
+                       start_method="spawn")
+    for r in range(world):
+        assert np.load(f"{out}.{r}.npy").tolist() == [1, 0, 0 if seeds_differ else 1]

@@ -28,7 +28,7 @@ pytestmark = pytest.mark.gpu
 
 import chain_oracle as CO  # noqa: E402
 import coracle  # noqa: E402
-from conftest import STEP_FIXTURES, load_step  # noqa: E402
+from conftest import STEP_FIXTURES, load_step, record  # noqa: E402
 
 U_TOL = 1e-4
 S_TOL = 5e-5
@@ -108,6 +108,8 @@ def test_chain_n7_against_c_oracle(K, T, lam, s99, paths):
     rel = np.abs(S - Sr) / np.abs(Sr)
     print(f"chain n=7 K={K} T={T} lam={lam:g}: S rel-err p50 {np.median(rel):.2e} p99 {np.percentile(rel, 99):.2e} "
           f"max {rel.max():.2e}, frac > 1e-3 {np.mean(rel > 1e-3):.2e}, w_eps rel-err {_urel(w, wr):.2e}")
+    record("chain_n7", K=K, T=T, lam=lam, S_p50=float(np.median(rel)), S_p99=float(np.percentile(rel, 99)),
+           S_max=float(rel.max()), frac_above_1e3=float(np.mean(rel > 1e-3)), w_eps_rel_err=_urel(w, wr))
     assert np.all(np.isfinite(S))
     assert int(np.argmin(S)) == int(np.argmin(Sr))
     assert float(np.percentile(rel, 99)) < s99

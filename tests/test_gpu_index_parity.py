@@ -26,7 +26,7 @@ torch = pytest.importorskip("torch")
 pytestmark = pytest.mark.gpu
 
 import mppi_oracle as O  # noqa: E402
-from conftest import load_step  # noqa: E402
+from conftest import load_step, record  # noqa: E402
 
 RUNPY = dict(param_exploration=0.0, param_lambda=100.0, param_alpha=0.98, sigma=np.eye(2) * 20.0,
              stage_cost_weight=np.array([0.5, 0.5, 5.0, 5.0]),
@@ -144,6 +144,7 @@ def test_fixture_indices(name, paths):
                                       float(g["param_exploration"]))
     print(f"{name}: K={K} T={T} mismatches vs fp64 oracle {rate:.3e}, search ties {ties:.3e}, "
           f"worst gap / bound {worst:.3f}")
+    record("index_parity", case=name, K=K, T=T, mismatch_rate=rate, search_ties=ties, worst_gap_over_bound=worst)
     eng.close()
 
 
@@ -168,5 +169,7 @@ def test_c3_window_indices(paths, converged):
     rate, ties, worst = check_indices(slot, pos, X0, u, eps_kt, win, 0.006)
     print(f"c3 window (converged={converged}): mismatches vs fp64 oracle {rate:.3e} "
           f"({int(round(rate * K * T))} of {K * T}), search ties {ties:.3e}, worst gap / bound {worst:.3f}")
+    record("index_parity", case=f"c3_{'converged' if converged else 'initial'}", K=K, T=T, mismatch_rate=rate,
+           search_ties=ties, worst_gap_over_bound=worst)
     assert rate < 1e-2
     eng.close()

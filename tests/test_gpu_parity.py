@@ -17,7 +17,7 @@ pytestmark = pytest.mark.gpu
 
 import coracle  # noqa: E402
 import mppi_oracle as O  # noqa: E402
-from conftest import LOOP_FIXTURES, STEP_FIXTURES, ctor_kwargs, load_loop, load_step  # noqa: E402
+from conftest import LOOP_FIXTURES, STEP_FIXTURES, ctor_kwargs, load_loop, load_step, record  # noqa: E402
 
 U_TOL = 1e-4
 S_TOL = 5e-5
@@ -265,10 +265,17 @@ def test_shard_invariance_and_merge(paths):
         e.close()
 
 
-def test_fused_device_update_matches_host_update(paths):
+@pytest.mark.parametrize("T,lam", [(5, 100.0), (6, 100.0), (7, 1.0e4), (8, 100.0), (9, 1.0e4), (10, 100.0),
+                                   (12, 1.0e4), (15, 100.0), (16, 1.0e4), (40, 100.0)])
+def test_fused_device_update_matches_host_update(T, lam, paths):
+    """The fused update's median (a 29-comparator network over the reflected
+    window [t-5, t+4]) and u += w_eps + shift (control.py:120-149) against
+    scipy.ndimage.median_filter(size=10, mode='reflect') and the fp64 add on the
+    host: bit-equal, including the short horizons T = 5..15 where the 10-wide
+    window reflects at both ends for most rows (control.py:319-327)."""
     from scipy.ndimage import median_filter
-    K, T = 8192, 40
-    eng = _engine(K, T)
+    K = 8192
+    eng = _engine(K, T, param_lambda=lam)
     u = np.array([[10.0, -2.0]] * T) + np.random.default_rng(3).normal(0, 0.3, (T, 2))
     eng.set_step_inputs(X0, _window(paths), u)
     for step in range(3):
@@ -279,7 +286,7 @@ def test_fused_device_update_matches_host_update(paths):
         un = u + filt
         expect = np.concatenate([un[1:], un[-1:]], 0)
         got = eng.nominal()
-        np.testing.assert_allclose(got, expect, rtol=1e-13, atol=1e-13)
+        np.testing.assert_array_equal(got, expect)
         u = got
     eng.close()
 
@@ -560,14 +567,16 @@ def test_config4_eight_virtual_shards(lam, paths, monkeypatch):
         assert w.sum() ** 2 / (w ** 2).sum() > 100
         assert len({int(k) // Kl for k in np.argsort(ref_S)[:64]}) == G
     print(f"config 4 lam={lam}: S max rel-err {float(np.max(rel)):.2e}, w_eps rel-err {_urel(w_sh, ref_weps):.2e}")
+    record("config4", lam=lam, S_max_rel_err=float(np.max(rel)), S_p99_rel_err=float(np.percentile(rel, 99)),
+           w_eps_rel_err=_urel(w_sh, ref_weps))
     for e in engs + [full]:
         e.close()
 
 
 def _runpy_ctrl(paths, K=4096, T=32, **kw):
     from mppi_robotarm_amd.controller import MPPIControllerForPathTracking
-    return MPPIControllerForPathTracking(delta_t=0.006, ref_path=paths["xydq_circle"], horizon_step_T=T,
-                                         number_of_samples_K=K, verbose=False, **{**RUNPY, **kw})
+    return MPPIControllerForPathTracking(delta_t=0.006, horizon_step_T=T, number_of_samples_K=K, verbose=False,
+                                         **{"ref_path": paths["xydq_circle"], **RUNPY, **kw})
 
 
 def test_device_noise_ticks_on_alternating_streams(paths):
@@ -676,6 +685,26 @@ def test_bound_tick_equals_general_dropin(paths):
     assert fast._bound is not None                  # the fast controller really took the tick
     fast.close()
     slow.close()
+
+
+def test_tick_nearest_waypoint_follows_python_min_on_nan_rows(paths):
+    """The native tick's waypoint update (mppi_dropin_tick) takes d.index(min(d))
+    like the reference (control.py:212-215) and the host path: a NaN row after
+    the nearest one is never chosen, a NaN in the window's first row always is."""
+    from mppi_robotarm_amd.controller import MPPIControllerForPathTracking
+    base = paths["xydq_circle"][:120].copy()
+    c = _runpy_ctrl(paths, K=1024, T=16, noise="device", seed=3, ref_path=base)
+    c.calc_control_input(X0)                        # builds the engine (general path)
+    host = MPPIControllerForPathTracking(ref_path=base, verbose=False)
+    host.prev_waypoints_idx = c.prev_waypoints_idx
+    want = host._get_nearest_waypoint(X0[0], X0[1])[0]
+    base[want + 1, :2] = np.nan
+    c.calc_control_input(X0)
+    assert c._bound is not None and c.prev_waypoints_idx == want
+    base[want, :2] = np.nan                         # the window's first row
+    c.calc_control_input(X0)
+    assert c.prev_waypoints_idx == want
+    c.close()
 
 
 def _random_cases(n=24, seed=2024):

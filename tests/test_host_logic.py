@@ -204,3 +204,37 @@ def test_bench_launches_ranks_itself(monkeypatch):
 def test_bench_host_cores_is_the_affinity_mask():
     import bench
     assert bench.host_cores() == len(os.sched_getaffinity(0))
+
+
+@pytest.mark.parametrize("d", [[3.0, 1.0, 2.0, 1.0], [3.0, np.nan, 1.0, 1.0], [np.nan, 2.0, 1.0],
+                               [2.0, np.nan, np.nan], [np.nan, np.nan], [1.0, 1.0, np.nan, 0.5],
+                               [np.inf, np.nan, np.inf]])
+def test_nearest_waypoint_nan_rule_is_python_min(d):
+    """control.py:212-215 builds a list and takes d.index(min(d)): min() keeps d[0]
+    and replaces it only on a strict '<', so a NaN at j > 0 is never chosen and a
+    NaN at j = 0 always is — unlike np.argmin (first NaN).  Host drop-in, NumPy
+    oracle (vectorised) and the chain oracle all follow it."""
+    import chain_oracle as CO
+    from mppi_robotarm_amd.controller import first_min_index
+    lst = [np.float64(v) for v in d]
+    want = lst.index(min(lst))
+    arr = np.array(d)
+    assert first_min_index(arr) == want
+    assert int(O.first_min_index(arr)) == want
+    assert O.first_min_index(np.stack([arr, arr[::-1]])).tolist() == [want, [*lst[::-1]].index(min(lst[::-1]))]
+    path = np.zeros((len(d), 4))
+    path[:len(d), 0] = np.sqrt(np.where(np.isnan(arr), np.nan, arr) / 100.0)   # (x - rx)^2 * 100 == d at x = 0
+    idx = CO.nearest_waypoint_xy(0.0, 0.0, path, 0)[0]
+    assert int(idx) == want
+
+
+def test_host_nearest_waypoint_skips_nan_rows(paths):
+    """The drop-in's host update (control.py:200-232) on a ref_path with NaN rows."""
+    path = paths["xydq_circle"].copy()
+    c = MPPIControllerForPathTracking(ref_path=path, verbose=False)
+    x0 = np.array([1.152198236517471885, -1.266101672070702344, 0.0, 0.0])
+    want = c._get_nearest_waypoint(x0[0], x0[1])[0]
+    path[want + 1] = np.nan                     # a NaN after the nearest row: never chosen
+    assert c._get_nearest_waypoint(x0[0], x0[1])[0] == want
+    path[0] = np.nan                            # a NaN in row 0 of the window: chosen
+    assert c._get_nearest_waypoint(x0[0], x0[1])[0] == 0
