@@ -909,6 +909,7 @@ __device__ __forceinline__ double median_at(const SM& sm, int t, int d, int T, i
 // ------------------------------------------------------------------ Philox
 
 // Philox4x32-10 (Salmon et al., SC'11).
+#ifdef MPPI_PHILOX_LIB
 __device__ __forceinline__ uint4 philox4x32_10(uint4 ctr, uint2 key) {
 #pragma unroll
     for (int r = 0; r < 10; ++r) {
@@ -930,6 +931,44 @@ __device__ __forceinline__ float2 box_muller(unsigned a, unsigned b) {
     sincospif(2.0f * u1, &s, &c);
     return make_float2(r * c, r * s);
 }
+#else
+// Each round's two 32 x 32 -> 64-bit products as one v_mad_u64_u32 apiece (the
+// 64-bit product of zero-extended words, which the compiler emits as one), not a
+// v_mul_lo_u32 + v_mul_hi_u32 pair: half the quarter-rate multiplies.  The round's two three-way XORs (hi ^ word ^ key)
+// are one v_bitop3_b32 each (truth table 0x96), the key word from an SGPR
+// (it must be wave-uniform: the "s" constraint takes lane 0's value).
+__device__ __forceinline__ unsigned long long mul_wide(unsigned a, unsigned m) {
+    return (unsigned long long)a * m;
+}
+__device__ __forceinline__ unsigned xor3(unsigned a, unsigned b, unsigned k) {
+    unsigned r;
+    asm("v_bitop3_b32 %0, %1, %2, %3 bitop3:0x96" : "=v"(r) : "v"(a), "v"(b), "s"(k));
+    return r;
+}
+__device__ __forceinline__ uint4 philox4x32_10(uint4 ctr, uint2 key) {
+#pragma unroll
+    for (int r = 0; r < 10; ++r) {
+        const unsigned long long p0 = mul_wide(ctr.x, 0xD2511F53u);
+        const unsigned long long p1 = mul_wide(ctr.z, 0xCD9E8D57u);
+        ctr = make_uint4(xor3((unsigned)(p1 >> 32), ctr.y, key.x), (unsigned)p1,
+                         xor3((unsigned)(p0 >> 32), ctr.w, key.y), (unsigned)p0);
+        key.x += 0x9E3779B9u;
+        key.y += 0xBB67AE85u;
+    }
+    return ctr;
+}
+
+// Two standard normals from two 32-bit uniforms (Box-Muller) on the hardware
+// transcendentals: v_log_f32 (log2), v_sqrt_f32, and v_sin_f32 / v_cos_f32, whose
+// input is in revolutions — exactly u1, so no 2 pi scaling and no range
+// reduction.  u0 lies in [2^-32, 1], a normal float: no denormal path.
+__device__ __forceinline__ float2 box_muller(unsigned a, unsigned b) {
+    const float inv = 2.3283064365386963e-10f;  // 2^-32
+    const float u0 = fminf(((float)a + 1.0f) * inv, 1.0f), u1 = (float)b * inv;
+    const float r = __builtin_amdgcn_sqrtf(-1.3862943611198906f * __builtin_amdgcn_logf(u0));   // -2 ln 2 log2 u0
+    return make_float2(r * __builtin_amdgcn_cosf(u1), r * __builtin_amdgcn_sinf(u1));
+}
+#endif
 
 }  // namespace mppi
 

@@ -13,8 +13,8 @@ word feeds which (t, k, d) element, for any shard offset, odd T and ragged K.
   against Random123's known-answer vectors in tests/test_philox_ref.py.
 * ``box_muller``: z = sqrt(-2 ln u0) (cos 2 pi u1, sin 2 pi u1) with the
   device's fp32 uniforms u0 = (a + 1) 2^-32, u1 = b 2^-32, evaluated in fp64
-  (the device uses fp32 logf / sincospif: agreement to ~1e-6 relative, far
-  below what a wrong mapping would give).
+  (the device uses the fp32 hardware log2 / sqrt / sin / cos: agreement to
+  ~1e-6 relative, far below what a wrong mapping would give).
 """
 from __future__ import annotations
 

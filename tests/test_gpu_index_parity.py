@@ -14,7 +14,7 @@ rollout's own dynamics and search code on the same inputs:
       (SEARCH_TOL: 2^-16 of the key scale, the 5-bit packing plus the fp32 key
       rounding, plus the fp32 rounding of the window coordinates);
   (b) against the fp64 oracle's indices on its fp64 trajectory: the mismatch
-      rate is reported, and every mismatch is a near-tie at the oracle's
+      rate is recorded and bounded, and every mismatch is a near-tie at the oracle's
       position — its gap is within what the fp32/fp64 position drift |dp| can
       move (|f(p) - f(p')| <= |dp| (|p - r| + |p' - r|) for f = |p - r|^2) plus
       the search tolerance of (a).
@@ -145,6 +145,8 @@ def test_fixture_indices(name, paths):
     print(f"{name}: K={K} T={T} mismatches vs fp64 oracle {rate:.3e}, search ties {ties:.3e}, "
           f"worst gap / bound {worst:.3f}")
     record("index_parity", case=name, K=K, T=T, mismatch_rate=rate, search_ties=ties, worst_gap_over_bound=worst)
+    # achieved on MI355X (profiles/r11/parity_records.jsonl): no mismatch on any fixture step
+    assert rate == 0.0
     eng.close()
 
 
@@ -171,5 +173,7 @@ def test_c3_window_indices(paths, converged):
           f"({int(round(rate * K * T))} of {K * T}), search ties {ties:.3e}, worst gap / bound {worst:.3f}")
     record("index_parity", case=f"c3_{'converged' if converged else 'initial'}", K=K, T=T, mismatch_rate=rate,
            search_ties=ties, worst_gap_over_bound=worst)
-    assert rate < 1e-2
+    # achieved on MI355X (profiles/r11/parity_records.jsonl): 0 of 262144 from the initial nominal,
+    # 46 of 262144 (1.75e-4) converged, every one a near-tie; bounds ~2x (initial: 5 lane-steps)
+    assert rate <= (4e-4 if converged else 2e-5)
     eng.close()

@@ -5,8 +5,12 @@ oracle/philox_ref.py (standard Philox4x32-10, pinned by Random123's known
 answers in tests/test_philox_ref.py) at the same (seed, step, t, global k, d):
 for odd T (the last step pair is half used), ragged K (partial workgroups),
 nonzero shard offsets and seeds / steps with high 32-bit words.  The tolerance
-covers only the fp32 logf / sincospif / Cholesky of the device's Box-Muller
-against the host's fp64 (a wrong counter or word mapping gives O(1) errors)."""
+covers only the fp32 transcendentals / Cholesky of the device's Box-Muller
+against the host's fp64 (a wrong counter or word mapping gives O(1) errors).
+The device evaluates Box-Muller on the hardware transcendentals (v_log_f32,
+v_sqrt_f32, v_sin_f32 / v_cos_f32 in revolutions); the bench's own stream
+(K = 65536, T = 64, 4.2 M elements) is checked whole, so the rare draws with
+u0 near 1, where the log's absolute error matters most, are in it."""
 import numpy as np
 import pytest
 
@@ -14,6 +18,7 @@ torch = pytest.importorskip("torch")
 pytestmark = pytest.mark.gpu
 
 import philox_ref as P  # noqa: E402
+from conftest import record  # noqa: E402
 
 TOL = 2e-5
 
@@ -26,7 +31,7 @@ def _gpu():
 
 
 @pytest.mark.parametrize("K_local,T,k_offset,seed,step", [(1000, 7, 0, 42, 3), (777, 1, 5000, 2 ** 40 + 9, 2 ** 33 + 1),
-                                                          (4099, 16, 123456, 0, 0)])
+                                                          (4099, 16, 123456, 0, 0), (65536, 64, 0, 1234, 0)])
 def test_arm_noise_stream(K_local, T, k_offset, seed, step):
     from mppi_robotarm_amd.engine import RolloutEngine
     from mppi_robotarm_amd.params import ArmParams
@@ -36,6 +41,7 @@ def test_arm_noise_stream(K_local, T, k_offset, seed, step):
     dev = eng.philox_noise(seed, step).double().cpu().numpy()
     ref = P.arm_noise(K_local, T, k_offset, seed, step, sig)
     err = np.abs(dev - ref) / (1.0 + np.abs(ref))
+    record("philox_stream", K=K_local, T=T, max_err=float(np.max(err)), p99_err=float(np.percentile(err, 99)))
     assert float(np.max(err)) < TOL, float(np.max(err))
     eng.close()
 

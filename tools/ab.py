@@ -4,6 +4,7 @@ the builds, so clock and thermal drift hit both alike.
 
     python tools/ab.py LIB_A.so LIB_B.so [LIB_C.so ...] [K T batches launches_per_batch]
     WORKLOAD=c5: the 7-link chain engine (default K 131072, T 128)
+    WORKLOAD=philox: the arm's noise draw (mppi_noise_philox) instead of the rollout
     LPS=n: lanes per sample of every arm build; LPS_LIST=a,b,...: per build (the same .so may repeat)
 
 Prints, per build, the median / min per-launch time (HIP events around each
@@ -89,6 +90,24 @@ def arm_runs(libs, K, T, lam, stream):
     return runs
 
 
+def philox_runs(libs, K, T, stream):
+    runs = []
+    for p in libs:
+        L = N.open_library(p)
+        ctx = make_ctx(L, K, T, 100.0, stream, 0)
+        out = torch.empty(T * K * 2, dtype=torch.float32, device="cuda")
+
+        def batch(n, L=L, ctx=ctx, out=out):
+            for i in range(n):
+                assert L.mppi_noise_philox(ctx, 1234, i, C.c_void_p(out.data_ptr())) == 0
+
+        def close(L=L, ctx=ctx, out=out, p=p):
+            print(f"    {os.path.basename(p)}: last draw sum {float(out.double().sum()):.6e}")
+            L.mppi_ctx_destroy(ctx)
+        runs.append((os.path.basename(p), batch, close, []))
+    return runs
+
+
 def main():
     libs = [os.path.abspath(a) for a in sys.argv[1:] if a.endswith(".so")]
     nums = [a for a in sys.argv[1:] if not a.endswith(".so")]
@@ -100,7 +119,10 @@ def main():
     lam = float(os.environ.get("LAMBDA", "100"))
     torch.cuda.set_device(0)
     stream = torch.cuda.current_stream().cuda_stream
-    runs = chain_runs(libs, K, T, lam) if c5 else arm_runs(libs, K, T, lam, stream)
+    if os.environ.get("WORKLOAD") == "philox":
+        runs = philox_runs(libs, K, T, stream)
+    else:
+        runs = chain_runs(libs, K, T, lam) if c5 else arm_runs(libs, K, T, lam, stream)
     torch.cuda.synchronize()
     for _, batch, _, _ in runs:   # warm-up
         batch(10)
