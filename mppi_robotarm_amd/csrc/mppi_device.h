@@ -908,35 +908,14 @@ __device__ __forceinline__ double median_at(const SM& sm, int t, int d, int T, i
 
 // ------------------------------------------------------------------ Philox
 
-// Philox4x32-10 (Salmon et al., SC'11).
-#ifdef MPPI_PHILOX_LIB
-__device__ __forceinline__ uint4 philox4x32_10(uint4 ctr, uint2 key) {
-#pragma unroll
-    for (int r = 0; r < 10; ++r) {
-        const unsigned lo0 = 0xD2511F53u * ctr.x, hi0 = __umulhi(0xD2511F53u, ctr.x);
-        const unsigned lo1 = 0xCD9E8D57u * ctr.z, hi1 = __umulhi(0xCD9E8D57u, ctr.z);
-        ctr = make_uint4(hi1 ^ ctr.y ^ key.x, lo1, hi0 ^ ctr.w ^ key.y, lo0);
-        key.x += 0x9E3779B9u;
-        key.y += 0xBB67AE85u;
-    }
-    return ctr;
-}
-
-// Two standard normals from two 32-bit uniforms (Box-Muller).
-__device__ __forceinline__ float2 box_muller(unsigned a, unsigned b) {
-    const float inv = 2.3283064365386963e-10f;  // 2^-32
-    const float u0 = ((float)a + 1.0f) * inv, u1 = (float)b * inv;
-    float s, c;
-    const float r = sqrtf(-2.0f * logf(fminf(u0, 1.0f)));
-    sincospif(2.0f * u1, &s, &c);
-    return make_float2(r * c, r * s);
-}
-#else
-// Each round's two 32 x 32 -> 64-bit products as one v_mad_u64_u32 apiece (the
-// 64-bit product of zero-extended words, which the compiler emits as one), not a
-// v_mul_lo_u32 + v_mul_hi_u32 pair: half the quarter-rate multiplies.  The round's two three-way XORs (hi ^ word ^ key)
-// are one v_bitop3_b32 each (truth table 0x96), the key word from an SGPR
-// (it must be wave-uniform: the "s" constraint takes lane 0's value).
+// Philox4x32-10 (Salmon et al., SC'11).  Each round's two 32 x 32 -> 64-bit
+// products are one v_mad_u64_u32 apiece (the 64-bit product of zero-extended
+// words, which the compiler emits as one), not a v_mul_lo_u32 + v_mul_hi_u32
+// pair: half the quarter-rate multiplies.  The round's two three-way XORs
+// (hi ^ word ^ key) are one v_bitop3_b32 each (truth table 0x96), the key word
+// from an SGPR (it must be wave-uniform: the "s" constraint takes lane 0's
+// value).  With the hardware Box-Muller below: 13.4 -> 8.35 us for config 3's
+// draw (profiles/r11/philox_ab.txt).
 __device__ __forceinline__ unsigned long long mul_wide(unsigned a, unsigned m) {
     return (unsigned long long)a * m;
 }
@@ -968,7 +947,6 @@ __device__ __forceinline__ float2 box_muller(unsigned a, unsigned b) {
     const float r = __builtin_amdgcn_sqrtf(-1.3862943611198906f * __builtin_amdgcn_logf(u0));   // -2 ln 2 log2 u0
     return make_float2(r * __builtin_amdgcn_cosf(u1), r * __builtin_amdgcn_sinf(u1));
 }
-#endif
 
 }  // namespace mppi
 
