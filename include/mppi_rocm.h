@@ -312,6 +312,8 @@ typedef struct {
     double stage_cost_weight[4];            /* on (x, y, dq_1, dq_2), control.py:185      */
     double terminal_cost_weight[4];         /* control.py:198                             */
     mppi_chain_params chain;
+    int precision;                          /* rollout arithmetic: 0 fp32 (default), 1 fp64
+                                               (for spread weights: see DESIGN §3b)       */
 } mppi_chain_config;
 
 typedef struct mppi_chain_ctx mppi_chain_ctx;

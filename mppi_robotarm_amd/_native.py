@@ -85,7 +85,7 @@ class ChainConfigC(C.Structure):
         ("delta_t", C.c_double), ("param_lambda", C.c_double), ("param_alpha", C.c_double),
         ("param_exploration", C.c_double), ("sigma", C.c_double * (CHAIN_MAX_DOF * CHAIN_MAX_DOF)),
         ("stage_cost_weight", C.c_double * 4), ("terminal_cost_weight", C.c_double * 4),
-        ("chain", ChainParamsC),
+        ("chain", ChainParamsC), ("precision", C.c_int),
     ]
 
 

@@ -102,8 +102,11 @@ class ChainEngine:
     def __init__(self, K_local: int, T: int, delta_t: float, param_lambda: float, param_alpha: float, sigma,
                  stage_cost_weight, terminal_cost_weight, param_exploration: float = 0.0,
                  chain: ChainParams = ChainParams(), K_total: int | None = None, k_offset: int = 0,
-                 device: int | torch.device | None = None):
+                 device: int | torch.device | None = None, precision: str = "f32"):
         self._lib = N.load()
+        if precision not in ("f32", "f64"):
+            raise ValueError("precision must be 'f32' or 'f64'")
+        self.precision = precision
         if device is None:
             device = torch.cuda.current_device()
         self.device = torch.device("cuda", device if isinstance(device, int) else device.index)
@@ -129,6 +132,7 @@ class ChainEngine:
             for i, v in enumerate(getattr(chain, f)):
                 arr[i] = float(v)
         cfg.chain.g = float(chain.g)
+        cfg.precision = 1 if precision == "f64" else 0
         with torch.cuda.device(self.device):
             self.stream = torch.cuda.current_stream(self.device)
             ctx = C.c_void_p()
@@ -284,8 +288,9 @@ class ChainMPPIController:
                  terminal_cost_weight: np.ndarray = np.array([5.0, 5.0, 50.0, 50.0]),
                  visualize_optimal_traj=True, visualze_sampled_trajs=False, *, chain: ChainParams = ChainParams(),
                  u_init=None, device: int | None = None, verbose: bool = False, noise: str = "numpy", seed: int = 0,
-                 process_group=None, exchange: str = "auto") -> None:
+                 process_group=None, exchange: str = "auto", precision: str = "f32") -> None:
         self.chain = chain
+        self.precision = precision   # rollout arithmetic: "f64" where the weights are spread
         self.dim_u, self.dim_x = chain.n, 2 * chain.n
         self.T, self.K = horizon_step_T, number_of_samples_K
         self.param_exploration, self.param_lambda, self.param_alpha = param_exploration, param_lambda, param_alpha
@@ -324,7 +329,8 @@ class ChainMPPIController:
             device = self._device if self._device is not None else torch.cuda.current_device()
             self._engine = ChainEngine(K_local, self.T, self.delta_t, self.param_lambda, self.param_alpha, self.Sigma,
                                        self.stage_cost_weight, self.terminal_cost_weight, self.param_exploration,
-                                       self.chain, K_total=self.K, k_offset=k_offset, device=device)
+                                       self.chain, K_total=self.K, k_offset=k_offset, device=device,
+                                       precision=self.precision)
             self._noise_dev = self._engine.new_noise()
             self._partial = self._engine.new_partial()
             self._S_dev = torch.empty(K_local, dtype=torch.float64, device=self._engine.device)

@@ -53,8 +53,11 @@ struct alignas(16) ChainStep {
     float4 key[kSlots];                    // centred search keys (see Search)
     float4 ctr;                            // window centre (cx, cy), W
     float x0[2 * kCMax];                   // q[n], dq[n]
+    double x0d[2 * kCMax];                 // the same in fp64 (fp64 rollout)
+    double wind[kSlots][4];                // the window rows in fp64 (fp64 rollout); rows >= W unused
     float ua[kMaxT + kCPU][2 * kCMax];     // u_t[n], a_t[n] (a = (gamma u_t)^T Sigma^-1), fp32; rows >= T zero
     double u[kMaxT][kCMax];                // nominal control sequence, fp64
+    double a[kMaxT][kCMax];                // a_t in fp64 (fp64 rollout)
 };
 
 // Launch constants (kernel argument, by value).
@@ -91,6 +94,7 @@ enum : int {
     kDynFloats = kOffG + 7,
 };
 static_assert(kDynFloats == kCDyn, "dyn layout");
+constexpr int kDynF64Off = (kCDyn + 1) & ~1;   // floats before the fp64 copy of the constants (8-B aligned)
 
 template <class F>   // F: const float (generic, kernel argument) or cfloat (constant address space)
 struct Dyn {
@@ -305,6 +309,130 @@ struct ChainState {
         *py = y.x + y.y;
     }
 };
+// The chain in fp64 (mppi_chain_config.precision = 1): the same equations as
+// ChainState, scalar doubles, sincos from the fp64 library.  Used where the
+// weights are spread (lambda comparable to the spread of S): in fp32 the
+// end effector sits ~1e-6 m from the fp64 one after 128 steps, so at a near-tie
+// of two window slots (slots 6e-5 m apart) the fp32 rollout may take the
+// neighbour, and that stage cost moves S by up to ~1e-3 relative — harmless
+// while one sample carries the weight, visible in w_eps when tens do.
+typedef __attribute__((address_space(4))) const double cdouble;
+template <int N>
+struct ChainStateD {
+    double q[N], dq[N], c[N], s[N];
+
+    __device__ __forceinline__ void load(const double* x0) {
+#pragma unroll
+        for (int a = 0; a < N; ++a) {
+            q[a] = x0[a];
+            dq[a] = x0[N + a];
+        }
+        angles();
+    }
+    __device__ __forceinline__ void angles() {
+        double th = 0.0;
+#pragma unroll
+        for (int a = 0; a < N; ++a) {
+            th += q[a];
+            sincos(th, &s[a], &c[a]);
+        }
+    }
+    // one semi-implicit Euler step (ChainState::step, oracle/chain_oracle.py chain_forward_dynamics)
+    __device__ __forceinline__ void step(const double (&v)[N], cdouble* k) {
+        double w[N], lc[N], ls[N], vc[N], vs[N], r[N];
+        double acc = 0.0;
+#pragma unroll
+        for (int a = 0; a < N; ++a) {
+            acc += dq[a];
+            w[a] = acc * acc;   // thdot^2
+            lc[a] = k[kOffL + a] * c[a];
+            ls[a] = k[kOffL + a] * s[a];
+            vc[a] = k[kOffNu + a] * c[a];
+            vs[a] = k[kOffNu + a] * s[a];
+        }
+        double ve[N];
+#pragma unroll
+        for (int a = 0; a < N; ++a) ve[a] = fma(-k[kOffDamp + a], dq[a], v[a]);
+        double Cs[N], Ss[N];
+        {
+            double cs = 0.0, ss = 0.0;
+#pragma unroll
+            for (int a = N - 1; a >= 0; --a) {
+                Cs[a] = cs;
+                Ss[a] = ss;
+                cs = fma(w[a], vc[a], cs);
+                ss = fma(w[a], vs[a], ss);
+            }
+        }
+        {
+            double cp = 0.0, sp = 0.0;
+            const double g = k[kOffG];
+#pragma unroll
+            for (int a = 0; a < N; ++a) {
+                const double X = fma(k[kOffL + a], Cs[a], k[kOffNu + a] * cp);
+                const double Y = fma(k[kOffL + a], Ss[a], k[kOffNu + a] * sp);
+                const double tau = a + 1 < N ? ve[a] - ve[a + 1] : ve[a];
+                r[a] = fma(c[a], Y, fma(-s[a], X, fma(-g, vc[a], tau)));
+                cp = fma(w[a], lc[a], cp);
+                sp = fma(w[a], ls[a], sp);
+            }
+        }
+        // D' lower triangle (L[i][a], i >= a), Cholesky in place
+        double L[N][N];
+#pragma unroll
+        for (int a = 0; a < N; ++a) {
+            L[a][a] = k[kOffDd + a];
+#pragma unroll
+            for (int i = a + 1; i < N; ++i) {
+                const double t = fma(ls[a], vs[i], lc[a] * vc[i]);
+                L[i][a] = i == a + 1 ? t + k[kOffJ + 2 * a + ((a + 1) & 1)] : t;   // -J_{a+1} beside the diagonal
+            }
+        }
+        double inv[N];
+#pragma unroll
+        for (int j = 0; j < N; ++j) {
+            inv[j] = rsqrt(L[j][j]);
+#pragma unroll
+            for (int i = j + 1; i < N; ++i) L[i][j] *= inv[j];
+#pragma unroll
+            for (int kk = j + 1; kk < N; ++kk)
+#pragma unroll
+                for (int i = kk; i < N; ++i) L[i][kk] = fma(-L[i][j], L[kk][j], L[i][kk]);
+        }
+#pragma unroll
+        for (int j = 0; j < N; ++j) {   // L y = r
+            r[j] *= inv[j];
+#pragma unroll
+            for (int i = j + 1; i < N; ++i) r[i] = fma(-L[i][j], r[j], r[i]);
+        }
+#pragma unroll
+        for (int i = N - 1; i >= 0; --i) {   // L^T x = y
+            double e = r[i];
+#pragma unroll
+            for (int kk = i + 1; kk < N; ++kk) e = fma(-L[kk][i], r[kk], e);
+            r[i] = e * inv[i];
+        }
+        const double dt = k[kOffDt];
+#pragma unroll
+        for (int a = 0; a < N; ++a) {
+            const double qdd = a ? r[a] - r[a - 1] : r[0];
+            dq[a] = fma(qdd, dt, dq[a]);
+            q[a] = fma(dq[a], dt, q[a]);
+        }
+        angles();
+    }
+    __device__ __forceinline__ void effector(cdouble* k, double* px, double* py) const {
+        double x = 0.0, y = 0.0;
+#pragma unroll
+        for (int a = 0; a < N; ++a) {
+            x = fma(k[kOffFk + a], c[a], x);
+            y = fma(k[kOffFk + a], s[a], y);
+        }
+        *px = x;
+        *py = y;
+    }
+};
+
 // Median filter (control.py:319-327) of the T x N weighted noise, u += w_eps
 // (control.py:126), shift (control.py:148-149) and the next launch's fp32
 // per-step constants.  u_cur[ch]: this thread's cur->u value idx = tid + ch kCT,
@@ -333,12 +461,72 @@ __device__ void chain_update_block(ChainStep* nxt, const ChainConst& c, CScratch
 #pragma unroll
             for (int e = 0; e < N; ++e) a += (c.gamma * u[e]) * c.sig_inv[e * N + d];
             nxt->ua[tid][kCMax + d] = (float)a;
+            nxt->a[tid][d] = a;
         }
     }
 }
 
+// The horizon loop in fp64 (control.py:95-109 with the chain model): returns S
+// of sample k.  Window rows in LDS; the nearest slot by the reference's own
+// distance ((x - rx)^2 + (y - ry)^2, first minimum, control.py:205-215).
+struct alignas(16) WinRowD {
+    double x, y, d1, d2;
+};
+template <int N>
+__device__ __forceinline__ double chain_horizon_f64(const ChainConst& c, const ChainStep* st, cdouble* kd,
+                                                    const float* noise, int k, float exf, WinRowD* s_wind) {
+    const int tid = threadIdx.x, K = c.K_local, T = c.T;
+    if (tid < kSlots) {
+        const double* r = st->wind[tid];
+        s_wind[tid] = WinRowD{r[0], r[1], r[2], r[3]};
+    }
+    __syncthreads();
+    ChainStateD<N> x;
+    x.load(st->x0d);
+    cdouble* cu = (cdouble*)&st->u[0][0];
+    cdouble* ca = (cdouble*)&st->a[0][0];
+    const int W = (int)st->ctr.z;
+    double S = 0.0, ex = 0.0, ey = 0.0, e1 = 0.0, e2 = 0.0;
+    float nx[N];
+#pragma unroll
+    for (int d = 0; d < N; ++d) nx[d] = noise[(size_t)d * K + k];
+    for (int t = 0; t < T; ++t) {
+        double v[N], g = 0.0;
+#pragma unroll
+        for (int d = 0; d < N; ++d) {
+            v[d] = exf != 0.f ? cu[t * kCMax + d] + (double)nx[d] : (double)nx[d];   // control.py:99-101
+            g = fma(ca[t * kCMax + d], v[d], g);                                      // control.py:106
+        }
+        const int tn = t + 1 < T ? t + 1 : t;
+#pragma unroll
+        for (int d = 0; d < N; ++d) nx[d] = noise[((size_t)tn * N + d) * K + k];
+        x.step(v, kd);
+        double px, py;
+        x.effector(kd, &px, &py);
+        int best = 0;
+        double dmin = INFINITY;
+        for (int j = 0; j < W; ++j) {
+            const WinRowD r = s_wind[j];
+            const double dx = px - r.x, dy = py - r.y;
+            const double d = fma(dx, dx, dy * dy);
+            if (d < dmin) {
+                dmin = d;
+                best = j;
+            }
+        }
+        const WinRowD r = s_wind[best];
+        ex = px - r.x;
+        ey = py - r.y;
+        e1 = x.dq[0] - r.d1;
+        e2 = x.dq[1] - r.d2;
+        S += fma(kd[kOffSw], ex * ex, fma(kd[kOffSw + 1], ey * ey, fma(kd[kOffSw + 2], e1 * e1, kd[kOffSw + 3] * (e2 * e2)))) + g;
+    }
+    // terminal cost, control.py:109
+    return S + fma(kd[kOffTw], ex * ex, fma(kd[kOffTw + 1], ey * ey, fma(kd[kOffTw + 2], e1 * e1, kd[kOffTw + 3] * (e2 * e2))));
+}
+
 // POLL / counter hand-off and the merges as in rollout_kernel (mppi_rocm.hip).
-template <int N, bool POLL>
+template <int N, bool POLL, bool F64>
 __global__ __launch_bounds__(kCT) __attribute__((amdgpu_waves_per_eu(2, 2))) void chain_rollout_kernel(
     const ChainConst c, const ChainStep* __restrict__ st, const float* __restrict__ dyn,
     const float* __restrict__ noise, double* __restrict__ S_out, double* __restrict__ slab, double* __restrict__ gslab,
@@ -348,6 +536,7 @@ __global__ __launch_bounds__(kCT) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
     static_assert(N <= kCMax && N >= 2, "links");
     __shared__ float4 s_win[kSlots];
     __shared__ KeyPair s_keys[kKeyPairs];
+    __shared__ WinRowD s_wind[F64 ? kSlots : 1];
     __shared__ double s_redd[kCT / 64];
     __shared__ int s_cnt[kCT / 64];
     __shared__ int s_k[kCT];
@@ -376,6 +565,10 @@ __global__ __launch_bounds__(kCT) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
         const int idx = tid + ch * kCT;
         u_cur[ch] = ((flags & MPPI_FLAG_FUSED_UPDATE) && idx < T * N) ? st->u[idx / N][idx % N] : 0.0;
     }
+    double S = 0.0;
+    if constexpr (F64) {
+        S = chain_horizon_f64<N>(c, st, (cdouble*)(dyn + kDynF64Off), noise, k, exf, s_wind);
+    } else {
     if (tid < kSlots) s_win[tid] = st->win[tid];
     // window keys in LDS (broadcast reads): the 90 key registers would cost the
     // chain kernel its second wave per SIMD; precise keys: the config-5 start
@@ -416,7 +609,6 @@ __global__ __launch_bounds__(kCT) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
 
     const DynMem kd{(cfloat*)dyn};
     // Horizon loop (control.py:95-109 with the chain model), S in fp64.
-    double S = 0.0;
     float S4 = 0.f;
     float ex = 0.f, ey = 0.f, e1 = 0.f, e2 = 0.f;
     auto step = [&](int t, auto i_c) {
@@ -460,6 +652,7 @@ __global__ __launch_bounds__(kCT) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
     }, std::make_integer_sequence<int, 3>{});
     S += (double)S4;
     S += (double)weighted_sq(ex, ey, e1, e2, c.dyn + kOffTw);  // terminal cost, control.py:109
+    }
 
     STAMP(1, NOW());
     if (S_out && valid) S_out[k] = S;
@@ -750,7 +943,8 @@ struct mppi_chain_ctx {
     float* d_base = nullptr;
     float* h_base = nullptr;
     float* d_chol = nullptr;       // Cholesky factor of Sigma (kCMax x kCMax, fp32) for the Philox noise
-    float* d_dyn = nullptr;        // packed per-step constants (DynMem)
+    float* d_dyn = nullptr;        // packed per-step constants (DynMem), then the same in fp64 at kDynF64Off
+    bool f64 = false;              // cfg.precision == 1
     unsigned* h_tmo = nullptr;
     unsigned* d_tmo = nullptr;
     unsigned long long* d_dbg = nullptr;
@@ -767,12 +961,12 @@ namespace {
 
 using mppi_host::fail;
 
-template <int N, bool P>
+template <int N, bool P, bool F64>
 void launch_rollout(mppi_chain_ctx* c, const ChainStep* cur, const float* noise, double* S, double* part, ChainStep* nxt,
                     unsigned flags) {
-    hipLaunchKernelGGL((chain_rollout_kernel<N, P>), dim3(c->nblocks), dim3(kCT), 0, c->stream, c->kc, cur, c->d_dyn, noise, S,
-                       c->d_slab, c->d_gslab, c->d_counter, part, c->d_weps, nxt, flags, c->xd, c->d_epoch, c->d_tmo, c->d_runmin,
-                       c->d_dbg);
+    hipLaunchKernelGGL((chain_rollout_kernel<N, P, F64>), dim3(c->nblocks), dim3(kCT), 0, c->stream, c->kc, cur, c->d_dyn,
+                       noise, S, c->d_slab, c->d_gslab, c->d_counter, part, c->d_weps, nxt, flags, c->xd, c->d_epoch, c->d_tmo,
+                       c->d_runmin, c->d_dbg);
 }
 
 // the link counts with an instantiated kernel
@@ -808,6 +1002,7 @@ int mppi_chain_ctx_create(const mppi_chain_config* cfg, int device, void* stream
     if (n < 2 || n > 7) return fail(MPPI_E_ARG, "chain.n must be in [2, 7]");
     if (cfg->T < 1 || cfg->T > MPPI_MAX_T) return fail(MPPI_E_ARG, "T must be in [1, 128]");
     if (cfg->T * n + 1 > kCMaxCh * kCT) return fail(MPPI_E_ARG, "T * n too large");
+    if (cfg->precision != 0 && cfg->precision != 1) return fail(MPPI_E_ARG, "precision must be 0 (fp32) or 1 (fp64)");
     if (cfg->K_local < 1 || cfg->K_total < cfg->K_local || cfg->k_offset < 0 ||
         cfg->k_offset + (long long)cfg->K_local > cfg->K_total)
         return fail(MPPI_E_ARG, "bad sample geometry (K_local, K_total, k_offset)");
@@ -848,6 +1043,7 @@ int mppi_chain_ctx_create(const mppi_chain_config* cfg, int device, void* stream
     c->n = n;
     c->stream = (hipStream_t)stream;
     c->nblocks = (cfg->K_local + kCT - 1) / kCT;
+    c->f64 = cfg->precision == 1;
     ChainConst& k = c->kc;
     memset(&k, 0, sizeof(k));
     k.K_local = cfg->K_local;
@@ -882,6 +1078,26 @@ int mppi_chain_ctx_create(const mppi_chain_config* cfg, int device, void* stream
     }
     dyn[kOffDt] = (float)cfg->delta_t;
     dyn[kOffG] = (float)P.g;
+    // the fp64 rollout's constants: the same layout, unrounded
+    double dynd[kCDyn] = {};
+    for (int a = 0; a < kCMax; ++a) dynd[kOffDd + a] = 1.0;
+    for (int a = 0; a < n; ++a) {
+        double tail = 0.0;
+        for (int q = a + 1; q < n; ++q) tail += P.m[q];
+        const double Jn = a + 1 < n ? P.J[a + 1] : 0.0;
+        dynd[kOffL + a] = P.l[a];
+        dynd[kOffNu + a] = P.m[a] * P.lc[a] + P.l[a] * tail;
+        dynd[kOffDd + a] = P.m[a] * P.lc[a] * P.lc[a] + P.l[a] * P.l[a] * tail + P.I[a] + P.J[a] + Jn;
+        dynd[kOffJ + 2 * a + ((a + 1) & 1)] = -Jn;
+        dynd[kOffDamp + a] = P.b[a];
+        dynd[kOffFk + a] = P.fk[a];
+    }
+    for (int i = 0; i < 4; ++i) {
+        dynd[kOffSw + i] = cfg->stage_cost_weight[i] * 10000.0;
+        dynd[kOffTw + i] = cfg->terminal_cost_weight[i] * 10000.0;
+    }
+    dynd[kOffDt] = cfg->delta_t;
+    dynd[kOffG] = P.g;
     k.lambda = cfg->param_lambda;
     k.inv_lambda = 1.0 / cfg->param_lambda;
     k.gamma = cfg->param_lambda * (1.0 - cfg->param_alpha);
@@ -897,7 +1113,10 @@ int mppi_chain_ctx_create(const mppi_chain_config* cfg, int device, void* stream
     int ncu = 0, per_cu = 0;
     if ((e = hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, device)) != hipSuccess)
         return cleanup_fail(fail(MPPI_E_HIP, std::string("device attributes: ") + hipGetErrorString(e)));
-#define MPPI_OCC(N) (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, (const void*)chain_rollout_kernel<N, true>, kCT, 0)
+#define MPPI_OCC(N)                                                                                                   \
+    (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(                                                               \
+        &per_cu, c->f64 ? (const void*)chain_rollout_kernel<N, true, true> : (const void*)chain_rollout_kernel<N, true, false>, \
+        kCT, 0)
     MPPI_CHAIN_DISPATCH(n, MPPI_OCC)
 #undef MPPI_OCC
     c->poll = per_cu >= 1 && c->nblocks <= ncu;
@@ -924,7 +1143,8 @@ int mppi_chain_ctx_create(const mppi_chain_config* cfg, int device, void* stream
         (e = hipMalloc(&c->d_weps, kCMaxVals * sizeof(double))) != hipSuccess ||
         (e = hipMalloc(&c->d_base, kCMaxVals * sizeof(float))) != hipSuccess ||
         (e = hipMalloc(&c->d_chol, sizeof(chol))) != hipSuccess ||
-        (e = hipMalloc(&c->d_dyn, sizeof(k.dyn))) != hipSuccess ||
+        (e = hipMalloc(&c->d_dyn, kDynF64Off * sizeof(float) + sizeof(dynd))) != hipSuccess ||
+        (e = hipMemcpy(c->d_dyn + kDynF64Off, dynd, sizeof(dynd), hipMemcpyHostToDevice)) != hipSuccess ||
         (e = hipHostMalloc(&c->h_step, sizeof(ChainStep), hipHostMallocDefault)) != hipSuccess ||
         (e = hipHostMalloc(&c->h_buf, kCMaxVals * sizeof(double), hipHostMallocDefault)) != hipSuccess ||
         (e = hipHostMalloc(&c->h_base, kCMaxVals * sizeof(float), hipHostMallocDefault)) != hipSuccess ||
@@ -1012,6 +1232,10 @@ int mppi_chain_set_step_inputs(mppi_chain_ctx* c, const double* x0, const double
     }
     h->ctr = make_float4((float)cx, (float)cy, (float)W, 0.f);
     for (int a = 0; a < 2 * kCMax; ++a) h->x0[a] = a < 2 * n ? (float)x0[a] : 0.f;
+    // fp64 rollout: x0 as [q(n), dq(n)] and the window rows unrounded
+    for (int a = 0; a < 2 * kCMax; ++a) h->x0d[a] = a < 2 * n ? x0[a] : 0.0;
+    for (int j = 0; j < kSlots; ++j)
+        for (int i = 0; i < 4; ++i) h->wind[j][i] = j < W ? window[4 * j + i] : 0.0;
     size_t bytes = offsetof(ChainStep, ua);
     if (u) {
         const ChainConst& k = c->kc;
@@ -1023,6 +1247,7 @@ int mppi_chain_set_step_inputs(mppi_chain_ctx* c, const double* x0, const double
                 if (d < n)
                     for (int e2 = 0; e2 < n; ++e2) a += (k.gamma * u[t * n + e2]) * k.sig_inv[e2 * n + d];
                 h->ua[t][kCMax + d] = (float)a;
+                h->a[t][d] = a;
             }
         }
         bytes = sizeof(ChainStep);
@@ -1047,8 +1272,11 @@ int mppi_chain_rollout(mppi_chain_ctx* c, const float* noise_dev, double* S_dev,
     const ChainStep* cur = c->d_step + c->cur;
     ChainStep* nxt = c->d_step + (c->cur ^ 1);
 #define MPPI_L(N)                                                                       \
-    if (c->poll) launch_rollout<N, true>(c, cur, noise_dev, S_dev, partial_dev, nxt, flags); \
-    else launch_rollout<N, false>(c, cur, noise_dev, S_dev, partial_dev, nxt, flags)
+    if (c->f64) {                                                                       \
+        if (c->poll) launch_rollout<N, true, true>(c, cur, noise_dev, S_dev, partial_dev, nxt, flags); \
+        else launch_rollout<N, false, true>(c, cur, noise_dev, S_dev, partial_dev, nxt, flags); \
+    } else if (c->poll) launch_rollout<N, true, false>(c, cur, noise_dev, S_dev, partial_dev, nxt, flags); \
+    else launch_rollout<N, false, false>(c, cur, noise_dev, S_dev, partial_dev, nxt, flags)
     MPPI_CHAIN_DISPATCH(c->n, MPPI_L)
 #undef MPPI_L
     const hipError_t e = hipGetLastError();

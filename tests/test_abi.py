@@ -69,11 +69,11 @@ def test_chain_struct_layout_matches_header(tmp_path):
 #include <stdio.h>
 #include "mppi_rocm.h"
 int main(void) {
-  printf("%zu %zu %zu %zu %zu %zu %zu %zu %zu %zu %d\n", sizeof(mppi_chain_config), sizeof(mppi_chain_params),
+  printf("%zu %zu %zu %zu %zu %zu %zu %zu %zu %zu %zu %d\n", sizeof(mppi_chain_config), sizeof(mppi_chain_params),
          offsetof(mppi_chain_config, delta_t), offsetof(mppi_chain_config, sigma),
          offsetof(mppi_chain_config, stage_cost_weight), offsetof(mppi_chain_config, terminal_cost_weight),
          offsetof(mppi_chain_config, chain), offsetof(mppi_chain_params, m), offsetof(mppi_chain_params, fk),
-         offsetof(mppi_chain_params, g), MPPI_CHAIN_MAX_DOF);
+         offsetof(mppi_chain_params, g), offsetof(mppi_chain_config, precision), MPPI_CHAIN_MAX_DOF);
   return 0;
 }
 ''')
@@ -83,7 +83,7 @@ int main(void) {
     Cc, Pc = N.ChainConfigC, N.ChainParamsC
     assert vals == [C.sizeof(Cc), C.sizeof(Pc), Cc.delta_t.offset, Cc.sigma.offset, Cc.stage_cost_weight.offset,
                     Cc.terminal_cost_weight.offset, Cc.chain.offset, Pc.m.offset, Pc.fk.offset, Pc.g.offset,
-                    N.CHAIN_MAX_DOF]
+                    Cc.precision.offset, N.CHAIN_MAX_DOF]
 
 
 def test_dropin_binding_layout_matches_header(tmp_path):

@@ -100,3 +100,27 @@ def test_theta_space_dynamics_equal_the_joint_space_equations():
     rhs = v - np.asarray(P7.b) * dq - S.T @ ((mu * np.sin(th[:, None] - th[None, :])) @ thd ** 2 + P7.g * nu * np.cos(th))
     qn, dqn = CO.chain_forward_dynamics(q[None], dq[None], v[None], 0.006, P7)
     np.testing.assert_allclose((dqn[0] - dq) / 0.006, np.linalg.solve(M, rhs), rtol=1e-10, atol=1e-10)
+
+
+def test_tie_flip_helper_explains_a_neighbour_pick(paths):
+    """tests/tieflip.py: a cost equal to the fp64 one with the neighbour slot taken
+    at the closest-tie step is explained (residual ~0, that step's gap reported)."""
+    from tieflip import tie_flip_residual, tie_table
+    rng = np.random.default_rng(3)
+    K, T = 64, 8
+    win = paths["xydq_circle"][:30]
+    from mppi_robotarm_amd.chain import CHAIN7_SIGMA, CHAIN7_X0, gravity_torque
+    x0 = CHAIN7_X0
+    u = np.tile(gravity_torque(x0[:7]), (T, 1))
+    eps = (rng.standard_normal((T, 7, K)) * np.sqrt(np.diag(CHAIN7_SIGMA))[None, :, None]).astype(np.float32)
+    W, TW = [0.5, 0.5, 5.0, 5.0], [5.0, 5.0, 50.0, 50.0]
+    Sr = coracle.chain_rollout_costs(x0, u, eps, win, 0.006, 100.0, 0.98, CHAIN7_SIGMA, W, TW, P7, layout="TNK")
+    idx = np.array([3, 17, 40])
+    gap, delta = tie_table(idx, x0, u, eps, win, 0.006, W, TW, P7)
+    S_dev = Sr.copy()
+    t1 = int(np.argmin(gap[0]))
+    S_dev[3] += delta[0, t1]                       # sample 3: the neighbour at its closest tie
+    res, used = tie_flip_residual(S_dev, Sr, idx, x0, u, eps, win, 0.006, W, TW, P7)
+    assert res[0] < 1e-12 and used[0] == gap[0, t1]
+    assert res[1] < 1e-12 and used[1] == 0.0       # unflipped samples need no flip
+    assert np.all(gap >= 0)
