@@ -96,7 +96,7 @@ def parse():
     p.add_argument("--K", type=int, default=None, help="c3: samples per GPU (65536); c2: 4096; c5: samples in total (131072)")
     p.add_argument("--T", type=int, default=None, help="horizon (c3: 64, c2: 32, c5: 128)")
     p.add_argument("--nbuf", type=int, default=None, help="rotated noise buffers (c3: 10, c5: 4)")
-    p.add_argument("--lps", type=int, default=0, help="lanes per sample (0 = auto)")
+    p.add_argument("--lps", type=int, default=0, help="lanes per sample (0 = auto; c5: 1 or 4)")
     p.add_argument("--precision", choices=("f32", "f64"), default="f32",
                    help="c5: rollout arithmetic of the chain (f64: for spread weights, DESIGN §3b)")
     p.add_argument("--cpu-seconds", type=float, default=10.0, help="CPU baseline budget (0 = skip)")
@@ -295,7 +295,7 @@ def main():
         K, k_offset = shard_geometry(K_total, world, rank)
         eng = ChainEngine(K, T, 0.006, 100.0, 0.98, CHAIN7_SIGMA, [0.5, 0.5, 5.0, 5.0], [5.0, 5.0, 50.0, 50.0],
                           0.0, ChainParams(), K_total=K_total, k_offset=k_offset, device=local_rank,
-                          precision=args.precision)
+                          precision=args.precision, lanes_per_sample=args.lps)
         x0 = CHAIN7_X0.copy()
         u = np.tile(gravity_torque(x0[:7]), (T, 1))
     else:
@@ -473,7 +473,7 @@ def main():
                                     f"2-DoF arm MPPI step, K={K_total} (K/GPU={K}) T={T}, run.py constants, "
                                     f"xydq_circle.txt window, Philox N(0,20I) noise x{args.nbuf} buffers"),
                        "K_total": K_total, "K_per_gpu": K, "T": T,
-                       "lanes_per_sample": 1 if c5 else eng.lanes_per_sample,
+                       "lanes_per_sample": eng.lanes_per_sample,
                        "exchange": xmode, "backend": args.backend if world > 1 else None,
                        "parallelism": (f"samples sharded x{world} ranks on {n_dev} GPU(s), " + (
                            ("partial rows exchanged inside the rollout launch (IPC inboxes"

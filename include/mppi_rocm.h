@@ -314,6 +314,8 @@ typedef struct {
     mppi_chain_params chain;
     int precision;                          /* rollout arithmetic: 0 fp32 (default), 1 fp64
                                                (for spread weights: see DESIGN §3b)       */
+    int lanes_per_sample;                   /* 0 = auto; 1, or 4 (fp32: a quad per sample,
+                                               lane p the link pair (2p, 2p+1))           */
 } mppi_chain_config;
 
 typedef struct mppi_chain_ctx mppi_chain_ctx;
@@ -322,7 +324,8 @@ typedef struct mppi_chain_ctx mppi_chain_ctx;
 int mppi_chain_ctx_create(const mppi_chain_config *cfg, int device, void *stream, mppi_chain_ctx **out);
 void mppi_chain_ctx_destroy(mppi_chain_ctx *ctx);
 int mppi_chain_set_stream(mppi_chain_ctx *ctx, void *stream);
-int mppi_chain_ctx_info(const mppi_chain_ctx *ctx, int *blocks, int *threads_per_block, int *poll);
+int mppi_chain_ctx_info(const mppi_chain_ctx *ctx, int *blocks, int *threads_per_block, int *poll,
+                        int *lanes_per_sample);
 /* inputs of control.py:70-75: x0[2n], the window (W x 4), u[T*n] (NULL: keep the device nominal) */
 int mppi_chain_set_step_inputs(mppi_chain_ctx *ctx, const double *x0, const double *window, int W,
                                const double *u);

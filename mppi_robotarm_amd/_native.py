@@ -85,7 +85,7 @@ class ChainConfigC(C.Structure):
         ("delta_t", C.c_double), ("param_lambda", C.c_double), ("param_alpha", C.c_double),
         ("param_exploration", C.c_double), ("sigma", C.c_double * (CHAIN_MAX_DOF * CHAIN_MAX_DOF)),
         ("stage_cost_weight", C.c_double * 4), ("terminal_cost_weight", C.c_double * 4),
-        ("chain", ChainParamsC), ("precision", C.c_int),
+        ("chain", ChainParamsC), ("precision", C.c_int), ("lanes_per_sample", C.c_int),
     ]
 
 
@@ -136,7 +136,7 @@ def open_library(path: str):
         "mppi_chain_ctx_create": ([C.POINTER(ChainConfigC), C.c_int, vp, C.POINTER(vp)], C.c_int),
         "mppi_chain_ctx_destroy": ([vp], None),
         "mppi_chain_set_stream": ([vp, vp], C.c_int),
-        "mppi_chain_ctx_info": ([vp, ip, ip, ip], C.c_int),
+        "mppi_chain_ctx_info": ([vp, ip, ip, ip, ip], C.c_int),
         "mppi_chain_set_step_inputs": ([vp, dp, dp, C.c_int, dp], C.c_int),
         "mppi_chain_rollout": ([vp, fp, vp, vp, C.c_uint], C.c_int),
         "mppi_chain_merge_partials": ([vp, vp, C.c_int, C.c_uint], C.c_int),

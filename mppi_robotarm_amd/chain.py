@@ -102,7 +102,7 @@ class ChainEngine:
     def __init__(self, K_local: int, T: int, delta_t: float, param_lambda: float, param_alpha: float, sigma,
                  stage_cost_weight, terminal_cost_weight, param_exploration: float = 0.0,
                  chain: ChainParams = ChainParams(), K_total: int | None = None, k_offset: int = 0,
-                 device: int | torch.device | None = None, precision: str = "f32"):
+                 device: int | torch.device | None = None, precision: str = "f32", lanes_per_sample: int = 0):
         self._lib = N.load()
         if precision not in ("f32", "f64"):
             raise ValueError("precision must be 'f32' or 'f64'")
@@ -133,6 +133,7 @@ class ChainEngine:
                 arr[i] = float(v)
         cfg.chain.g = float(chain.g)
         cfg.precision = 1 if precision == "f64" else 0
+        cfg.lanes_per_sample = int(lanes_per_sample)
         with torch.cuda.device(self.device):
             self.stream = torch.cuda.current_stream(self.device)
             ctx = C.c_void_p()
@@ -140,10 +141,10 @@ class ChainEngine:
                                                     C.c_void_p(self.stream.cuda_stream), C.byref(ctx)),
                     "mppi_chain_ctx_create")
         self._ctx = ctx
-        blocks, threads, poll = C.c_int(), C.c_int(), C.c_int()
-        N.check(self._lib.mppi_chain_ctx_info(ctx, C.byref(blocks), C.byref(threads), C.byref(poll)),
+        blocks, threads, poll, lps = C.c_int(), C.c_int(), C.c_int(), C.c_int()
+        N.check(self._lib.mppi_chain_ctx_info(ctx, C.byref(blocks), C.byref(threads), C.byref(poll), C.byref(lps)),
                 "mppi_chain_ctx_info")
-        self.blocks, self.threads = blocks.value, threads.value
+        self.blocks, self.threads, self.lanes_per_sample = blocks.value, threads.value, lps.value
         self.handoff = "poll" if poll.value else "counter"
         self.partial_len = 2 + self.n * self.T
 

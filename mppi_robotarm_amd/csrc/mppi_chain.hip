@@ -525,8 +525,223 @@ __device__ __forceinline__ double chain_horizon_f64(const ChainConst& c, const C
     return S + fma(kd[kOffTw], ex * ex, fma(kd[kOffTw + 1], ey * ey, fma(kd[kOffTw + 2], e1 * e1, kd[kOffTw + 3] * (e2 * e2))));
 }
 
+// ---------------------------------------------------------------- 4 lanes per sample
+//
+// When K is too small to give every SIMD a wave (config 5 sharded 8 ways: K =
+// 16384 per GPU is 256 waves on 1024 SIMDs), the four lanes of a quad share one
+// sample: lane p holds the link pair (2p, 2p+1) — exactly one f32x2 of
+// ChainState's representation — and the quad exchanges values with DPP
+// quad_perm (one instruction per broadcast or scan step).  Per lane and step:
+// one pair's sincos, prefix / suffix sums as 4-lane scans, the rows (2p, 2p+1)
+// of D' and of the right-looking Cholesky (each pivot and each L[kk][j]
+// broadcast from the lane that owns it, so every lane ends with all of L), the
+// forward solve on the pairs with each y_j broadcast, the backward solve
+// redundantly from those broadcast values, and 8 of the 30 window slots.
+// ~0.55x the instructions per lane of one lane per sample, on 4x the lanes.
+
+// v from lane Q of each quad
+template <int Q>
+__device__ __forceinline__ float qbc(float v) {
+    return dpp_f32<Q * 0x55>(v);   // quad_perm [Q, Q, Q, Q]
+}
+// sum over the lanes p' < p of the quad (m1 = p >= 1, m2 = p >= 2 as 1.f / 0.f)
+__device__ __forceinline__ float q_excl_prefix(float x, float m1, float m2) {
+    const float e = dpp_f32<0x90>(x) * m1;          // quad_perm [0, 0, 1, 2]: x_{p-1}
+    const float f = fmaf(dpp_f32<0x90>(e), m1, e);  // x_{p-1} + x_{p-2}
+    return fmaf(dpp_f32<0x40>(f), m2, f);          // quad_perm [0, 0, 0, 1]: + f_{p-2}
+}
+// sum over the lanes p' > p of the quad (u1 = p <= 2, u2 = p <= 1)
+__device__ __forceinline__ float q_excl_suffix(float x, float u1, float u2) {
+    const float e = dpp_f32<0xF9>(x) * u1;          // quad_perm [1, 2, 3, 3]: x_{p+1}
+    const float f = fmaf(dpp_f32<0xF9>(e), u1, e);  // x_{p+1} + x_{p+2}
+    return fmaf(dpp_f32<0xFE>(f), u2, f);          // quad_perm [2, 3, 3, 3]: + f_{p+2}
+}
+__device__ __forceinline__ float q_sum(float x) {
+    x += dpp_f32<0xB1>(x);   // quad_perm xor 1
+    return x + dpp_f32<0x4E>(x);
+}
+__device__ __forceinline__ double q_sum_f64(double x) {
+    x += dpp_f64<0xB1>(x);
+    return x + dpp_f64<0x4E>(x);
+}
+template <int J>
+__device__ __forceinline__ float elem(f32x2 v) {
+    return (J & 1) ? v.y : v.x;
+}
+
+// The horizon loop of sample k on the 4 lanes of its quad (control.py:95-109 with
+// the chain model).  Returns S, the same value in all 4 lanes.  s_ua4 holds
+// (T + kCPF) x 4 rows: (u_2p, u_2p+1, a_2p, a_2p+1) of step t for lane p.
+template <int N>
+__device__ __forceinline__ double chain_horizon_lps4(const ChainConst& c, const ChainStep* st, const float* dyn,
+                                                     const float* noise, int k, float exf, float4* s_ua4,
+                                                     float4* s_win) {
+    static_assert(N <= 8, "four link pairs");
+    const int tid = threadIdx.x, sub = tid & 3, K = c.K_local, T = c.T;
+    if (tid < kSlots) s_win[tid] = st->win[tid];
+    for (int i = tid; i < (T + kCPF) * 4; i += kCT) {
+        const int t = min(i >> 2, T - 1), p = i & 3;
+        const float* r = st->ua[t];
+        s_ua4[i] = make_float4(r[2 * p], r[2 * p + 1], r[kCMax + 2 * p], r[kCMax + 2 * p + 1]);
+    }
+    Search<4, true> sr;
+    sr.load(st->key, st->ctr, sub);
+    const int a0 = 2 * sub, a1 = 2 * sub + 1;   // this lane's links
+    const float m1 = sub >= 1 ? 1.f : 0.f, m2 = sub >= 2 ? 1.f : 0.f;
+    const float u1 = sub <= 2 ? 1.f : 0.f, u2 = sub <= 1 ? 1.f : 0.f;
+    const float own = sub == 0 ? 1.f : 0.f;
+    const f32x2 pad = {a0 < N ? 1.f : 0.f, a1 < N ? 1.f : 0.f};
+    const f32x2 l2 = {dyn[kOffL + a0], dyn[kOffL + a1]}, nu2 = {dyn[kOffNu + a0], dyn[kOffNu + a1]};
+    const f32x2 damp2 = {dyn[kOffDamp + a0], dyn[kOffDamp + a1]}, fk2 = {dyn[kOffFk + a0], dyn[kOffFk + a1]};
+    const float dt = dyn[kOffDt], g = dyn[kOffG];
+    float sw[4], tw[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        sw[i] = dyn[kOffSw + i];
+        tw[i] = dyn[kOffTw + i];
+    }
+    // column a of D' on rows (a0, a1): l_a nu_i cos(th_a - th_i) from the broadcast (l c, l s) of link a, plus
+    // corr[a]: Dd_a - l_a nu_a on the diagonal (the product gives l_a nu_a there) and -J_{a+1} below it
+    f32x2 corr[N];
+    {
+        const float dc0 = dyn[kOffDd + a0] - l2.x * nu2.x, dc1 = dyn[kOffDd + a1] - l2.y * nu2.y;
+        const float j0 = a0 >= 1 ? dyn[kOffJ + 2 * (a0 - 1) + (a0 & 1)] : 0.f;   // -J_{a0} at (a0, a0 - 1)
+        const float j1 = dyn[kOffJ + 2 * (a1 - 1) + (a1 & 1)];                    // -J_{a1} at (a1, a1 - 1)
+#pragma unroll
+        for (int a = 0; a < N; ++a)
+            corr[a] = f32x2{a0 == a ? dc0 : (a0 == a + 1 ? j0 : 0.f), a1 == a ? dc1 : (a1 == a + 1 ? j1 : 0.f)};
+    }
+    // state of this lane's pair
+    f32x2 Q = {a0 < N ? st->x0[a0] : 0.f, a1 < N ? st->x0[a1] : 0.f};
+    f32x2 DQ = {a0 < N ? st->x0[N + a0] : 0.f, a1 < N ? st->x0[N + a1] : 0.f};
+    f32x2 C, Sn;
+    auto angles = [&]() {
+        const float t = Q.x + Q.y;
+        const float e = q_excl_prefix(t, m1, m2);
+        float s0, c0, s1, c1;
+        sincos_f32(e + Q.x, &s0, &c0);
+        sincos_f32(e + t, &s1, &c1);
+        Sn = f32x2{s0, s1};
+        C = f32x2{c0, c1};
+    };
+    angles();
+    // noise of links (a0, a1) at step t: rows (t N + d) K + k; pad links read link N - 1 (masked below).
+    // A uniform row base plus a 32-bit lane byte offset (the saddr form of global_load).
+    const unsigned o0 = (unsigned)(min(a0, N - 1) * K + k) * 4u, o1 = (unsigned)(min(a1, N - 1) * K + k) * 4u;
+    auto nrow = [&](int t) {
+        const char* row = (const char*)(noise + (size_t)min(t, T - 1) * N * K);
+        return f32x2{*(const float*)(row + o0), *(const float*)(row + o1)};
+    };
+    f32x2 ring[kCPF];
+#pragma unroll
+    for (int j = 0; j < kCPF; ++j) ring[j] = nrow(j);
+    __syncthreads();
+
+    double S = 0.0;
+    float S4 = 0.f;
+    f32x2 G2 = {0.f, 0.f};   // this lane's (gamma u^T Sigma^-1) v terms
+    float ex = 0.f, ey = 0.f, e1 = 0.f, e2 = 0.f;
+    auto step = [&](int t, auto slot_c) {
+        constexpr int slot = decltype(slot_c)::value;
+        const float4 ua = s_ua4[t * 4 + sub];
+        const f32x2 v = __builtin_elementwise_fma(splat(exf), f32x2{ua.x, ua.y}, ring[slot]) * pad;  // control.py:99-101
+        G2 = __builtin_elementwise_fma(f32x2{ua.z, ua.w}, v, G2);                                  // control.py:106
+        ring[slot] = nrow(t + kCPF);
+        PIN_LOADS();
+        // ---- dynamics (ChainState::step on the quad)
+        f32x2 w;
+        {
+            const float t2 = DQ.x + DQ.y;
+            const float e = q_excl_prefix(t2, m1, m2);
+            w = f32x2{e + DQ.x, e + t2};
+            w = w * w;   // thdot^2
+        }
+        const f32x2 lc = l2 * C, ls = l2 * Sn, vc = nu2 * C, vs = nu2 * Sn;
+        const f32x2 wvc = w * vc, wvs = w * vs, wlc = w * lc, wls = w * ls;
+        const float sC = q_excl_suffix(wvc.x + wvc.y, u1, u2), sS = q_excl_suffix(wvs.x + wvs.y, u1, u2);
+        const float pC = q_excl_prefix(wlc.x + wlc.y, m1, m2), pS = q_excl_prefix(wls.x + wls.y, m1, m2);
+        const f32x2 Cs = {wvc.y + sC, sC}, Ss = {wvs.y + sS, sS};
+        const f32x2 Cp = {pC, wlc.x + pC}, Sp = {pS, wls.x + pS};
+        const f32x2 X = __builtin_elementwise_fma(l2, Cs, nu2 * Cp);
+        const f32x2 Y = __builtin_elementwise_fma(l2, Ss, nu2 * Sp);
+        const f32x2 ve = __builtin_elementwise_fma(-damp2, DQ, v);
+        const float ve_next = dpp_f32<0xF9>(ve.x) * u1;   // link a1 + 1 (0 past the quad)
+        f32x2 r = {ve.x - ve.y, ve.y - ve_next};            // tau
+        r = __builtin_elementwise_fma(C, Y, __builtin_elementwise_fma(-Sn, X, __builtin_elementwise_fma(splat(-g), vc, r)));
+        // D' rows (a0, a1), Cholesky: every lane keeps the broadcast L[kk][j] and 1 / L[j][j]
+        f32x2 col[N];
+        unroll_seq([&](auto a_c) {
+            constexpr int a = decltype(a_c)::value;
+            const float la = qbc<a / 2>(elem<a>(lc)), sa = qbc<a / 2>(elem<a>(ls));
+            col[a] = __builtin_elementwise_fma(splat(la), vc, __builtin_elementwise_fma(splat(sa), vs, corr[a]));
+        }, std::make_integer_sequence<int, N>{});
+        float inv[N], L[N][N];
+        unroll_seq([&](auto j_c) {
+            constexpr int j = decltype(j_c)::value;
+            inv[j] = __builtin_amdgcn_rsqf(qbc<j / 2>(elem<j>(col[j])));
+            col[j] = col[j] * splat(inv[j]);
+            unroll_seq([&](auto k_c) {
+                constexpr int kk = decltype(k_c)::value;
+                if constexpr (kk > j) {
+                    L[kk][j] = qbc<kk / 2>(elem<kk>(col[j]));
+                    col[kk] = __builtin_elementwise_fma(splat(-L[kk][j]), col[j], col[kk]);
+                }
+            }, std::make_integer_sequence<int, N>{});
+        }, std::make_integer_sequence<int, N>{});
+        // L y = r on the pairs (rows <= j go stale once their y is out); every lane keeps every y_j
+        float y[N];
+        unroll_seq([&](auto j_c) {
+            constexpr int j = decltype(j_c)::value;
+            y[j] = qbc<j / 2>(elem<j>(r) * inv[j]);
+            r = __builtin_elementwise_fma(splat(-y[j]), col[j], r);
+        }, std::make_integer_sequence<int, N>{});
+        // L^T x = y, redundantly in every lane from the broadcast values
+        float x[N];
+#pragma unroll
+        for (int i = N - 1; i >= 0; --i) {
+            float e = y[i];
+#pragma unroll
+            for (int kk = i + 1; kk < N; ++kk) e = fmaf(-L[kk][i], x[kk], e);
+            x[i] = e * inv[i];
+        }
+        auto xs = [&](int i) { return i >= 0 && i < N ? x[i] : 0.f; };   // i compile-time below
+        const bool b0 = sub & 1, b1 = sub & 2;
+        const float xa = b1 ? (b0 ? xs(6) : xs(4)) : (b0 ? xs(2) : xs(0));
+        const float xb = b1 ? (b0 ? xs(7) : xs(5)) : (b0 ? xs(3) : xs(1));
+        const float xp = b1 ? (b0 ? xs(5) : xs(3)) : (b0 ? xs(1) : 0.f);   // link a0 - 1
+        const f32x2 qdd = f32x2{xa - xp, xb - xa} * pad;                     // q_ddot = diff(theta_ddot)
+        DQ = __builtin_elementwise_fma(qdd, splat(dt), DQ);
+        Q = __builtin_elementwise_fma(DQ, splat(dt), Q);
+        angles();
+        // ---- end effector, nearest waypoint, stage cost (control.py:174-198)
+        const f32x2 fx = fk2 * C, fy = fk2 * Sn;
+        const float px = q_sum(fx.x + fx.y), py = q_sum(fy.x + fy.y);
+        const float4 rw = s_win[sr.nearest(px, py)];
+        ex = px - rw.x;
+        ey = py - rw.y;
+        e1 = qbc<0>(DQ.x) - rw.z;
+        e2 = qbc<0>(DQ.y) - rw.w;
+        S4 = fmaf(own, weighted_sq(ex, ey, e1, e2, sw), S4);
+        if constexpr (slot == kCPF - 1) {
+            S += (double)(S4 + (G2.x + G2.y));
+            S4 = 0.f;
+            G2 = f32x2{0.f, 0.f};
+        }
+    };
+    static_assert(kCPF == 2, "unrolled for a 2-deep ring");
+    int t = 0;
+    for (; t + 2 <= T; t += 2) {
+        step(t, std::integral_constant<int, 0>{});
+        step(t + 1, std::integral_constant<int, 1>{});
+    }
+    if (t < T) step(t, std::integral_constant<int, 0>{});
+    S += (double)(S4 + (G2.x + G2.y));
+    S += (double)(own * weighted_sq(ex, ey, e1, e2, tw));   // terminal cost, control.py:109
+    return q_sum_f64(S);
+}
+
 // POLL / counter hand-off and the merges as in rollout_kernel (mppi_rocm.hip).
-template <int N, bool POLL, bool F64>
+template <int N, bool POLL, bool F64, int LPS>
 __global__ __launch_bounds__(kCT) __attribute__((amdgpu_waves_per_eu(2, 2))) void chain_rollout_kernel(
     const ChainConst c, const ChainStep* __restrict__ st, const float* __restrict__ dyn,
     const float* __restrict__ noise, double* __restrict__ S_out, double* __restrict__ slab, double* __restrict__ gslab,
@@ -537,6 +752,7 @@ __global__ __launch_bounds__(kCT) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
     __shared__ float4 s_win[kSlots];
     __shared__ KeyPair s_keys[kKeyPairs];
     __shared__ WinRowD s_wind[F64 ? kSlots : 1];
+    __shared__ float4 s_ua4[LPS == 4 ? (kMaxT + kCPF) * 4 : 1];
     __shared__ double s_redd[kCT / 64];
     __shared__ int s_cnt[kCT / 64];
     __shared__ int s_k[kCT];
@@ -545,10 +761,13 @@ __global__ __launch_bounds__(kCT) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
     __shared__ double s_run;
     __shared__ CScratch sm;
 
+    static_assert(LPS == 1 || (LPS == 4 && !F64), "lanes per sample: 1, or 4 for the fp32 rollout");
+    constexpr int NS = kCT / LPS;   // samples per workgroup
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-    const int k_raw = blockIdx.x * kCT + tid;
+    const int k_raw = (blockIdx.x * kCT + tid) / LPS;
     if (c.fair) draw_cu_ticket(counters + c.cu_off, &s_parity);
     const bool valid = k_raw < c.K_local;
+    const bool owner = valid && (tid & (LPS - 1)) == 0;   // the lane that stands for its sample
     const int k = valid ? k_raw : c.K_local - 1;
     const float exf = (c.k_offset + k) < c.k_exploit ? 1.f : 0.f;  // control.py:98-101
     const int K = c.K_local, T = c.T;
@@ -568,6 +787,8 @@ __global__ __launch_bounds__(kCT) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
     double S = 0.0;
     if constexpr (F64) {
         S = chain_horizon_f64<N>(c, st, (cdouble*)(dyn + kDynF64Off), noise, k, exf, s_wind);
+    } else if constexpr (LPS == 4) {
+        S = chain_horizon_lps4<N>(c, st, dyn, noise, k, exf, s_ua4, s_win);
     } else {
     if (tid < kSlots) s_win[tid] = st->win[tid];
     // window keys in LDS (broadcast reads): the 90 key registers would cost the
@@ -655,15 +876,15 @@ __global__ __launch_bounds__(kCT) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
     }
 
     STAMP(1, NOW());
-    if (S_out && valid) S_out[k] = S;
+    if (S_out && owner) S_out[k] = S;
 
     // ---- workgroup partial: rho_b, eta_b, N_b (control.py:112-118 over this block)
-    const double rho_b = block_min_f64<kCT>(valid ? S : INFINITY, sm);
+    const double rho_b = block_min_f64<kCT>(owner ? S : INFINITY, sm);
     // fp64, like the reference's weights; a wave whose samples all lie below the
     // floor (exp(-44.4) = 2^-64: the usual case, S spread >> lambda) skips the exp
     const double warg = (rho_b - S) * c.inv_lambda;
     double wgt = 0.0;
-    if (__any(valid && warg >= -45.0)) wgt = valid ? exp(warg) : 0.0;
+    if (__any(owner && warg >= -45.0)) wgt = owner ? exp(warg) : 0.0;
     const bool nz = wgt >= kMergeFloor;
     const unsigned long long bal = __ballot(nz);
     const double esum = wave_sum_f64(nz ? wgt : 0.0);
@@ -726,16 +947,19 @@ __global__ __launch_bounds__(kCT) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
             publish(blockIdx.x * stride + 2 + col, gather_col(base, 1, s_k, s_e, nl));
         }
     } else {
-        constexpr int PER = kCT / 64;
+        constexpr int PER = (NS + 63) / 64;
         constexpr int kRowBatch = 4;
-        const int k0 = blockIdx.x * kCT;
-        s_e[tid] = 0.0;
+        const int k0 = blockIdx.x * NS;
+        if (tid < NS) s_e[tid] = 0.0;
         __syncthreads();
         if (nz) s_e[k - k0] = wgt;
         __syncthreads();
         double w[PER];
 #pragma unroll
-        for (int i = 0; i < PER; ++i) w[i] = (k0 + lane + 64 * i < K) ? s_e[lane + 64 * i] : 0.0;
+        for (int i = 0; i < PER; ++i) {
+            const int ks = lane + 64 * i;
+            w[i] = (ks < NS && k0 + ks < K) ? s_e[ks] : 0.0;
+        }
         for (int cb = wave * kRowBatch; cb < nval; cb += (kCT / 64) * kRowBatch) {
             float e[kRowBatch][PER];
 #pragma unroll
@@ -945,6 +1169,7 @@ struct mppi_chain_ctx {
     float* d_chol = nullptr;       // Cholesky factor of Sigma (kCMax x kCMax, fp32) for the Philox noise
     float* d_dyn = nullptr;        // packed per-step constants (DynMem), then the same in fp64 at kDynF64Off
     bool f64 = false;              // cfg.precision == 1
+    int lps = 1;                   // lanes per sample: 1, or 4 (fp32 rollout at small K)
     unsigned* h_tmo = nullptr;
     unsigned* d_tmo = nullptr;
     unsigned long long* d_dbg = nullptr;
@@ -961,10 +1186,10 @@ namespace {
 
 using mppi_host::fail;
 
-template <int N, bool P, bool F64>
+template <int N, bool P, bool F64, int LPS>
 void launch_rollout(mppi_chain_ctx* c, const ChainStep* cur, const float* noise, double* S, double* part, ChainStep* nxt,
                     unsigned flags) {
-    hipLaunchKernelGGL((chain_rollout_kernel<N, P, F64>), dim3(c->nblocks), dim3(kCT), 0, c->stream, c->kc, cur, c->d_dyn,
+    hipLaunchKernelGGL((chain_rollout_kernel<N, P, F64, LPS>), dim3(c->nblocks), dim3(kCT), 0, c->stream, c->kc, cur, c->d_dyn,
                        noise, S, c->d_slab, c->d_gslab, c->d_counter, part, c->d_weps, nxt, flags, c->xd, c->d_epoch, c->d_tmo,
                        c->d_runmin, c->d_dbg);
 }
@@ -980,6 +1205,14 @@ void launch_rollout(mppi_chain_ctx* c, const ChainStep* cur, const float* noise,
         case 7: F(7); break;      \
         default: break;           \
     }
+
+// Lanes per sample of the fp32 rollout: 4 while one lane per sample would leave
+// SIMDs without a wave (K <= 32768: at most 512 waves of 64 samples on 1024 SIMDs);
+// measured in DESIGN §3b.  The fp64 rollout keeps one lane per sample.
+int chain_auto_lps(int K_local, bool f64) {
+    if (f64) return 1;
+    return K_local <= 32768 ? 4 : 1;
+}
 
 int check_tmo(mppi_chain_ctx* c) {
     if (c->h_tmo && __atomic_load_n(c->h_tmo, __ATOMIC_ACQUIRE)) {
@@ -1042,8 +1275,17 @@ int mppi_chain_ctx_create(const mppi_chain_config* cfg, int device, void* stream
     c->device = device;
     c->n = n;
     c->stream = (hipStream_t)stream;
-    c->nblocks = (cfg->K_local + kCT - 1) / kCT;
     c->f64 = cfg->precision == 1;
+    c->lps = cfg->lanes_per_sample > 0 ? cfg->lanes_per_sample : chain_auto_lps(cfg->K_local, c->f64);
+    if (c->lps != 1 && c->lps != 4) {
+        delete c;
+        return fail(MPPI_E_ARG, "lanes_per_sample must be 0 (auto), 1 or 4");
+    }
+    if (c->lps == 4 && c->f64) {
+        delete c;
+        return fail(MPPI_E_ARG, "lanes_per_sample 4 is for the fp32 rollout");
+    }
+    c->nblocks = (int)(((long long)cfg->K_local * c->lps + kCT - 1) / kCT);
     ChainConst& k = c->kc;
     memset(&k, 0, sizeof(k));
     k.K_local = cfg->K_local;
@@ -1113,9 +1355,12 @@ int mppi_chain_ctx_create(const mppi_chain_config* cfg, int device, void* stream
     int ncu = 0, per_cu = 0;
     if ((e = hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, device)) != hipSuccess)
         return cleanup_fail(fail(MPPI_E_HIP, std::string("device attributes: ") + hipGetErrorString(e)));
-#define MPPI_OCC(N)                                                                                                   \
-    (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(                                                               \
-        &per_cu, c->f64 ? (const void*)chain_rollout_kernel<N, true, true> : (const void*)chain_rollout_kernel<N, true, false>, \
+#define MPPI_OCC(N)                                                                                          \
+    (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(                                                      \
+        &per_cu,                                                                                             \
+        c->f64 ? (const void*)chain_rollout_kernel<N, true, true, 1>                                          \
+               : (c->lps == 4 ? (const void*)chain_rollout_kernel<N, true, false, 4>                          \
+                              : (const void*)chain_rollout_kernel<N, true, false, 1>),                        \
         kCT, 0)
     MPPI_CHAIN_DISPATCH(n, MPPI_OCC)
 #undef MPPI_OCC
@@ -1198,8 +1443,9 @@ int mppi_chain_set_stream(mppi_chain_ctx* c, void* stream) {
     return MPPI_OK;
 }
 
-int mppi_chain_ctx_info(const mppi_chain_ctx* c, int* blocks, int* threads, int* poll) {
+int mppi_chain_ctx_info(const mppi_chain_ctx* c, int* blocks, int* threads, int* poll, int* lanes_per_sample) {
     if (!c) return fail(MPPI_E_ARG, "null context");
+    if (lanes_per_sample) *lanes_per_sample = c->lps;
     if (blocks) *blocks = c->nblocks;
     if (threads) *threads = kCT;
     if (poll) *poll = c->poll ? 1 : 0;
@@ -1273,10 +1519,13 @@ int mppi_chain_rollout(mppi_chain_ctx* c, const float* noise_dev, double* S_dev,
     ChainStep* nxt = c->d_step + (c->cur ^ 1);
 #define MPPI_L(N)                                                                       \
     if (c->f64) {                                                                       \
-        if (c->poll) launch_rollout<N, true, true>(c, cur, noise_dev, S_dev, partial_dev, nxt, flags); \
-        else launch_rollout<N, false, true>(c, cur, noise_dev, S_dev, partial_dev, nxt, flags); \
-    } else if (c->poll) launch_rollout<N, true, false>(c, cur, noise_dev, S_dev, partial_dev, nxt, flags); \
-    else launch_rollout<N, false, false>(c, cur, noise_dev, S_dev, partial_dev, nxt, flags)
+        if (c->poll) launch_rollout<N, true, true, 1>(c, cur, noise_dev, S_dev, partial_dev, nxt, flags); \
+        else launch_rollout<N, false, true, 1>(c, cur, noise_dev, S_dev, partial_dev, nxt, flags); \
+    } else if (c->lps == 4) {                                                           \
+        if (c->poll) launch_rollout<N, true, false, 4>(c, cur, noise_dev, S_dev, partial_dev, nxt, flags); \
+        else launch_rollout<N, false, false, 4>(c, cur, noise_dev, S_dev, partial_dev, nxt, flags); \
+    } else if (c->poll) launch_rollout<N, true, false, 1>(c, cur, noise_dev, S_dev, partial_dev, nxt, flags); \
+    else launch_rollout<N, false, false, 1>(c, cur, noise_dev, S_dev, partial_dev, nxt, flags)
     MPPI_CHAIN_DISPATCH(c->n, MPPI_L)
 #undef MPPI_L
     const hipError_t e = hipGetLastError();

@@ -12,13 +12,15 @@
 //    argmin is split over the LPS lanes of a sample and closed with DPP
 //    quad_perm min (no LDS, no MFMA: the work is element-wise VALU).  The
 //    per-step noise row eps[t][k][:] is one coalesced 8-B-per-lane load,
-//    prefetched two steps ahead.  S accumulates in fp64.
+//    prefetched four steps ahead.  S accumulates in fp64.
 //  * the block epilogue turns its samples into a log-sum-exp partial
 //    {rho_b, eta_b, N_b[T][2]} (only samples with non-zero weight are
-//    visited), publishes it with an agent-scope release + arrival counter,
-//    and the last-arriving workgroup merges every partial (agent acquire),
-//    so one launch covers control.py:81-118.  With MPPI_FLAG_FUSED_UPDATE
-//    that workgroup also applies the median filter / update / shift of
+//    visited) and publishes it write-through.  Default (grid co-resident):
+//    tagged granules polled by workgroup 0, which merges every row directly
+//    (or the first workgroup of each group of 16, then workgroup 0, when many
+//    rows carry weight); larger grids: arrival counters and the last arriver
+//    merges.  One launch covers control.py:81-118.  With MPPI_FLAG_FUSED_UPDATE
+//    the merging workgroup also applies the median filter / update / shift of
 //    control.py:122-149 into the ping-pong step block for the next launch.
 //  * merge_kernel: the same merge over the all-gathered per-device partials
 //    (multi-GPU), traj_kernel: trajectory re-roll (control.py:129-145),

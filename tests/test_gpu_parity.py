@@ -511,11 +511,10 @@ def test_config4_eight_virtual_shards(lam, paths, monkeypatch):
     and (ii) the C fp64 oracle at full size (S <= 5e-5 rel, same argmin,
     w_eps <= 1e-4).  lam = 3e6 spreads the weights over many shards.
 
-    The unsharded launch is held to the shards' 256-thread workgroups: the
-    epilogue's weights are fp32 relative to the workgroup minimum, so a different
-    workgroup partition (the default 512 threads at this K) moves w_eps by ~1e-8
-    relative, the fp32 weight rounding; with the same partition only the fp64
-    merge order differs."""
+    The unsharded launch is held to the shards' 256-thread workgroups, so the
+    two runs partition the samples the same way and only the fp64 merge order
+    differs (the weights are fp64 relative to each workgroup's minimum; another
+    partition changes the summation order only, <= 1e-10)."""
     K, T, G = 524288, 64, 8
     Kl = K // G
     u = np.array([[10.0, -2.0]] * T) + np.random.default_rng(4).normal(0, 0.5, (T, 2))
