@@ -271,6 +271,8 @@ def main():
         args.nbuf = 4 if c5 else 10
     if args.traffic_json is None:
         name = "traffic.json" if args.workload == "c3" else f"traffic_{args.workload}.json"
+        if args.K != {"c5": 131072, "c2": 4096}.get(args.workload, 65536):
+            name = f"traffic_{args.workload}_k{args.K}.json"   # e.g. config 5's 8-way shard, K = 16384
         args.traffic_json = os.path.join(ROOT, "profiles", name)
     rank = int(os.environ.get("RANK", "0"))
     world = int(os.environ.get("WORLD_SIZE", "1"))

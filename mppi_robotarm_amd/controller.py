@@ -136,6 +136,7 @@ class MPPIControllerForPathTracking:
         self.keep_costs = False        # set True to keep per-sample S (self.last_S)
         self.last_S = None
         self._bound = None             # what the engine's drop-in tick is bound to (_bind_key)
+        self._last_sampled = None      # the previous call's sampled_traj_list (_fresh_sampled)
 
     # ------------------------------------------------------------ engine
     def _shard(self):
@@ -284,6 +285,15 @@ class MPPIControllerForPathTracking:
         self._prefetch_noise(eng)
         return u[0], u, optimal_traj, sampled_traj_list
 
+    def _fresh_sampled(self) -> np.ndarray:
+        """A fresh writable zero array for sampled_traj_list (control.py:137: np.zeros each call, 134 MB at
+        K = 65536, T = 64), made while the launch runs.  The controller keeps the previous call's array until
+        now, so if the caller has dropped it, its unmapping (~12 us) also happens here, under the launch,
+        instead of in the caller after the call returns; an array the caller still holds is untouched."""
+        out = np.zeros((self.K, self.T, self.dim_x))
+        self._last_sampled = out
+        return out
+
     def _tick(self, observed_x):
         """The whole call in one native step (mppi_dropin_tick) when the buffers it
         binds are plain arrays: the fp64 nearest-waypoint update and end-of-path
@@ -326,7 +336,7 @@ class MPPIControllerForPathTracking:
             self._step_count -= 1
             print("[ERROR] Reached the end of the reference path.")
             raise IndexError
-        sampled = np.zeros((self.K, self.T, self.dim_x))   # control.py:135, allocated while the launch runs
+        sampled = self._fresh_sampled()                     # control.py:135, allocated while the launch runs
         eng.dropin_tick_wait()
         self._noise_ready = (self.seed, self._step_count)
         if self.keep_costs:
@@ -351,7 +361,7 @@ class MPPIControllerForPathTracking:
             self.last_S = self._S_dev.cpu().numpy()
         u[:] = u_new                                       # the shifted nominal, in place (aliasing kept)
         optimal_traj = traj if traj is not None else np.zeros((self.T, self.dim_x))
-        return u[0], u, optimal_traj, np.zeros((self.K, self.T, self.dim_x))
+        return u[0], u, optimal_traj, self._fresh_sampled()
 
     def _fused_step(self, eng: RolloutEngine, x0, u: np.ndarray, world: int):
         """control.py:81-152 with the update inside the launch (the multi-GPU merge

@@ -8,11 +8,12 @@ export TMPDIR=/tmp
 TAG=${1:-r01}
 O=gpurun_out/prof_$TAG; mkdir -p $O
 WL=${2:-c3}
+XA=${3:-}   # extra bench.py arguments, e.g. "--K 16384"
 # stats pass: the bench as it runs (clock settle, 1000 timed steps); PMC passes:
 # few launches, no settle (byte counts do not depend on the clock, and every
 # PMC dispatch is serialised)
-B="python3 bench.py --workload $WL --steps 1000 --warmup 100 --cpu-seconds 0"
-BP="python3 bench.py --workload $WL --steps 40 --warmup 4 --settle-ms 0 --cpu-seconds 0"
+B="python3 bench.py --workload $WL $XA --steps 1000 --warmup 100 --cpu-seconds 0"
+BP="python3 bench.py --workload $WL $XA --steps 40 --warmup 4 --settle-ms 0 --cpu-seconds 0"
 if [ "$WL" = c5 ]; then KR=chain_rollout; CA=4; else KR=rollout; CA=8; fi
 # the calibration kernel is a git-ignored build product: compile it on the box
 [ -x tools/calib_fetch ] || hipcc --offload-arch=gfx950 -O3 tools/calib_fetch.hip -o tools/calib_fetch 2>/dev/null || exit 3

@@ -1,6 +1,6 @@
 """Summarise one tools/profile_round.sh run into the committed profile files.
 
-    python tools/traffic_summary.py gpurun_out/prof_TAG profiles/TAG [K T [c3|c5]]
+    python tools/traffic_summary.py gpurun_out/prof_TAG profiles/TAG [K T [c3|c2|c5 [traffic file name]]]
 
 Reads the kernel-trace stats and the PMC passes (each counter in its own
 rocprofv3 run, as the MI355X guide prescribes), applies the measured gfx950
@@ -91,7 +91,7 @@ def main():
             # the cycles one VALU instruction occupies it (4 = the wave64 issue cadence)
             out["valu_active_frac_of_wave_time"] = sq["SQ_ACTIVE_INST_VALU"] / sq["SQ_WAVE_CYCLES"]
             out["cycles_per_valu_inst"] = 4.0 * sq["SQ_ACTIVE_INST_VALU"] / sq["SQ_INSTS_VALU"]
-    name = "traffic.json" if workload == "c3" else f"traffic_{workload}.json"
+    name = sys.argv[6] if len(sys.argv) > 6 else ("traffic.json" if workload == "c3" else f"traffic_{workload}.json")
     json.dump(out, open(os.path.join(os.path.dirname(dst.rstrip('/')), name), "w"), indent=1)
     if sq:
         gr = {}
