@@ -1,7 +1,7 @@
 """Where the drop-in's control-step latency goes (diagnostic tool, not product).
 
 MPPIControllerForPathTracking.calc_control_input at the bench's K, T with device
-noise, on the one-call tick (mppi_dropin_tick: native waypoint update, inputs
+noise, on the one-call tick (mppi_dropin_tick_launch / _wait: native waypoint update, inputs
 staged as kernel arguments, fused launch, wait, host trajectory, next noise):
 
   * closed loop: run.py's driver (harness), plant work between ticks — the
@@ -51,28 +51,34 @@ def main():
         c.calc_control_input(x)
         c.prev_waypoints_idx = 0
     eng = c._get_engine()
-    stamps = []
-    native = eng.dropin_tick
+    stamps = {}
+    launch, wait = eng.dropin_tick_launch, eng.dropin_tick_wait
 
-    def timed(*args, **kwargs):
-        t0 = time.perf_counter()
-        out = native(*args, **kwargs)
-        stamps.append((t0, time.perf_counter()))
+    def t_launch(*args):
+        stamps["l0"] = time.perf_counter()
+        out = launch(*args)
+        stamps["l1"] = time.perf_counter()
         return out
 
-    eng.dropin_tick = timed
-    whole, pre, nat, post = [], [], [], []
+    def t_wait():
+        stamps["w0"] = time.perf_counter()
+        wait()
+        stamps["w1"] = time.perf_counter()
+
+    eng.dropin_tick_launch, eng.dropin_tick_wait = t_launch, t_wait
+    whole, pre, nat, mid, wt, post = [], [], [], [], [], []
     for _ in range(n):
         c.prev_waypoints_idx = 0
         t0 = time.perf_counter()
         c.calc_control_input(x)
         t3 = time.perf_counter()
-        t1, t2 = stamps[-1]
         whole.append(t3 - t0)
-        pre.append(t1 - t0)
-        nat.append(t2 - t1)
-        post.append(t3 - t2)
-    eng.dropin_tick = native
+        pre.append(stamps["l0"] - t0)
+        nat.append(stamps["l1"] - stamps["l0"])
+        mid.append(stamps["w0"] - stamps["l1"])
+        wt.append(stamps["w1"] - stamps["w0"])
+        post.append(t3 - stamps["w1"])
+    eng.dropin_tick_launch, eng.dropin_tick_wait = launch, wait
     phases = []
     for _ in range(n):
         c.prev_waypoints_idx = 0
@@ -98,8 +104,10 @@ def main():
     print(f"K={K} T={T}, device noise, one-call drop-in tick (mppi_dropin_tick), {n} calls")
     print(f"  closed loop (run.py driver, plant between ticks) {us(closed)}")
     print(f"  back to back (no work between calls)             {us(whole)}")
-    print(f"    Python before the native call                  {us(pre)}")
-    print(f"    native call (stage, launch, wait, traj, noise) {us(nat)}")
+    print(f"    Python before the native launch                {us(pre)}")
+    print(f"    native launch (waypoint, stage, launch, noise) {us(nat)}")
+    print(f"    Python between (sampled_traj_list zeros)       {us(mid)}")
+    print(f"    native wait (+ fp64 optimal trajectory)        {us(wt)}")
     print(f"    Python after                                   {us(post)}")
     names = ["waypoint update + stage inputs (host keys)", "launch fused rollout", "queue next Philox draw",
              "wait for the rollout's outputs", "copy outputs + fp64 optimal trajectory"]
