@@ -675,11 +675,16 @@ __device__ __forceinline__ double chain_horizon_lps4(const ChainConst& c, const 
             const float la = qbc<a / 2>(elem<a>(lc)), sa = qbc<a / 2>(elem<a>(ls));
             col[a] = __builtin_elementwise_fma(splat(la), vc, __builtin_elementwise_fma(splat(sa), vs, corr[a]));
         }, std::make_integer_sequence<int, N>{});
-        float inv[N], L[N][N];
+        // with L y = r folded in as the factorization's extra column: y_j leaves as soon as column j is
+        // scaled (rows <= j of r go stale once their y is out), so the solve's chain runs beside the
+        // factorization's instead of after it; every lane keeps every y_j
+        float inv[N], L[N][N], y[N];
         unroll_seq([&](auto j_c) {
             constexpr int j = decltype(j_c)::value;
             inv[j] = __builtin_amdgcn_rsqf(qbc<j / 2>(elem<j>(col[j])));
             col[j] = col[j] * splat(inv[j]);
+            y[j] = qbc<j / 2>(elem<j>(r) * inv[j]);
+            r = __builtin_elementwise_fma(splat(-y[j]), col[j], r);
             unroll_seq([&](auto k_c) {
                 constexpr int kk = decltype(k_c)::value;
                 if constexpr (kk > j) {
@@ -688,20 +693,14 @@ __device__ __forceinline__ double chain_horizon_lps4(const ChainConst& c, const 
                 }
             }, std::make_integer_sequence<int, N>{});
         }, std::make_integer_sequence<int, N>{});
-        // L y = r on the pairs (rows <= j go stale once their y is out); every lane keeps every y_j
-        float y[N];
-        unroll_seq([&](auto j_c) {
-            constexpr int j = decltype(j_c)::value;
-            y[j] = qbc<j / 2>(elem<j>(r) * inv[j]);
-            r = __builtin_elementwise_fma(splat(-y[j]), col[j], r);
-        }, std::make_integer_sequence<int, N>{});
-        // L^T x = y, redundantly in every lane from the broadcast values
+        // L^T x = y, redundantly in every lane from the broadcast values; the oldest x first, so each
+        // x_i waits on x_{i+1} through one fma and one multiply
         float x[N];
 #pragma unroll
         for (int i = N - 1; i >= 0; --i) {
             float e = y[i];
 #pragma unroll
-            for (int kk = i + 1; kk < N; ++kk) e = fmaf(-L[kk][i], x[kk], e);
+            for (int kk = N - 1; kk > i; --kk) e = fmaf(-L[kk][i], x[kk], e);
             x[i] = e * inv[i];
         }
         auto xs = [&](int i) { return i >= 0 && i < N ? x[i] : 0.f; };   // i compile-time below

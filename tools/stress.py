@@ -50,3 +50,9 @@ ch = ChainEngine(131072, 128, 0.006, 100.0, 0.98, CHAIN7_SIGMA, [0.5, 0.5, 5, 5]
 run(ch, max(1, n // 10), CHAIN7_X0, np.tile(gravity_torque(CHAIN7_X0[:7]), (128, 1)), "c5 K=131072 T=128", chunk=200,
     reset=32)
 ch.close()
+# config 5's 8-way shard: a quad per sample
+ch = ChainEngine(16384, 128, 0.006, 100.0, 0.98, CHAIN7_SIGMA, [0.5, 0.5, 5, 5], [5, 5, 50, 50], 0.0, device=0)
+assert ch.lanes_per_sample == 4
+run(ch, max(1, n // 10), CHAIN7_X0, np.tile(gravity_torque(CHAIN7_X0[:7]), (128, 1)), "c5 shard K=16384 T=128 (quad)",
+    chunk=200, reset=32)
+ch.close()
