@@ -283,10 +283,20 @@ def main():
         args.backend = default_backend(world)
     if world > 1:
         import torch.distributed as dist
-        if args.backend == "nccl":
-            dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
-        else:
-            dist.init_process_group(args.backend)
+        # the process-group set-up may print to stdout (gloo's "Rank n is connected" lines); rank 0's stdout
+        # carries only the JSON line, so the set-up's fd 1 goes to stderr
+        sys.stdout.flush()
+        saved = os.dup(1)
+        os.dup2(2, 1)
+        try:
+            if args.backend == "nccl":
+                dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
+            else:
+                dist.init_process_group(args.backend)
+            dist.barrier()
+        finally:
+            os.dup2(saved, 1)
+            os.close(saved)
     T = args.T
     path = np.load(os.path.join(ROOT, "tests", "golden", "paths.npz"))["xydq_circle"][:, :4]
     window = path[0:30]
