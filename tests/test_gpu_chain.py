@@ -383,3 +383,30 @@ def test_chain_lanes_per_sample_agree(paths):
     assert float(np.percentile(rel, 99)) < 1e-4
     assert _urel(out[4][1], out[1][1]) < U_TOL
     assert _engine(16384, 8).lanes_per_sample == 4 and _engine(131072, 8).lanes_per_sample == 1
+
+
+@pytest.mark.parametrize("T", [1, 2, 3])
+@pytest.mark.parametrize("precision,lps", [("f32", 1), ("f32", 4), ("f64", 1)])
+def test_chain_short_horizons(T, precision, lps, paths):
+    """Horizons shorter than the prefetch rings and the 2- / 4-step unrolls (the remainder steps alone), ragged K,
+    against the C fp64 chain oracle."""
+    K, lam = 999, 100.0
+    _, x0, sig, ug = _c5()
+    win = paths["xydq_circle"][:30]
+    u = np.tile(ug, (T, 1)) + np.random.default_rng(T).normal(0, 0.3, (T, 7))
+    eng = _engine(K, T, lam, precision=precision, lanes_per_sample=lps)
+    eng.set_step_inputs(x0, win, u)
+    noise = eng.philox_noise(21, T)
+    S_dev = torch.empty(K, dtype=torch.float64, device="cuda")
+    eng.rollout(noise, S_out=S_dev)
+    w = eng.weighted_noise()
+    S = S_dev.cpu().numpy()
+    nz = noise.cpu().numpy()
+    eng.close()
+    Sr = coracle.chain_rollout_costs(x0, u, nz, win, 0.006, lam, 0.98, sig, W, TW, CO.ChainParams(), layout="TNK")
+    _, wr = coracle.chain_weighted_noise(Sr, nz, lam, layout="TNK")
+    rel = np.abs(S - Sr) / np.abs(Sr)
+    bound = 1e-11 if precision == "f64" else 1e-5
+    assert int(np.argmin(S)) == int(np.argmin(Sr))
+    assert float(np.percentile(rel, 99)) < bound
+    assert _urel(w, wr) < (1e-10 if precision == "f64" else U_TOL)

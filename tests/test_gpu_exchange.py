@@ -98,7 +98,7 @@ def test_exchange_flag_needs_attach():
 CK, CT = 6144, 16
 
 
-def _chain_rank(rank, world, port, out):
+def _chain_rank(rank, world, port, out, precision="f32", lps=0):
     import torch.distributed as dist
     from mppi_robotarm_amd.chain import CHAIN7_SIGMA, CHAIN7_X0, ChainEngine, gravity_torque
     from mppi_robotarm_amd.distributed import attach_exchange, shard_geometry
@@ -108,7 +108,7 @@ def _chain_rank(rank, world, port, out):
         torch.cuda.set_device(0)
         n, off = shard_geometry(CK, world, rank)
         eng = ChainEngine(n, CT, 0.006, 1.0e5, 0.98, CHAIN7_SIGMA, [0.5, 0.5, 5, 5], [5, 5, 50, 50],
-                          K_total=CK, k_offset=off, device=0)
+                          K_total=CK, k_offset=off, device=0, precision=precision, lanes_per_sample=lps)
         _, win, _ = _inputs()
         eng.set_step_inputs(CHAIN7_X0, win, np.tile(gravity_torque(CHAIN7_X0[:7]), (CT, 1)))
         attach_exchange(eng)
@@ -122,16 +122,20 @@ def _chain_rank(rank, world, port, out):
         dist.destroy_process_group()
 
 
-def test_chain_exchange_two_ranks_match_unsharded(tmp_path):
-    """Config 5's multi-GPU step: (2 + 7T) rows exchanged inside the launch."""
+@pytest.mark.parametrize("precision,lps", [("f32", 1), ("f32", 4), ("f64", 1)])
+def test_chain_exchange_two_ranks_match_unsharded(precision, lps, tmp_path):
+    """Config 5's multi-GPU step: (2 + 7T) rows exchanged inside the launch, for one lane and a quad per sample
+    and for the fp64 rollout."""
     import torch.multiprocessing as mp
     from mppi_robotarm_amd.chain import CHAIN7_SIGMA, CHAIN7_X0, ChainEngine, gravity_torque
     torch.cuda.set_device(0)
     out = str(tmp_path / "c")
-    mp.start_processes(_chain_rank, args=(2, _free_port(), out), nprocs=2, join=True, start_method="spawn")
+    mp.start_processes(_chain_rank, args=(2, _free_port(), out, precision, lps), nprocs=2, join=True,
+                       start_method="spawn")
     r0, r1 = np.load(out + ".0.npy"), np.load(out + ".1.npy")
     assert np.array_equal(r0, r1)
-    full = ChainEngine(CK, CT, 0.006, 1.0e5, 0.98, CHAIN7_SIGMA, [0.5, 0.5, 5, 5], [5, 5, 50, 50], device=0)
+    full = ChainEngine(CK, CT, 0.006, 1.0e5, 0.98, CHAIN7_SIGMA, [0.5, 0.5, 5, 5], [5, 5, 50, 50], device=0,
+                       precision=precision, lanes_per_sample=lps)
     _, win, _ = _inputs()
     full.set_step_inputs(CHAIN7_X0, win, np.tile(gravity_torque(CHAIN7_X0[:7]), (CT, 1)))
     for s in range(STEPS):
