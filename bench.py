@@ -205,32 +205,36 @@ def cpu_baseline_c5(args, window, x0, u, K, T):
             "cores_available": avail, "os_cpu_count": os.cpu_count()}
 
 
-def dropin_latency(K, T, device, ticks=100):
+def dropin_latency(K, T, device, ticks=200, warm=100):
     """SURVEY §8(d)'s control-step latency: the wall time of the drop-in's
     calc_control_input, median over a closed loop of run.py's driver
     (mppi_robotarm_amd.harness, the plant stepped on the host between ticks) at
     the bench's K and T, plus the same calls back to back (nothing between them,
-    so each call also waits for the previous call's noise draw)."""
+    so each call also waits for the previous call's noise draw).  Steady state:
+    a first closed loop of `warm` ticks and the first `warm` back-to-back calls
+    are not counted (the first ~100 calls of a process run 10-20% slower:
+    tools/lat_compare.py)."""
     from mppi_robotarm_amd.harness import run_closed_loop
     from mppi_robotarm_amd.controller import MPPIControllerForPathTracking
     from mppi_robotarm_amd.params import runpy_config
     path = np.load(os.path.join(ROOT, "tests", "golden", "paths.npz"))["xydq_circle"][:, :4]
-    rec = run_closed_loop(path, ticks=ticks, number_of_samples_K=K, horizon_step_T=T, noise="device", seed=0,
-                          verbose=False, visualze_sampled_trajs=False, device=device)
-    rec["controller"].close()
+    for n in (warm, ticks):
+        rec = run_closed_loop(path, ticks=n, number_of_samples_K=K, horizon_step_T=T, noise="device", seed=0,
+                              verbose=False, visualze_sampled_trajs=False, device=device)
+        rec["controller"].close()
     lat = rec["latency_s"][3:] * 1e3
     kw = runpy_config()
     kw.update(number_of_samples_K=K, horizon_step_T=T, visualze_sampled_trajs=False)
     c = MPPIControllerForPathTracking(ref_path=path, noise="device", seed=0, verbose=False, device=device, **kw)
     x = X0_RUNPY.copy()
     b2b = []
-    for i in range(ticks):
+    for i in range(warm + ticks):
         c.prev_waypoints_idx = 0
         t0 = time.perf_counter()
         c.calc_control_input(x)
         b2b.append(time.perf_counter() - t0)
     c.close()
-    b2b = np.array(b2b[3:]) * 1e3
+    b2b = np.array(b2b[warm:]) * 1e3
     return float(np.median(lat)), float(np.percentile(lat, 90)), float(np.median(b2b))
 
 
@@ -509,7 +513,8 @@ def main():
                 "weighted noise, median filter, update, shift), wait on its host-mapped result, fp64 optimal "
                 "trajectory on the host; the next tick's Philox draw is queued behind the launch and overlaps the "
                 "plant step between ticks. back_to_back: the same calls with nothing between them (each then "
-                "also waits for the previous draw). ms_per_step is the device-resident loop")
+                "also waits for the previous draw). Steady state: 200 ticks each, after 100 uncounted. "
+                "ms_per_step is the device-resident loop")
         if world == 1 and args.cpu_seconds > 0:
             out["cpu_baseline"] = (cpu_baseline_c5(args, window, x0, u, K, T) if c5
                                    else cpu_baseline(args, window, x0, u))

@@ -137,6 +137,7 @@ class MPPIControllerForPathTracking:
         self.last_S = None
         self._bound = None             # what the engine's drop-in tick is bound to (_bind_key)
         self._last_sampled = None      # the previous call's sampled_traj_list (_fresh_sampled)
+        self._fast = None              # what the last bound tick checked (calc_control_input's fast test)
 
     # ------------------------------------------------------------ engine
     def _shard(self):
@@ -215,6 +216,12 @@ class MPPIControllerForPathTracking:
     # ------------------------------------------------------------ API
     def calc_control_input(self, observed_x: np.ndarray) -> Tuple[float, np.ndarray]:
         """calculate optimal control input (control.py:67-152)"""
+        f = self._fast
+        if (f is not None and f[0] is self.ref_path and f[1] is self.u_prev and f[2] is self.Sigma
+                and f[3] is self.stage_cost_weight and f[4] is self.terminal_cost_weight and f[5] is self._engine
+                and f[6] == self._fast_scalars() and f[7] == self.Sigma.tobytes()
+                and f[8] == self.stage_cost_weight.tobytes() and f[9] == self.terminal_cost_weight.tobytes()):
+            return self._tick_bound(observed_x)
         if (self.noise_source == "device" and not self.host_update and not self.visualze_sampled_trajs
                 and (self.process_group is None or self._xmode == "launch") and self.K >= 1):
             out = self._tick(observed_x)
@@ -321,13 +328,38 @@ class MPPIControllerForPathTracking:
             eng.dropin_bind(path, float(self.l1), float(self.l2), self._x_buf, self._idx_buf, u, self._traj_buf,
                             self._noise_dev, self._noise_dev, self._S_dev if self.keep_costs else None, self.seed)
             self._bound = bkey
-        self._x_buf[:] = np.asarray(observed_x, dtype=np.float64).ravel()[:4]
-        self._idx_buf[0] = self.prev_waypoints_idx
         if self._noise_ready != (self.seed, self._step_count):
             eng.philox_noise(self.seed, self._step_count, out=self._noise_dev)
+        out = self._tick_bound(observed_x)
+        # the next call may skip every check above while nothing they read has changed
+        # (the same objects, scalars and array contents): calc_control_input's fast test
+        if all(isinstance(a, np.ndarray) and a.dtype == np.float64
+               for a in (self.Sigma, self.stage_cost_weight, self.terminal_cost_weight)):
+            self._fast = (path, u, self.Sigma, self.stage_cost_weight, self.terminal_cost_weight, eng,
+                          self._fast_scalars(), self.Sigma.tobytes(), self.stage_cost_weight.tobytes(),
+                          self.terminal_cost_weight.tobytes())
+        return out
+
+    def _fast_scalars(self):
+        """Every scalar _tick's checks and the engine key read (control.py's per-call reads of
+        lambda, gamma, the exploration split, delta_t, l1/l2), plus the controller switches."""
+        return (self.noise_source, self.host_update, self.visualze_sampled_trajs, self.process_group, self.K,
+                self.param_lambda, self.param_gamma, self.param_exploration, self.delta_t, self.l1, self.l2,
+                self.arm, self.seed, self.keep_costs, self.visualize_optimal_traj, self.verbose,
+                self._noise_ready == (self.seed, self._step_count))
+
+    def _tick_bound(self, observed_x):
+        """The bound drop-in tick (engine built, buffers bound, the noise of this step in
+        the buffer): stage x0 and the index, launch, allocate sampled_traj_list, wait."""
+        eng = self._engine
+        if type(observed_x) is np.ndarray and observed_x.shape == (4,):
+            self._x_buf[:] = observed_x
+        else:
+            self._x_buf[:] = np.asarray(observed_x, dtype=np.float64).ravel()[:4]
+        self._idx_buf[0] = self.prev_waypoints_idx
         self._step_count += 1
         rc = eng.dropin_tick_launch(self._step_count)
-        self.prev_waypoints_idx = int(self._idx_buf[0])
+        self.prev_waypoints_idx = self._idx_buf.item(0)
         if self.verbose:
             print(f"0     prev_idx = {int(self._idx_buf[1])}")
             print(f"0     nearest_idx = {self.prev_waypoints_idx}")
@@ -342,6 +374,7 @@ class MPPIControllerForPathTracking:
         if self.keep_costs:
             self.last_S = self._S_dev.cpu().numpy()
         traj = self._traj_buf.copy() if self._traj_buf is not None else np.zeros((self.T, self.dim_x))
+        u = self.u_prev
         return u[0], u, traj, sampled
 
     def _dropin_step(self, eng: RolloutEngine, x0, window, u: np.ndarray):
@@ -453,4 +486,5 @@ class MPPIControllerForPathTracking:
         self._noise_ready = None       # the next engine's noise buffer is fresh: draw again
         self._engine_built_for = None
         self._bound = None
+        self._fast = None
         self._xmode = None

@@ -1144,11 +1144,12 @@ int wait_host_out(mppi_ctx* c) {
 // optimal trajectory of a drop-in step (control.py:129-134), O(T) host work.
 void host_F(const mppi_arm_params& a, double dt, double* x, double u1, double u2) {
     const double q1 = x[0], q2 = x[1], dq1 = x[2], dq2 = x[3];
-    const double c2 = cos(q2);
+    double s2, c2;
+    sincos(q2, &s2, &c2);   // glibc: the same values as sin() and cos()
     const double M11 = a.m1 * a.lc1 * a.lc1 + a.l1 + a.m2 * (a.l1 * a.l1 + a.lc2 * a.lc2 + 2 * a.l1 * a.lc2 * c2) + a.l2;
     const double M22 = a.m2 * a.lc2 * a.lc2 + a.l2;
     const double M12 = a.m2 * a.l1 * a.lc2 * c2 + a.m2 * a.lc2 * a.lc2 + a.l2;
-    const double h = a.m2 * a.l1 * a.lc2 * sin(q2);
+    const double h = a.m2 * a.l1 * a.lc2 * s2;
     const double c1 = cos(q1), c12 = cos(q1 + q2);   // each evaluated once (the reference evaluates them twice)
     const double g1 = a.m1 * a.lc1 * a.g * c1 + a.m2 * a.g * (a.lc2 * c12 + a.l1 * c1);
     const double g2 = a.m2 * a.lc2 * a.g * c12;

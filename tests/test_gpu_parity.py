@@ -686,6 +686,54 @@ def test_bound_tick_equals_general_dropin(paths):
     slow.close()
 
 
+def test_fast_tick_sees_every_per_call_read(paths):
+    """calc_control_input's fast test (the last bound tick's objects, scalars and
+    array contents unchanged -> straight to the launch) against a controller that
+    runs every check on every call, bit for bit, while the caller edits what the
+    reference re-reads per call between ticks: Sigma in place and rebound
+    (control.py:84,106), lambda (:112), the stage weights in place (:185), the
+    exploration split (:98), the seed (device noise), prev_waypoints_idx and
+    ref_path rebound."""
+    from mppi_robotarm_amd.controller import MPPIControllerForPathTracking
+    base = paths["xydq_circle"][:400].copy()
+    kw = dict(delta_t=0.006, horizon_step_T=16, number_of_samples_K=2048, verbose=False, noise="device", seed=3,
+              device=0, **RUNPY)
+    fast = MPPIControllerForPathTracking(ref_path=base[:, 0:4], **kw)
+    full = MPPIControllerForPathTracking(ref_path=base[:, 0:4], **kw)
+    for c in (fast, full):
+        c.Sigma = np.array(c.Sigma, dtype=np.float64)
+        c.stage_cost_weight = np.array(c.stage_cost_weight, dtype=np.float64)
+        c.terminal_cost_weight = np.array(c.terminal_cost_weight, dtype=np.float64)
+    edits = {
+        3: lambda c: c.Sigma.__setitem__((0, 0), c.Sigma[0, 0] * 1.5),
+        6: lambda c: setattr(c, "param_lambda", 40.0),
+        9: lambda c: c.stage_cost_weight.__setitem__(1, 3.0),
+        12: lambda c: setattr(c, "Sigma", np.array([[12.0, 3.0], [3.0, 25.0]])),
+        15: lambda c: setattr(c, "param_exploration", 0.25),
+        18: lambda c: setattr(c, "seed", 11),
+        21: lambda c: setattr(c, "prev_waypoints_idx", c.prev_waypoints_idx + 3),
+        24: lambda c: setattr(c, "ref_path", base[:, 0:4].copy()),
+    }
+    slow_calls = []
+    tick_checked = fast._tick
+    fast._tick = lambda x: (slow_calls.append(1), tick_checked(x))[1]   # every call but the fast test's
+    x = X0.copy()
+    n = 27
+    for tick in range(n):
+        if tick in edits:
+            for c in (fast, full):
+                edits[tick](c)
+        full._fast = None                            # every check, every call
+        ua, _, oa, _ = fast.calc_control_input(x)
+        ub, _, ob, _ = full.calc_control_input(x)
+        assert fast.prev_waypoints_idx == full.prev_waypoints_idx, tick
+        assert np.array_equal(fast.u_prev, full.u_prev) and np.array_equal(oa, ob), tick
+        x = oa[4].copy()
+    assert n - len(slow_calls) >= 8                  # the fast test really passed between the edits
+    fast.close()
+    full.close()
+
+
 def test_tick_nearest_waypoint_follows_python_min_on_nan_rows(paths):
     """The native tick's waypoint update (mppi_dropin_tick) takes d.index(min(d))
     like the reference (control.py:212-215) and the host path: a NaN row after
