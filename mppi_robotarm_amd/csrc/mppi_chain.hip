@@ -1165,7 +1165,7 @@ struct mppi_chain_ctx {
     double* h_buf = nullptr;
     float* d_base = nullptr;
     float* h_base = nullptr;
-    float* d_chol = nullptr;       // Cholesky factor of Sigma (kCMax x kCMax, fp32) for the Philox noise
+    float* d_chol = nullptr;       // Cholesky factor of Sigma x kBoxMullerScale (kCMax x kCMax, fp32) for the Philox noise
     float* d_dyn = nullptr;        // packed per-step constants (DynMem), then the same in fp64 at kDynF64Off
     bool f64 = false;              // cfg.precision == 1
     int lps = 1;                   // lanes per sample: 1, or 4 (fp32 rollout at small K)
@@ -1379,7 +1379,7 @@ int mppi_chain_ctx_create(const mppi_chain_config* cfg, int device, void* stream
     c->kc.fair = c->nblocks > ncu ? 1 : 0;
     float chol[kCMax * kCMax] = {};
     for (int i = 0; i < n; ++i)
-        for (int j = 0; j <= i; ++j) chol[i * kCMax + j] = (float)Lc[i][j];
+        for (int j = 0; j <= i; ++j) chol[i * kCMax + j] = (float)(Lc[i][j] * kBoxMullerScale);   // box_muller's constant
     if ((e = hipMalloc(&c->d_step, 2 * sizeof(ChainStep))) != hipSuccess ||
         (e = hipMalloc(&c->d_slab, slab)) != hipSuccess || (e = hipMalloc(&c->d_gslab, gslab)) != hipSuccess ||
         (e = hipMalloc(&c->d_counter, ctr_bytes)) != hipSuccess ||

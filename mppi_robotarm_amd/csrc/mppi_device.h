@@ -940,11 +940,18 @@ __device__ __forceinline__ uint4 philox4x32_10(uint4 ctr, uint2 key) {
 // Two standard normals from two 32-bit uniforms (Box-Muller) on the hardware
 // transcendentals: v_log_f32 (log2), v_sqrt_f32, and v_sin_f32 / v_cos_f32, whose
 // input is in revolutions — exactly u1, so no 2 pi scaling and no range
-// reduction.  u0 lies in [2^-32, 1], a normal float: no denormal path.
+// reduction.  Returned WITHOUT the constant sqrt(2 ln 2) (kBoxMullerScale): the
+// callers fold it into their Cholesky factor, so the value is
+//   sqrt(-log2 u0) (cos 2 pi u1, sin 2 pi u1) = z / sqrt(2 ln 2).
+// u0 = (a + 1) 2^-32 in [2^-32, 1] (a normal float: no denormal path) is one fma:
+// scaling by 2^-32 is exact, so fma(a, 2^-32, 2^-32) rounds the same real as
+// (float(a) + 1) * 2^-32, and it never exceeds 1 (float(a) <= 2^32, and 2^32 + 1
+// rounds to 2^32), so no clamp.  The negation of log2 u0 <= 0 is a source modifier.
+constexpr double kBoxMullerScale = 1.1774100225154747;   // sqrt(2 ln 2)
 __device__ __forceinline__ float2 box_muller(unsigned a, unsigned b) {
     const float inv = 2.3283064365386963e-10f;  // 2^-32
-    const float u0 = fminf(((float)a + 1.0f) * inv, 1.0f), u1 = (float)b * inv;
-    const float r = __builtin_amdgcn_sqrtf(-1.3862943611198906f * __builtin_amdgcn_logf(u0));   // -2 ln 2 log2 u0
+    const float u0 = fmaf((float)a, inv, inv), u1 = (float)b * inv;
+    const float r = __builtin_amdgcn_sqrtf(-__builtin_amdgcn_logf(u0));
     return make_float2(r * __builtin_amdgcn_cosf(u1), r * __builtin_amdgcn_sinf(u1));
 }
 

@@ -729,7 +729,8 @@ __global__ __launch_bounds__(kThreads) void nearest_debug_kernel(const KConst c,
     }
 }
 
-// Philox4x32-10 + Box-Muller (mppi_device.h); eps = L z, L = chol(Sigma).
+// Philox4x32-10 + Box-Muller (mppi_device.h); eps = L z, L = chol(Sigma) (the
+// arguments carry L x kBoxMullerScale, box_muller's constant).
 // Grid (ceil(K_local / kThreads), ceil(T / 2)): blockIdx.y is the step pair, so
 // no 64-bit divide per thread (it was ~half the kernel's instructions).
 __global__ __launch_bounds__(kThreads) void philox_noise_kernel(int K_local, int T, long long k_offset,
@@ -1524,9 +1525,10 @@ int mppi_noise_philox(mppi_ctx* c, unsigned long long seed, unsigned long long s
     const double L00 = sqrt(S[0]), L10 = s01 / L00, d = S[3] - L10 * L10;
     if (!(d >= 0.0)) return fail(MPPI_E_ARG, "Sigma not positive semi-definite");
     const double L11 = sqrt(d);
+    constexpr double bm = kBoxMullerScale;   // box_muller's constant, folded into L
     const dim3 grid((unsigned)((c->cfg.K_local + kThreads - 1) / kThreads), (unsigned)((c->cfg.T + 1) / 2));
     hipLaunchKernelGGL(philox_noise_kernel, grid, dim3(kThreads), 0, c->stream, c->cfg.K_local,
-                       c->cfg.T, (long long)c->cfg.k_offset, seed, step, (float)L00, (float)L10, (float)L11,
+                       c->cfg.T, (long long)c->cfg.k_offset, seed, step, (float)(L00 * bm), (float)(L10 * bm), (float)(L11 * bm),
                        reinterpret_cast<float2*>(out_dev));
     return launch_check("philox_noise_kernel");
 }
