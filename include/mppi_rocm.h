@@ -347,6 +347,12 @@ int mppi_chain_noise_philox(mppi_chain_ctx *ctx, unsigned long long seed, unsign
                             float *out_dev);
 int mppi_chain_sync(mppi_chain_ctx *ctx);
 int mppi_chain_debug_set_buffer(mppi_chain_ctx *ctx, void *dbg_dev);
+/* Tests only: one rollout (as mppi_chain_rollout with no flags; S_dev nullable)
+ * through a build of the same kernel that also records the window slot every
+ * sample picked at every step (the argmin of control.py:205-215 inside _c),
+ * slots_dev int32 [K_local][T].  7-link contexts only.  The parity tests use it
+ * to recompute a sample's fp64 cost with the device's own picks. */
+int mppi_chain_debug_slots(mppi_chain_ctx *ctx, const float *noise_dev, double *S_dev, int *slots_dev);
 
 #ifdef __cplusplus
 }

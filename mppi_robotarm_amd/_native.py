@@ -41,7 +41,7 @@ EXPORTS = (
     "mppi_chain_set_step_inputs", "mppi_chain_rollout", "mppi_chain_merge_partials", "mppi_chain_exchange_handle",
     "mppi_chain_exchange_attach",
     "mppi_chain_get_weighted_noise", "mppi_chain_get_nominal", "mppi_chain_rollout_traj",
-    "mppi_chain_noise_philox", "mppi_chain_sync", "mppi_chain_debug_set_buffer",
+    "mppi_chain_noise_philox", "mppi_chain_sync", "mppi_chain_debug_set_buffer", "mppi_chain_debug_slots",
 )
 
 
@@ -148,6 +148,7 @@ def open_library(path: str):
         "mppi_chain_noise_philox": ([vp, C.c_ulonglong, C.c_ulonglong, fp], C.c_int),
         "mppi_chain_sync": ([vp], C.c_int),
         "mppi_chain_debug_set_buffer": ([vp, vp], C.c_int),
+        "mppi_chain_debug_slots": ([vp, fp, vp, vp], C.c_int),
     }
     for name, (args, res) in sig.items():
         if not hasattr(L, name):   # an older diagnostic build (tools/ab.py); load() checks the product's exports

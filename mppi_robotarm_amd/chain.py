@@ -261,6 +261,20 @@ class ChainEngine:
         self._keep_traj = bu
         return out
 
+    def debug_slots(self, noise: torch.Tensor, S_out: torch.Tensor | None = None) -> np.ndarray:
+        """Tests: one rollout (as rollout(noise, S_out)) through the slot-recording build of the
+        kernel -> the window slot every sample picked at every step, (K_local, T) int32
+        (mppi_chain_debug_slots; the 7-link chain only)."""
+        self._sync_stream()
+        self._check_noise(noise)
+        if S_out is not None:
+            assert S_out.dtype == torch.float64 and S_out.numel() >= self.K_local and S_out.device == self.device
+        slots = torch.full((self.K_local, self.T), -1, dtype=torch.int32, device=self.device)
+        N.check(self._lib.mppi_chain_debug_slots(self._ctx, C.c_void_p(noise.data_ptr()),
+                                                 C.c_void_p(S_out.data_ptr()) if S_out is not None else None,
+                                                 C.c_void_p(slots.data_ptr())), "mppi_chain_debug_slots")
+        return slots.cpu().numpy()
+
     def philox_noise(self, seed: int, step: int = 0, out: torch.Tensor | None = None) -> torch.Tensor:
         self._sync_stream()
         out = self.new_noise() if out is None else out

@@ -35,6 +35,7 @@ namespace {
 using namespace mppi;
 
 constexpr int kCMax = MPPI_CHAIN_MAX_DOF;   // links
+constexpr int kCDebugN = 7;                  // the link count with slot-recording debug instances (config 5)
 constexpr int kCT = 256;                    // threads per workgroup, one lane per sample
 constexpr int kCMaxCh = 4;                  // column chunks of a partial row: T N + 1 <= 4 x 256 ... (N <= 7)
 constexpr int kCMaxVals = kMaxT * kCMax;    // T N values per row, at most
@@ -474,7 +475,8 @@ struct alignas(16) WinRowD {
 };
 template <int N>
 __device__ __forceinline__ double chain_horizon_f64(const ChainConst& c, const ChainStep* st, cdouble* kd,
-                                                    const float* noise, int k, float exf, WinRowD* s_wind) {
+                                                    const float* noise, int k, float exf, WinRowD* s_wind,
+                                                    int* slots) {
     const int tid = threadIdx.x, K = c.K_local, T = c.T;
     if (tid < kSlots) {
         const double* r = st->wind[tid];
@@ -514,6 +516,7 @@ __device__ __forceinline__ double chain_horizon_f64(const ChainConst& c, const C
                 best = j;
             }
         }
+        if (slots) slots[(size_t)k * T + t] = best;   // debug instances only (mppi_chain_debug_slots)
         const WinRowD r = s_wind[best];
         ex = px - r.x;
         ey = py - r.y;
@@ -575,7 +578,7 @@ __device__ __forceinline__ float elem(f32x2 v) {
 template <int N>
 __device__ __forceinline__ double chain_horizon_lps4(const ChainConst& c, const ChainStep* st, const float* dyn,
                                                      const float* noise, int k, float exf, float4* s_ua4,
-                                                     float4* s_win) {
+                                                     float4* s_win, int* slots) {
     static_assert(N <= 8, "four link pairs");
     const int tid = threadIdx.x, sub = tid & 3, K = c.K_local, T = c.T;
     if (tid < kSlots) s_win[tid] = st->win[tid];
@@ -715,7 +718,9 @@ __device__ __forceinline__ double chain_horizon_lps4(const ChainConst& c, const 
         // ---- end effector, nearest waypoint, stage cost (control.py:174-198)
         const f32x2 fx = fk2 * C, fy = fk2 * Sn;
         const float px = q_sum(fx.x + fx.y), py = q_sum(fy.x + fy.y);
-        const float4 rw = s_win[sr.nearest(px, py)];
+        const unsigned j = sr.nearest(px, py);
+        if (slots && sub == 0) slots[(size_t)k * T + t] = (int)j;   // debug instances only
+        const float4 rw = s_win[j];
         ex = px - rw.x;
         ey = py - rw.y;
         e1 = qbc<0>(DQ.x) - rw.z;
@@ -740,7 +745,9 @@ __device__ __forceinline__ double chain_horizon_lps4(const ChainConst& c, const 
 }
 
 // POLL / counter hand-off and the merges as in rollout_kernel (mppi_rocm.hip).
-template <int N, bool POLL, bool F64, int LPS>
+// SLOTS (debug instances, mppi_chain_debug_slots): dbg receives the window slot
+// each sample picked at each step, int32 [k][t].
+template <int N, bool POLL, bool F64, int LPS, bool SLOTS = false>
 __global__ __launch_bounds__(kCT) __attribute__((amdgpu_waves_per_eu(2, 2))) void chain_rollout_kernel(
     const ChainConst c, const ChainStep* __restrict__ st, const float* __restrict__ dyn,
     const float* __restrict__ noise, double* __restrict__ S_out, double* __restrict__ slab, double* __restrict__ gslab,
@@ -770,6 +777,7 @@ __global__ __launch_bounds__(kCT) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
     const int k = valid ? k_raw : c.K_local - 1;
     const float exf = (c.k_offset + k) < c.k_exploit ? 1.f : 0.f;  // control.py:98-101
     const int K = c.K_local, T = c.T;
+    int* const slots = SLOTS ? reinterpret_cast<int*>(dbg) : nullptr;
 
     STAMP(0, NOW());
 #ifdef MPPI_STAMPS
@@ -785,9 +793,9 @@ __global__ __launch_bounds__(kCT) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
     }
     double S = 0.0;
     if constexpr (F64) {
-        S = chain_horizon_f64<N>(c, st, (cdouble*)(dyn + kDynF64Off), noise, k, exf, s_wind);
+        S = chain_horizon_f64<N>(c, st, (cdouble*)(dyn + kDynF64Off), noise, k, exf, s_wind, slots);
     } else if constexpr (LPS == 4) {
-        S = chain_horizon_lps4<N>(c, st, dyn, noise, k, exf, s_ua4, s_win);
+        S = chain_horizon_lps4<N>(c, st, dyn, noise, k, exf, s_ua4, s_win, slots);
     } else {
     if (tid < kSlots) s_win[tid] = st->win[tid];
     // window keys in LDS (broadcast reads): the 90 key registers would cost the
@@ -849,7 +857,9 @@ __global__ __launch_bounds__(kCT) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
         x.step(v, kd);
         float px, py;
         x.effector(kd, &px, &py);
-        const float4 r = s_win[sr.nearest(px, py)];
+        const unsigned j = sr.nearest(px, py);
+        if constexpr (SLOTS) slots[(size_t)k * T + t] = (int)j;
+        const float4 r = s_win[j];
         ex = px - r.x;
         ey = py - r.y;
         e1 = x.dqa(0) - r.z;
@@ -1187,7 +1197,14 @@ using mppi_host::fail;
 
 template <int N, bool P, bool F64, int LPS>
 void launch_rollout(mppi_chain_ctx* c, const ChainStep* cur, const float* noise, double* S, double* part, ChainStep* nxt,
-                    unsigned flags) {
+                    unsigned flags, int* slots = nullptr) {
+    if (slots) {   // the debug instance: identical arithmetic, plus the slot stores
+        if constexpr (N == kCDebugN)
+            hipLaunchKernelGGL((chain_rollout_kernel<N, P, F64, LPS, true>), dim3(c->nblocks), dim3(kCT), 0, c->stream, c->kc,
+                               cur, c->d_dyn, noise, S, c->d_slab, c->d_gslab, c->d_counter, part, c->d_weps, nxt, flags,
+                               c->xd, c->d_epoch, c->d_tmo, c->d_runmin, reinterpret_cast<unsigned long long*>(slots));
+        return;
+    }
     hipLaunchKernelGGL((chain_rollout_kernel<N, P, F64, LPS>), dim3(c->nblocks), dim3(kCT), 0, c->stream, c->kc, cur, c->d_dyn,
                        noise, S, c->d_slab, c->d_gslab, c->d_counter, part, c->d_weps, nxt, flags, c->xd, c->d_epoch, c->d_tmo,
                        c->d_runmin, c->d_dbg);
@@ -1505,7 +1522,12 @@ int mppi_chain_set_step_inputs(mppi_chain_ctx* c, const double* x0, const double
     return MPPI_OK;
 }
 
-int mppi_chain_rollout(mppi_chain_ctx* c, const float* noise_dev, double* S_dev, double* partial_dev, unsigned flags) {
+}  // extern "C"
+
+namespace {
+// slots: the debug instances (kCDebugN links) record every sample's window slot per step
+int chain_rollout(mppi_chain_ctx* c, const float* noise_dev, double* S_dev, double* partial_dev, unsigned flags,
+                  int* slots) {
     if (!c || !noise_dev) return fail(MPPI_E_ARG, "null argument");
     if ((flags & MPPI_FLAG_FUSED_UPDATE) && c->cfg.T < 5)
         return fail(MPPI_E_ARG, "device median filter needs T >= 5 (use the host update)");
@@ -1518,13 +1540,13 @@ int mppi_chain_rollout(mppi_chain_ctx* c, const float* noise_dev, double* S_dev,
     ChainStep* nxt = c->d_step + (c->cur ^ 1);
 #define MPPI_L(N)                                                                       \
     if (c->f64) {                                                                       \
-        if (c->poll) launch_rollout<N, true, true, 1>(c, cur, noise_dev, S_dev, partial_dev, nxt, flags); \
-        else launch_rollout<N, false, true, 1>(c, cur, noise_dev, S_dev, partial_dev, nxt, flags); \
+        if (c->poll) launch_rollout<N, true, true, 1>(c, cur, noise_dev, S_dev, partial_dev, nxt, flags, slots); \
+        else launch_rollout<N, false, true, 1>(c, cur, noise_dev, S_dev, partial_dev, nxt, flags, slots); \
     } else if (c->lps == 4) {                                                           \
-        if (c->poll) launch_rollout<N, true, false, 4>(c, cur, noise_dev, S_dev, partial_dev, nxt, flags); \
-        else launch_rollout<N, false, false, 4>(c, cur, noise_dev, S_dev, partial_dev, nxt, flags); \
-    } else if (c->poll) launch_rollout<N, true, false, 1>(c, cur, noise_dev, S_dev, partial_dev, nxt, flags); \
-    else launch_rollout<N, false, false, 1>(c, cur, noise_dev, S_dev, partial_dev, nxt, flags)
+        if (c->poll) launch_rollout<N, true, false, 4>(c, cur, noise_dev, S_dev, partial_dev, nxt, flags, slots); \
+        else launch_rollout<N, false, false, 4>(c, cur, noise_dev, S_dev, partial_dev, nxt, flags, slots); \
+    } else if (c->poll) launch_rollout<N, true, false, 1>(c, cur, noise_dev, S_dev, partial_dev, nxt, flags, slots); \
+    else launch_rollout<N, false, false, 1>(c, cur, noise_dev, S_dev, partial_dev, nxt, flags, slots)
     MPPI_CHAIN_DISPATCH(c->n, MPPI_L)
 #undef MPPI_L
     const hipError_t e = hipGetLastError();
@@ -1532,6 +1554,20 @@ int mppi_chain_rollout(mppi_chain_ctx* c, const float* noise_dev, double* S_dev,
     if (flags & MPPI_FLAG_FUSED_UPDATE) c->cur ^= 1;
     return MPPI_OK;
 }
+}  // namespace
+
+extern "C" {
+
+int mppi_chain_rollout(mppi_chain_ctx* c, const float* noise_dev, double* S_dev, double* partial_dev, unsigned flags) {
+    return chain_rollout(c, noise_dev, S_dev, partial_dev, flags, nullptr);
+}
+
+int mppi_chain_debug_slots(mppi_chain_ctx* c, const float* noise_dev, double* S_dev, int* slots_dev) {
+    if (!c || !noise_dev || !slots_dev) return fail(MPPI_E_ARG, "null argument");
+    if (c->n != kCDebugN) return fail(MPPI_E_ARG, "slot recording is built for the 7-link chain only");
+    return chain_rollout(c, noise_dev, S_dev, nullptr, 0u, slots_dev);
+}
+
 
 int mppi_chain_exchange_handle(mppi_chain_ctx* c, int world, void* handle_out) {
     if (!c || !handle_out || world < 1 || world > kMaxWorld) return fail(MPPI_E_ARG, "bad argument");

@@ -124,3 +124,38 @@ def test_tie_flip_helper_explains_a_neighbour_pick(paths):
     assert res[0] < 1e-12 and used[0] == gap[0, t1]
     assert res[1] < 1e-12 and used[1] == 0.0       # unflipped samples need no flip
     assert np.all(gap >= 0)
+
+
+def test_device_pick_helper_recomputes_with_given_slots(paths):
+    """tests/tieflip.py device_pick_residual: with the fp64 argmin everywhere it returns S_ref itself
+    (residual 0, no differing pick); with the second-nearest slot forced at one step, S_ref plus
+    exactly that step's cost step (tie_table's delta), that step's gap and one differing pick."""
+    from tieflip import device_pick_residual, tie_table
+    rng = np.random.default_rng(4)
+    K, T = 32, 6
+    win = paths["xydq_circle"][:30]
+    from mppi_robotarm_amd.chain import CHAIN7_SIGMA, CHAIN7_X0, gravity_torque
+    x0 = CHAIN7_X0
+    u = np.tile(gravity_torque(x0[:7]), (T, 1))
+    eps = (rng.standard_normal((T, 7, K)) * np.sqrt(np.diag(CHAIN7_SIGMA))[None, :, None]).astype(np.float32)
+    W, TW = [0.5, 0.5, 5.0, 5.0], [5.0, 5.0, 50.0, 50.0]
+    Sr = coracle.chain_rollout_costs(x0, u, eps, win, 0.006, 100.0, 0.98, CHAIN7_SIGMA, W, TW, P7, layout="TNK")
+    idx = np.arange(K)
+    # the fp64 picks (first minimum) from the oracle's own walk
+    slots = np.zeros((K, T), dtype=np.int32)
+    from tieflip import _walk
+    second = np.zeros((K, T), dtype=np.int32)
+    for t, x, y, dq in _walk(idx, x0, u, eps, 0.006, P7, None):
+        d = (x[:, None] - win[:, 0]) ** 2 + (y[:, None] - win[:, 1]) ** 2
+        o = np.argsort(d, axis=1, kind="stable")
+        slots[:, t], second[:, t] = o[:, 0], o[:, 1]
+    res, gap, nd = device_pick_residual(Sr, Sr, idx, x0, u, eps, win, 0.006, W, TW, P7, slots)
+    assert np.all(res < 1e-13) and np.all(gap == 0) and np.all(nd == 0)
+    gap2, delta = tie_table([5], x0, u, eps, win, 0.006, W, TW, P7)
+    forced = slots.copy()
+    forced[5, 2] = second[5, 2]
+    S_dev = Sr.copy()
+    S_dev[5] += delta[0, 2]
+    res, gap, nd = device_pick_residual(S_dev, Sr, idx, x0, u, eps, win, 0.006, W, TW, P7, forced)
+    assert res[5] < 1e-12 and nd[5] == 1 and abs(gap[5] - gap2[0, 2]) < 1e-15
+    assert np.all(np.delete(nd, 5) == 0)

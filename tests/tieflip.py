@@ -12,6 +12,11 @@ relative residual |S_dev - S_alt| / |S_alt| over every combination of flips at
 its closest-tie steps (gap below ``gap_max``), with the largest gap that combination used.
 An outlier is explained when the residual falls to the normal fp32 level and
 the gaps used are below the fp32 position resolution of the trajectory.
+
+``device_pick_residual`` is the exact form for the 7-link chain, whose kernel
+can record the slot it picked at every step (ChainEngine.debug_slots): the fp64
+cost recomputed with the device's own picks, and the gap at every step where a
+pick differs from the fp64 argmin — no search over flip combinations.
 """
 from __future__ import annotations
 
@@ -51,6 +56,55 @@ def tie_table(idx, x0, u, eps_tnk, win, dt, stage_w, term_w, P, exploit=None):
         delta[:, t] = cost(j2) - cost(j1)
         gap[:, t] = np.sqrt(d[rows, j2] / 100) - np.sqrt(d[rows, j1] / 100)
     return gap, delta
+
+
+def _walk(idx, x0, u, eps_tnk, dt, P, exploit):
+    """fp64 oracle states of the samples idx, step by step: yields (t, x, y, dq)."""
+    idx = np.asarray(idx)
+    e = np.asarray(eps_tnk)[:, :, idx].astype(np.float64).transpose(2, 0, 1)   # (m, T, n)
+    m, T, n = e.shape
+    q = np.tile(np.asarray(x0[:n], dtype=np.float64), (m, 1))
+    dq = np.tile(np.asarray(x0[n:2 * n], dtype=np.float64), (m, 1))
+    ex = np.ones(m, bool) if exploit is None else np.asarray(exploit)[idx]
+    for t in range(T):
+        v = np.where(ex[:, None], u[t] + e[:, t], e[:, t])
+        q, dq = CO.chain_forward_dynamics(q, dq, v, dt, P)
+        x, y = CO.chain_fk(q, P)
+        yield t, x, y, dq
+
+
+def device_pick_residual(S_dev, S_ref, idx, x0, u, eps_tnk, win, dt, stage_w, term_w, P, slots, exploit=None):
+    """(residual, largest gap [m] among the differing picks, number of differing steps) per sample
+    of ``idx``: S_ref plus, at every step where the device's slot (``slots`` (K, T)) differs from
+    the fp64 first minimum, that step's cost difference between the two slots."""
+    idx = np.asarray(idx)
+    win = np.asarray(win, dtype=np.float64)
+    m = len(idx)
+    rows = np.arange(m)
+    alt = np.asarray(S_ref, dtype=np.float64)[idx].copy()
+    gap = np.zeros(m)
+    ndiff = np.zeros(m, dtype=np.int64)
+    T = np.asarray(eps_tnk).shape[0]
+    for t, x, y, dq in _walk(idx, x0, u, eps_tnk, dt, P, exploit):
+        d = ((x[:, None] - win[:, 0]) ** 2 + (y[:, None] - win[:, 1]) ** 2) * 100
+        j1 = np.argmin(d, axis=1)                       # first minimum, as list.index(min(d))
+        jd = np.asarray(slots)[idx, t].astype(np.int64)
+        w = np.asarray(stage_w, dtype=np.float64)
+        if t == T - 1:
+            w = w + np.asarray(term_w, dtype=np.float64)   # the terminal cost uses the same slot
+
+        def cost(j):
+            r = win[j]
+            return 10000 * (w[0] * (x - r[:, 0]) ** 2 + w[1] * (y - r[:, 1]) ** 2 +
+                            w[2] * (dq[:, 0] - r[:, 2]) ** 2 + w[3] * (dq[:, 1] - r[:, 3]) ** 2)
+
+        diff = jd != j1
+        alt += np.where(diff, cost(jd) - cost(j1), 0.0)
+        g = np.sqrt(d[rows, jd] / 100) - np.sqrt(d[rows, j1] / 100)
+        gap = np.maximum(gap, np.where(diff, g, 0.0))
+        ndiff += diff
+    res = np.abs(np.asarray(S_dev, dtype=np.float64)[idx] - alt) / np.abs(alt)
+    return res, gap, ndiff
 
 
 def tie_flip_residual(S_dev, S_ref, idx, x0, u, eps_tnk, win, dt, stage_w, term_w, P, exploit=None,
