@@ -132,12 +132,22 @@ class MPPIControllerForPathTracking:
         self._step_count = 0
         self._noise_ready = None       # (seed, step) of the device noise already in the buffer
         self._engine_built_for = None  # _engine_key() of the live engine
-        self.host_update = bool(host_update) or self.T < 5   # the device median needs T >= 5
+        self.host_update = host_update  # property: forced, or T < 5 (the device median needs T >= 5)
         self.keep_costs = False        # set True to keep per-sample S (self.last_S)
         self.last_S = None
         self._bound = None             # what the engine's drop-in tick is bound to (_bind_key)
         self._last_sampled = None      # the previous call's sampled_traj_list (_fresh_sampled)
         self._fast = None              # what the last bound tick checked (calc_control_input's fast test)
+
+    @property
+    def host_update(self) -> bool:
+        """The update of control.py:120-149 on the host: asked for, or T < 5 (the
+        device median filter needs T >= 5), following self.T if it changes."""
+        return self._host_update or self.T < 5
+
+    @host_update.setter
+    def host_update(self, value) -> None:
+        self._host_update = bool(value)
 
     # ------------------------------------------------------------ engine
     def _shard(self):
@@ -150,8 +160,9 @@ class MPPIControllerForPathTracking:
         """Everything the engine bakes in at creation that the reference reads on
         every call (Sigma at control.py:84,106; lambda :112; gamma :106; the cost
         weights :185,198; the exploration split :98; delta_t :256-259; the
-        kinematics lengths self.l1/l2 of :178-179,205-206; the arm constants)."""
-        return (np.asarray(self.Sigma, dtype=np.float64).tobytes(), float(self.param_lambda),
+        kinematics lengths self.l1/l2 of :178-179,205-206; the arm constants; the
+        sample count and horizon self.K / self.T of :81-95)."""
+        return (int(self.K), int(self.T), np.asarray(self.Sigma, dtype=np.float64).tobytes(), float(self.param_lambda),
                 float(self.param_gamma), np.asarray(self.stage_cost_weight, dtype=np.float64).tobytes(),
                 np.asarray(self.terminal_cost_weight, dtype=np.float64).tobytes(), float(self.param_exploration),
                 float(self.delta_t), float(self.l1), float(self.l2), self.arm)
@@ -343,7 +354,7 @@ class MPPIControllerForPathTracking:
     def _fast_scalars(self):
         """Every scalar _tick's checks and the engine key read (control.py's per-call reads of
         lambda, gamma, the exploration split, delta_t, l1/l2), plus the controller switches."""
-        return (self.noise_source, self.host_update, self.visualze_sampled_trajs, self.process_group, self.K,
+        return (self.noise_source, self.host_update, self.visualze_sampled_trajs, self.process_group, self.K, self.T,
                 self.param_lambda, self.param_gamma, self.param_exploration, self.delta_t, self.l1, self.l2,
                 self.arm, self.seed, self.keep_costs, self.visualize_optimal_traj, self.verbose,
                 self._noise_ready == (self.seed, self._step_count))

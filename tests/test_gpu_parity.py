@@ -634,6 +634,36 @@ def test_sigma_and_lambda_reread_per_call(paths):
     assert _urel(got, want) < U_TOL
 
 
+@pytest.mark.parametrize("noise", ["numpy", "device"])
+def test_sample_count_and_horizon_reread_per_call(noise, paths):
+    """self.K and self.T are read on every call (control.py:81-95): changing them between calls (with a
+    u_prev of the new horizon) must act on the next step exactly as a controller built with the new values
+    would — including a horizon below 5, which takes the host update."""
+    from mppi_robotarm_amd.controller import MPPIControllerForPathTracking
+    kw = dict(delta_t=0.006, verbose=False, noise=noise, seed=5, device=0, **RUNPY)
+    c = MPPIControllerForPathTracking(ref_path=paths["xydq_circle"], horizon_step_T=16, number_of_samples_K=2048, **kw)
+    np.random.seed(1)
+    c.calc_control_input(X0)
+    c.calc_control_input(X0)
+    for K, T in ((1000, 12), (3000, 4), (2048, 16)):
+        u0 = np.tile([[9.0, -1.5]], (T, 1)) + 0.01 * np.arange(T)[:, None]
+        c.K, c.T, c.u_prev = K, T, u0.copy()
+        ref = MPPIControllerForPathTracking(ref_path=paths["xydq_circle"], horizon_step_T=T, number_of_samples_K=K,
+                                            **kw)
+        ref.u_prev, ref.prev_waypoints_idx = u0.copy(), c.prev_waypoints_idx
+        if noise == "device":
+            ref._step_count = c._step_count             # the same (seed, step) of the device stream
+        np.random.seed(7)
+        got = c.calc_control_input(X0)
+        np.random.seed(7)
+        want = ref.calc_control_input(X0)
+        assert got[1].shape == (T, 2) and got[3].shape == (K, T, 4)
+        assert np.array_equal(got[1], want[1]) and np.array_equal(got[2], want[2]), (K, T)
+        assert c.prev_waypoints_idx == ref.prev_waypoints_idx
+        ref.close()
+    c.close()
+
+
 def test_bound_tick_equals_general_dropin(paths):
     """The one-call tick (mppi_dropin_tick: native nearest-waypoint update, no
     input copy when u_prev is the nominal the last step published) against the

@@ -41,9 +41,21 @@ def main():
     kw = runpy_config()
     kw.update(number_of_samples_K=K, horizon_step_T=T, visualze_sampled_trajs=False)
 
-    rec = run_closed_loop(path, ticks=n, noise="device", seed=0, verbose=False, device=0, **kw)
-    rec["controller"].close()
+    run_closed_loop(path, ticks=100, noise="device", seed=0, verbose=False, device=0, **kw)["controller"].close()
+    cl_phases = []
+    ctl = {}
+
+    def on_tick(k, state, u):   # the native phase ends of the tick just run (the controller's engine)
+        eng_ = ctl["c"]._engine if "c" in ctl else None
+        if eng_ is not None and k > 3:
+            cl_phases.append(eng_.dropin_times() * 1e-6)
+
+    from mppi_robotarm_amd.controller import MPPIControllerForPathTracking as _C
+    ctl["c"] = _C(ref_path=path, noise="device", seed=0, verbose=False, device=0, **kw)
+    rec = run_closed_loop(path, ticks=n, controller=ctl["c"], on_tick=on_tick)
+    ctl["c"].close()
     closed = rec["latency_s"][3:]
+    cl_phases = np.array(cl_phases)
 
     c = MPPIControllerForPathTracking(ref_path=path, noise="device", seed=0, verbose=False, device=0, **kw)
     x = X0_RUNPY.copy()
@@ -115,6 +127,11 @@ def main():
     for i, nm in enumerate(names):
         print(f"      native: {nm:43s}{us(phases[:, i] - prev)}")
         prev = phases[:, i]
+    print("  closed loop, native phases of the same ticks:")
+    prev = np.zeros(len(cl_phases))
+    for i, nm in enumerate(names):
+        print(f"      native: {nm:43s}{us(cl_phases[:, i] - prev)}")
+        prev = cl_phases[:, i]
     print(f"  device: fused rollout launch                     {us(kern)}")
     print(f"  device: Philox draw of the next step's noise     {us(phil)}")
 
