@@ -310,6 +310,7 @@ class ChainMPPIController:
         self.T, self.K = horizon_step_T, number_of_samples_K
         self.param_exploration, self.param_lambda, self.param_alpha = param_exploration, param_lambda, param_alpha
         self.param_gamma = self.param_lambda * (1.0 - self.param_alpha)
+        self._lambda0 = self.param_lambda
         self.Sigma = np.asarray(sigma, dtype=np.float64)
         self.stage_cost_weight, self.terminal_cost_weight = stage_cost_weight, terminal_cost_weight
         self.visualize_optimal_traj, self.visualze_sampled_trajs = visualize_optimal_traj, visualze_sampled_trajs
@@ -327,6 +328,7 @@ class ChainMPPIController:
         self._xmode = None
         self._device = device
         self._engine = None
+        self._engine_built_for = None
         self._step_count = 0
         self.keep_costs = False
         self.last_S = None
@@ -337,12 +339,27 @@ class ChainMPPIController:
         import torch.distributed as dist
         return dist.get_world_size(self.process_group), dist.get_rank(self.process_group)
 
+    def _engine_key(self):
+        """What the engine bakes in that a call reads (as MPPIControllerForPathTracking._engine_key:
+        K, T, Sigma, lambda, gamma, the cost weights, the exploration split, delta_t, the chain and
+        the rollout precision); a change rebuilds the engine before the next step."""
+        return (int(self.K), int(self.T), np.asarray(self.Sigma, dtype=np.float64).tobytes(), float(self.param_lambda),
+                float(self.param_gamma), np.asarray(self.stage_cost_weight, dtype=np.float64).tobytes(),
+                np.asarray(self.terminal_cost_weight, dtype=np.float64).tobytes(), float(self.param_exploration),
+                float(self.delta_t), self.chain, self.precision)
+
     def _get_engine(self) -> ChainEngine:
+        key = self._engine_key()
+        if self._engine is not None and key != self._engine_built_for:
+            self.close()
         if self._engine is None:
             world, rank = self._shard()
             K_local, k_offset = shard_geometry(self.K, world, rank)
             device = self._device if self._device is not None else torch.cuda.current_device()
-            self._engine = ChainEngine(K_local, self.T, self.delta_t, self.param_lambda, self.param_alpha, self.Sigma,
+            # gamma stays the constructor's (control.py:45) when lambda changes: the engine takes alpha
+            alpha = (self.param_alpha if self.param_lambda == self._lambda0 or self.param_lambda == 0
+                     else 1.0 - self.param_gamma / self.param_lambda)
+            self._engine = ChainEngine(K_local, self.T, self.delta_t, self.param_lambda, alpha, self.Sigma,
                                        self.stage_cost_weight, self.terminal_cost_weight, self.param_exploration,
                                        self.chain, K_total=self.K, k_offset=k_offset, device=device,
                                        precision=self.precision)
@@ -353,6 +370,7 @@ class ChainMPPIController:
                 self._gathered = torch.empty(world * self._engine.partial_len, dtype=torch.float64,
                                              device=self._engine.device)
             self._xmode = None
+            self._engine_built_for = key
         return self._engine
 
     def _multi_setup(self, eng: ChainEngine, noise_check) -> None:
@@ -453,4 +471,5 @@ class ChainMPPIController:
         if self._engine is not None:
             self._engine.close()
             self._engine = None
+        self._engine_built_for = None
         self._xmode = None

@@ -424,3 +424,36 @@ def test_chain_short_horizons(T, precision, lps, paths):
     assert int(np.argmin(S)) == int(np.argmin(Sr))
     assert float(np.percentile(rel, 99)) < bound
     assert _urel(w, wr) < (1e-10 if precision == "f64" else U_TOL)
+
+
+def test_chain_controller_rereads_its_parameters(paths):
+    """ChainMPPIController follows what a call reads, as the 2-DoF drop-in does: K, T, Sigma (in place or
+    rebound), lambda (gamma kept from construction, control.py:45), the cost weights, the exploration split
+    and delta_t changed between calls act on the next step exactly as a controller built with them would."""
+    from mppi_robotarm_amd.chain import CHAIN7_X0, ChainMPPIController, gravity_torque
+    _, x0, sig, ug = _c5()
+    kw = dict(device=0, verbose=False, noise="numpy")
+    c = ChainMPPIController(0.006, paths["xydq_circle"], 16, 2048, 0.0, 100.0, 0.98, sig.copy(), u_init=ug, **kw)
+    np.random.seed(1)
+    c.calc_control_input(x0)
+    edits = [
+        lambda o: o.Sigma.__setitem__((0, 0), o.Sigma[0, 0] * 1.5),
+        lambda o: setattr(o, "param_lambda", 40.0),
+        lambda o: setattr(o, "stage_cost_weight", np.array([0.5, 1.0, 5.0, 5.0])),
+        lambda o: setattr(o, "param_exploration", 0.25),
+        lambda o: (setattr(o, "K", 1000), setattr(o, "T", 12), setattr(o, "u_prev", np.tile(ug, (12, 1)))),
+        lambda o: setattr(o, "delta_t", 0.005),
+    ]
+    for i, edit in enumerate(edits):
+        edit(c)
+        ref = ChainMPPIController(c.delta_t, paths["xydq_circle"], c.T, c.K, c.param_exploration, 100.0, 0.98,
+                                  c.Sigma.copy(), c.stage_cost_weight, c.terminal_cost_weight, u_init=c.u_prev.copy(), **kw)
+        ref.param_lambda = c.param_lambda                   # gamma from lambda = 100, as c's
+        ref.prev_waypoints_idx = c.prev_waypoints_idx
+        np.random.seed(10 + i)
+        got = c.calc_control_input(x0)
+        np.random.seed(10 + i)
+        want = ref.calc_control_input(x0)
+        assert np.array_equal(got[1], want[1]), i
+        ref.close()
+    c.close()
