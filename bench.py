@@ -238,6 +238,25 @@ def dropin_latency(K, T, device, ticks=200, warm=100):
     return float(np.median(lat)), float(np.percentile(lat, 90)), float(np.median(b2b))
 
 
+def chain_dropin_latency(K, T, device, precision="f32", calls=40, warm=10):
+    """The chain drop-in's calc_control_input back to back (ms, median) from the config-5 start state, the
+    start nominal re-staged before each call (the bench loop's reset: no plant between calls)."""
+    from mppi_robotarm_amd.chain import CHAIN7_X0, ChainMPPIController, gravity_torque
+    path = np.load(os.path.join(ROOT, "tests", "golden", "paths.npz"))["xydq_circle"][:, :4]
+    c = ChainMPPIController(0.006, path, T, K, u_init=gravity_torque(CHAIN7_X0[:7]), device=device, noise="device",
+                            precision=precision)
+    u0 = c.u_prev.copy()
+    ts = []
+    for i in range(warm + calls):
+        c.u_prev[:] = u0
+        c.prev_waypoints_idx = 0
+        t0 = time.perf_counter()
+        c.calc_control_input(CHAIN7_X0)
+        ts.append(time.perf_counter() - t0)
+    c.close()
+    return float(np.median(ts[warm:])) * 1e3
+
+
 def launch_ranks(args) -> int:
     """`--gpus N` (N > 1) without a launcher: start N rank processes under
     torch.distributed.run on this node (127.0.0.1) and return their exit code.
@@ -514,6 +533,15 @@ def main():
                 "trajectory on the host; the next tick's Philox draw is queued behind the launch and overlaps the "
                 "plant step between ticks. back_to_back: the same calls with nothing between them (each then "
                 "also waits for the previous draw). Steady state: 200 ticks each, after 100 uncounted. "
+                "ms_per_step is the device-resident loop")
+        if world == 1 and c5:
+            out["control_step_latency_back_to_back_ms"] = chain_dropin_latency(K, T, local_rank, args.precision)
+            out["control_step_latency_def"] = (
+                "median wall time of ChainMPPIController.calc_control_input (noise='device') at this K, T, back "
+                "to back from the config-5 start state (no plant model exists for the build-defined chain, so no "
+                "closed loop): one fused launch (rollouts, soft-min, weighted noise, median filter, update, shift), "
+                "one read-back, fp64 optimal trajectory on the host, the next step's Philox draw queued behind "
+                "the launch (each call then also waits for the previous draw). 40 calls after 10 uncounted. "
                 "ms_per_step is the device-resident loop")
         if world == 1 and args.cpu_seconds > 0:
             out["cpu_baseline"] = (cpu_baseline_c5(args, window, x0, u, K, T) if c5

@@ -339,6 +339,15 @@ int mppi_chain_exchange_handle(mppi_chain_ctx *ctx, int world, void *handle_out)
 int mppi_chain_exchange_attach(mppi_chain_ctx *ctx, int rank, int world, const void *handles);
 int mppi_chain_get_weighted_noise(mppi_chain_ctx *ctx, double *w_eps_host);
 int mppi_chain_get_nominal(mppi_chain_ctx *ctx, double *u_host);
+/* After a MPPI_FLAG_FUSED_UPDATE launch (control.py:120-149 on the device): the
+ * shifted nominal u_out[T][n] (the drop-in's returned sequence) and, when traj_out
+ * is given, the optimal trajectory of control.py:129-134 in fp64 on the host from
+ * x0[2n] and the update before its shift, traj_out[T][2n] (q, dq).  Replaces the
+ * read-back of w_eps + the host median + u += w_eps + the trajectory launch. */
+int mppi_chain_wait_outputs(mppi_chain_ctx *ctx, const double *x0, double *u_out, double *traj_out);
+/* control.py:129-134 for the chain on the host in fp64: traj_out[T][2n] from x0[2n]
+ * and the updated (not yet shifted) controls u_new[T][n]. */
+int mppi_chain_optimal_traj_host(mppi_chain_ctx *ctx, const double *x0, const double *u_new, double *traj_out);
 /* control.py:129-145 analogue: out_dev[K][T][2n] fp32 (q, dq) */
 int mppi_chain_rollout_traj(mppi_chain_ctx *ctx, const double *base_u, const float *noise_dev, int K,
                             float *out_dev);

@@ -42,6 +42,7 @@ EXPORTS = (
     "mppi_chain_exchange_attach",
     "mppi_chain_get_weighted_noise", "mppi_chain_get_nominal", "mppi_chain_rollout_traj",
     "mppi_chain_noise_philox", "mppi_chain_sync", "mppi_chain_debug_set_buffer", "mppi_chain_debug_slots",
+    "mppi_chain_wait_outputs", "mppi_chain_optimal_traj_host",
 )
 
 
@@ -149,6 +150,8 @@ def open_library(path: str):
         "mppi_chain_sync": ([vp], C.c_int),
         "mppi_chain_debug_set_buffer": ([vp, vp], C.c_int),
         "mppi_chain_debug_slots": ([vp, fp, vp, vp], C.c_int),
+        "mppi_chain_wait_outputs": ([vp, dp, dp, dp], C.c_int),
+        "mppi_chain_optimal_traj_host": ([vp, dp, dp, dp], C.c_int),
     }
     for name, (args, res) in sig.items():
         if not hasattr(L, name):   # an older diagnostic build (tools/ab.py); load() checks the product's exports

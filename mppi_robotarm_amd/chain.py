@@ -245,6 +245,31 @@ class ChainEngine:
         N.check(self._lib.mppi_chain_get_nominal(self._ctx, _dptr(out)), "mppi_chain_get_nominal")
         return out
 
+    def wait_outputs(self, x0=None) -> tuple[np.ndarray, np.ndarray | None]:
+        """After rollout(..., fused_update=True): the shifted nominal (T, n) and, with x0 (2n,), the fp64
+        optimal trajectory (T, 2n) of the update before its shift (mppi_chain_wait_outputs)."""
+        self._sync_stream()
+        u = np.empty((self.T, self.n))
+        traj = None
+        xp = None
+        if x0 is not None:
+            traj = np.empty((self.T, 2 * self.n))
+            xv = np.ascontiguousarray(np.asarray(x0, dtype=np.float64).ravel()[:2 * self.n])
+            xp = _dptr(xv)
+        N.check(self._lib.mppi_chain_wait_outputs(self._ctx, xp, _dptr(u), _dptr(traj) if traj is not None else None),
+                "mppi_chain_wait_outputs")
+        return u, traj
+
+    def optimal_traj_host(self, x0, u_new) -> np.ndarray:
+        """(T, 2n) fp64 optimal trajectory of control.py:129-134 from the updated, not yet shifted
+        controls u_new (T, n), on the host (mppi_chain_optimal_traj_host)."""
+        xv = np.ascontiguousarray(np.asarray(x0, dtype=np.float64).ravel()[:2 * self.n])
+        uv = np.ascontiguousarray(np.asarray(u_new, dtype=np.float64).reshape(self.T, self.n))
+        out = np.empty((self.T, 2 * self.n))
+        N.check(self._lib.mppi_chain_optimal_traj_host(self._ctx, _dptr(xv), _dptr(uv), _dptr(out)),
+                "mppi_chain_optimal_traj_host")
+        return out
+
     def trajectories(self, base_u=None, noise: torch.Tensor | None = None, K: int | None = None) -> torch.Tensor:
         """(K, T, 2n) fp32 states of the off-by-one re-roll (control.py:129-145 analogue)."""
         self._sync_stream()
@@ -329,6 +354,7 @@ class ChainMPPIController:
         self._device = device
         self._engine = None
         self._engine_built_for = None
+        self._noise_ready = None       # (seed, step) of the device noise already in the buffer
         self._step_count = 0
         self.keep_costs = False
         self.last_S = None
@@ -429,7 +455,7 @@ class ChainMPPIController:
         eng = self._get_engine()
         if epsilon is not None:
             eng.upload_noise(epsilon[eng.k_offset:eng.k_offset + eng.K_local], out=self._noise_dev)
-        else:
+        elif self._noise_ready != (self.seed, self._step_count):
             eng.philox_noise(self.seed, self._step_count, out=self._noise_dev)
         self._step_count += 1
         window = self.ref_path[self.prev_waypoints_idx:(self.prev_waypoints_idx + SEARCH_IDX_LEN)]
@@ -438,6 +464,18 @@ class ChainMPPIController:
         S_out = self._S_dev if self.keep_costs else None
         if world > 1 and self._xmode is None:
             self._multi_setup(eng, float(epsilon[0, 0, 0] + epsilon[-1, -1, -1]) if epsilon is not None else None)
+        if world == 1 and self.T >= 5 and not self.visualze_sampled_trajs:
+            # the update of control.py:120-149 inside the launch (the median of 10 is a selection and the
+            # add the same fp64 add: the host path's values), one read-back, the optimal trajectory in fp64
+            # on the host, the next step's device noise queued behind the launch
+            eng.rollout(self._noise_dev, S_out=S_out, fused_update=True)
+            sampled = np.zeros((self.K, self.T, self.dim_x))   # control.py:135, while the launch runs
+            u_new, traj = eng.wait_outputs(x0 if self.visualize_optimal_traj else None)
+            if self.keep_costs:
+                self.last_S = self._S_dev.cpu().numpy()
+            self._prefetch_noise(eng)
+            u[:] = u_new                                        # the shifted nominal, in place (aliasing kept)
+            return u[0], u, traj if traj is not None else np.zeros((self.T, self.dim_x)), sampled
         if world == 1:
             eng.rollout(self._noise_dev, S_out=S_out)
         elif self._xmode == "launch":
@@ -454,7 +492,7 @@ class ChainMPPIController:
         u += w_epsilon
         optimal_traj = np.zeros((self.T, self.dim_x))
         if self.visualize_optimal_traj:
-            optimal_traj = eng.trajectories(base_u=u, K=1)[0].double().cpu().numpy()
+            optimal_traj = eng.optimal_traj_host(x0, u)
         sampled = np.zeros((self.K, self.T, self.dim_x))
         if self.visualze_sampled_trajs:
             tr = eng.trajectories(base_u=None, noise=self._noise_dev)
@@ -465,11 +503,20 @@ class ChainMPPIController:
                 sampled[:] = tr.double().cpu().numpy()
         self.u_prev[:-1] = u[1:]
         self.u_prev[-1] = u[-1]
+        self._prefetch_noise(eng)
         return u[0], u, optimal_traj, sampled
+
+    def _prefetch_noise(self, eng: ChainEngine) -> None:
+        """Device noise: the next step's draw, queued behind every reader of this step's (the
+        draw is 470 MB at config 5, ~0.1 ms: off the next call's path when the caller works between calls)."""
+        if self.noise_source == "device":
+            eng.philox_noise(self.seed, self._step_count, out=self._noise_dev)
+            self._noise_ready = (self.seed, self._step_count)
 
     def close(self):
         if self._engine is not None:
             self._engine.close()
             self._engine = None
         self._engine_built_for = None
+        self._noise_ready = None       # a new engine's noise buffer is fresh: draw again
         self._xmode = None

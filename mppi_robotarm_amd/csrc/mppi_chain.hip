@@ -59,6 +59,7 @@ struct alignas(16) ChainStep {
     float ua[kMaxT + kCPU][2 * kCMax];     // u_t[n], a_t[n] (a = (gamma u_t)^T Sigma^-1), fp32; rows >= T zero
     double u[kMaxT][kCMax];                // nominal control sequence, fp64
     double a[kMaxT][kCMax];                // a_t in fp64 (fp64 rollout)
+    double u_first[kCMax];                 // fused update: u_new[0], the element the shift drops (optimal_traj)
 };
 
 // Launch constants (kernel argument, by value).
@@ -318,11 +319,20 @@ struct ChainState {
 // neighbour, and that stage cost moves S by up to ~1e-3 relative — harmless
 // while one sample carries the weight, visible in w_eps when tens do.
 typedef __attribute__((address_space(4))) const double cdouble;
+// 1 / sqrt in fp64 on either side (the device's rsqrt; the host's sqrt and divide)
+__host__ __device__ __forceinline__ double rsqrt_hd(double x) {
+#ifdef __HIP_DEVICE_COMPILE__
+    return rsqrt(x);
+#else
+    return 1.0 / sqrt(x);
+#endif
+}
+
 template <int N>
 struct ChainStateD {
     double q[N], dq[N], c[N], s[N];
 
-    __device__ __forceinline__ void load(const double* x0) {
+    __host__ __device__ __forceinline__ void load(const double* x0) {
 #pragma unroll
         for (int a = 0; a < N; ++a) {
             q[a] = x0[a];
@@ -330,7 +340,7 @@ struct ChainStateD {
         }
         angles();
     }
-    __device__ __forceinline__ void angles() {
+    __host__ __device__ __forceinline__ void angles() {
         double th = 0.0;
 #pragma unroll
         for (int a = 0; a < N; ++a) {
@@ -338,8 +348,10 @@ struct ChainStateD {
             sincos(th, &s[a], &c[a]);
         }
     }
-    // one semi-implicit Euler step (ChainState::step, oracle/chain_oracle.py chain_forward_dynamics)
-    __device__ __forceinline__ void step(const double (&v)[N], cdouble* k) {
+    // one semi-implicit Euler step (ChainState::step, oracle/chain_oracle.py chain_forward_dynamics);
+    // host and device: k is the fp64 constant block (constant memory on the device)
+    template <class KP>
+    __host__ __device__ __forceinline__ void step(const double (&v)[N], KP k) {
         double w[N], lc[N], ls[N], vc[N], vs[N], r[N];
         double acc = 0.0;
 #pragma unroll
@@ -392,7 +404,7 @@ struct ChainStateD {
         double inv[N];
 #pragma unroll
         for (int j = 0; j < N; ++j) {
-            inv[j] = rsqrt(L[j][j]);
+            inv[j] = rsqrt_hd(L[j][j]);
 #pragma unroll
             for (int i = j + 1; i < N; ++i) L[i][j] *= inv[j];
 #pragma unroll
@@ -447,6 +459,7 @@ __device__ void chain_update_block(ChainStep* nxt, const ChainConst& c, CScratch
         if (idx < T * N) sm.unew[idx] = u_cur[ch] + median_at(sm, idx / N, idx % N, T, N);
     }
     __syncthreads();
+    if (tid < N) nxt->u_first[tid] = sm.unew[tid];
     if (tid < T) {
         const int src = tid + 1 < T ? tid + 1 : T - 1;
         double u[N];
@@ -1124,9 +1137,16 @@ __global__ __launch_bounds__(kCT) void chain_traj_kernel(const ChainConst c, con
 
 // eps[t][d][k] = (L z)_d, z ~ N(0, I) from Philox4x32-10 counters (global k, t,
 // call) + Box-Muller: a shard generates exactly its slice of the unsharded draw.
-__global__ __launch_bounds__(kCT) void chain_philox_kernel(int K_local, int T, int n, long long k_offset,
+// The factor travels by value (kernel argument, scalar loads) and the link count
+// is a template argument, so the matvec unrolls and z stays in registers (a
+// runtime-n loop indexed z dynamically and sent it to scratch: 504 us at config 5).
+struct CholArg {
+    float L[kCMax * kCMax];   // lower triangle, row-major, x kBoxMullerScale (box_muller's constant)
+};
+template <int N>
+__global__ __launch_bounds__(kCT) void chain_philox_kernel(int K_local, int T, long long k_offset,
                                                            unsigned long long seed, unsigned long long step,
-                                                           const float* __restrict__ Lch, float* __restrict__ out) {
+                                                           const CholArg Lc, float* __restrict__ out) {
     // grid (ceil(K_local / kCT), T): no 64-bit divide per thread
     const int k = (int)blockIdx.x * kCT + (int)threadIdx.x;
     if (k >= K_local) return;
@@ -1144,10 +1164,13 @@ __global__ __launch_bounds__(kCT) void chain_philox_kernel(int K_local, int T, i
         z[4 * call + 2] = b.x;
         z[4 * call + 3] = b.y;
     }
-    for (int d = 0; d < n; ++d) {
+    float* row = out + (size_t)t * N * K_local + k;
+#pragma unroll
+    for (int d = 0; d < N; ++d) {
         float e = 0.f;
-        for (int j = 0; j <= d; ++j) e = fmaf(Lch[d * kCMax + j], z[j], e);
-        out[((size_t)t * n + d) * K_local + k] = e;
+#pragma unroll
+        for (int j = 0; j <= d; ++j) e = fmaf(Lc.L[d * kCMax + j], z[j], e);
+        row[(size_t)d * K_local] = e;
     }
 }
 
@@ -1175,8 +1198,12 @@ struct mppi_chain_ctx {
     double* h_buf = nullptr;
     float* d_base = nullptr;
     float* h_base = nullptr;
-    float* d_chol = nullptr;       // Cholesky factor of Sigma x kBoxMullerScale (kCMax x kCMax, fp32) for the Philox noise
+    CholArg chol{};                // Cholesky factor of Sigma x kBoxMullerScale (kCMax x kCMax, fp32) for the Philox noise
     float* d_dyn = nullptr;        // packed per-step constants (DynMem), then the same in fp64 at kDynF64Off
+    double h_dynd[kCDyn] = {};     // the fp64 constants on the host (the optimal trajectory)
+    bool upd_valid = false;        // the current step block holds a fused update's output
+    bool pub_valid = false;        // ... and h_pub is its shifted nominal as mppi_chain_wait_outputs returned it
+    double h_pub[kCMaxVals] = {};
     bool f64 = false;              // cfg.precision == 1
     int lps = 1;                   // lanes per sample: 1, or 4 (fp32 rollout at small K)
     unsigned* h_tmo = nullptr;
@@ -1356,6 +1383,7 @@ int mppi_chain_ctx_create(const mppi_chain_config* cfg, int device, void* stream
     }
     dynd[kOffDt] = cfg->delta_t;
     dynd[kOffG] = P.g;
+    memcpy(c->h_dynd, dynd, sizeof(dynd));
     k.lambda = cfg->param_lambda;
     k.inv_lambda = 1.0 / cfg->param_lambda;
     k.gamma = cfg->param_lambda * (1.0 - cfg->param_alpha);
@@ -1394,20 +1422,18 @@ int mppi_chain_ctx_create(const mppi_chain_config* cfg, int device, void* stream
     const size_t ctr_bytes = (cu_off + kCuSlots) * sizeof(unsigned);
     c->kc.cu_off = (int)cu_off;
     c->kc.fair = c->nblocks > ncu ? 1 : 0;
-    float chol[kCMax * kCMax] = {};
     for (int i = 0; i < n; ++i)
-        for (int j = 0; j <= i; ++j) chol[i * kCMax + j] = (float)(Lc[i][j] * kBoxMullerScale);   // box_muller's constant
+        for (int j = 0; j <= i; ++j) c->chol.L[i * kCMax + j] = (float)(Lc[i][j] * kBoxMullerScale);   // box_muller's constant
     if ((e = hipMalloc(&c->d_step, 2 * sizeof(ChainStep))) != hipSuccess ||
         (e = hipMalloc(&c->d_slab, slab)) != hipSuccess || (e = hipMalloc(&c->d_gslab, gslab)) != hipSuccess ||
         (e = hipMalloc(&c->d_counter, ctr_bytes)) != hipSuccess ||
         (e = hipMalloc(&c->d_runmin, 256)) != hipSuccess || (e = hipMemset(c->d_runmin, 0xFF, 256)) != hipSuccess ||
         (e = hipMalloc(&c->d_weps, kCMaxVals * sizeof(double))) != hipSuccess ||
         (e = hipMalloc(&c->d_base, kCMaxVals * sizeof(float))) != hipSuccess ||
-        (e = hipMalloc(&c->d_chol, sizeof(chol))) != hipSuccess ||
         (e = hipMalloc(&c->d_dyn, kDynF64Off * sizeof(float) + sizeof(dynd))) != hipSuccess ||
         (e = hipMemcpy(c->d_dyn + kDynF64Off, dynd, sizeof(dynd), hipMemcpyHostToDevice)) != hipSuccess ||
         (e = hipHostMalloc(&c->h_step, sizeof(ChainStep), hipHostMallocDefault)) != hipSuccess ||
-        (e = hipHostMalloc(&c->h_buf, kCMaxVals * sizeof(double), hipHostMallocDefault)) != hipSuccess ||
+        (e = hipHostMalloc(&c->h_buf, (kCMaxVals + kCMax) * sizeof(double), hipHostMallocDefault)) != hipSuccess ||
         (e = hipHostMalloc(&c->h_base, kCMaxVals * sizeof(float), hipHostMallocDefault)) != hipSuccess ||
         (e = hipHostMalloc(&c->h_tmo, 256, hipHostMallocMapped)) != hipSuccess ||
         (e = hipHostGetDevicePointer((void**)&c->d_tmo, c->h_tmo, 0)) != hipSuccess ||
@@ -1416,7 +1442,6 @@ int mppi_chain_ctx_create(const mppi_chain_config* cfg, int device, void* stream
         (e = hipMemset(c->d_gslab, 0, gslab)) != hipSuccess ||
         (e = hipMemset(c->d_step, 0, 2 * sizeof(ChainStep))) != hipSuccess ||
         (e = hipMemset(c->d_weps, 0, kCMaxVals * sizeof(double))) != hipSuccess ||
-        (e = hipMemcpy(c->d_chol, chol, sizeof(chol), hipMemcpyHostToDevice)) != hipSuccess ||
         (e = hipMemcpy(c->d_dyn, k.dyn, sizeof(k.dyn), hipMemcpyHostToDevice)) != hipSuccess ||
         (e = hipDeviceSynchronize()) != hipSuccess)
         return cleanup_fail(fail(MPPI_E_HIP, std::string("allocation: ") + hipGetErrorString(e)));
@@ -1438,7 +1463,6 @@ void mppi_chain_ctx_destroy(mppi_chain_ctx* c) {
     (void)hipFree(c->d_runmin);
     (void)hipFree(c->d_weps);
     (void)hipFree(c->d_base);
-    (void)hipFree(c->d_chol);
     (void)hipFree(c->d_dyn);
     for (void* p : c->xopened)
         if (p) (void)hipIpcCloseMemHandle(p);
@@ -1499,6 +1523,12 @@ int mppi_chain_set_step_inputs(mppi_chain_ctx* c, const double* x0, const double
     for (int j = 0; j < kSlots; ++j)
         for (int i = 0; i < 4; ++i) h->wind[j][i] = j < W ? window[4 * j + i] : 0.0;
     size_t bytes = offsetof(ChainStep, ua);
+    // the caller's u is the nominal the last fused launch wrote and wait_outputs returned: the device block
+    // already holds it with the same (u, a) bits the staging below would compute, so only x0 and the window go
+    bool same = u && c->pub_valid;
+    for (int t = 0; same && t < T; ++t)
+        for (int d = 0; d < n; ++d) same = same && u[t * n + d] == c->h_pub[t * kCMax + d];
+    if (same) u = nullptr;
     if (u) {
         const ChainConst& k = c->kc;
         for (int t = 0; t < T; ++t) {
@@ -1513,6 +1543,8 @@ int mppi_chain_set_step_inputs(mppi_chain_ctx* c, const double* x0, const double
             }
         }
         bytes = sizeof(ChainStep);
+        c->upd_valid = false;   // the block now holds the staged nominal, not a fused update's output
+        c->pub_valid = false;
     }
     if (hipMemcpyAsync(c->d_step + (c->cur ^ 1), h, offsetof(ChainStep, ua), hipMemcpyHostToDevice, c->stream) !=
             hipSuccess ||
@@ -1552,6 +1584,8 @@ int chain_rollout(mppi_chain_ctx* c, const float* noise_dev, double* S_dev, doub
     const hipError_t e = hipGetLastError();
     if (e != hipSuccess) return fail(MPPI_E_HIP, std::string("chain_rollout_kernel: ") + hipGetErrorString(e));
     if (flags & MPPI_FLAG_FUSED_UPDATE) c->cur ^= 1;
+    c->upd_valid = (flags & MPPI_FLAG_FUSED_UPDATE) != 0;
+    if (flags & MPPI_FLAG_FUSED_UPDATE) c->pub_valid = false;
     return MPPI_OK;
 }
 }  // namespace
@@ -1630,6 +1664,8 @@ int mppi_chain_merge_partials(mppi_chain_ctx* c, const double* partials_dev, int
     const hipError_t e = hipGetLastError();
     if (e != hipSuccess) return fail(MPPI_E_HIP, std::string("chain_merge_kernel: ") + hipGetErrorString(e));
     if (flags & MPPI_FLAG_FUSED_UPDATE) c->cur ^= 1;
+    c->upd_valid = (flags & MPPI_FLAG_FUSED_UPDATE) != 0;
+    if (flags & MPPI_FLAG_FUSED_UPDATE) c->pub_valid = false;
     return MPPI_OK;
 }
 
@@ -1653,6 +1689,66 @@ int mppi_chain_get_nominal(mppi_chain_ctx* c, double* u_host) {
     for (int t = 0; t < T; ++t)
         for (int d = 0; d < n; ++d) u_host[t * n + d] = c->h_buf[t * kCMax + d];
     return check_tmo(c);
+}
+
+}  // extern "C"
+
+namespace {
+// control.py:129-134 for the chain in fp64 on the host: x_{t+1} = F(x_t, u_new[t - 1]) (u_new[-1] at t = 0),
+// the same ChainStateD step as the fp64 rollout.  One sequential trajectory: the host's fp64 is ~5x the
+// device's single lane here (~1.7 us per step of dependent VALU on one wave).
+template <int N>
+void chain_traj_host(const double* kd, const double* x0, const double* u_new, int T, double* out) {
+    ChainStateD<N> x;
+    x.load(x0);
+    for (int t = 0; t < T; ++t) {
+        const double* ut = u_new + (size_t)N * (t == 0 ? T - 1 : t - 1);
+        double v[N];
+        for (int d = 0; d < N; ++d) v[d] = ut[d];
+        x.step(v, kd);
+        for (int a = 0; a < N; ++a) {
+            out[(size_t)t * 2 * N + a] = x.q[a];
+            out[(size_t)t * 2 * N + N + a] = x.dq[a];
+        }
+    }
+}
+}  // namespace
+
+extern "C" {
+
+int mppi_chain_wait_outputs(mppi_chain_ctx* c, const double* x0, double* u_out, double* traj_out) {
+    if (!c || !u_out || (traj_out && !x0)) return fail(MPPI_E_ARG, "bad argument");
+    if (!c->upd_valid) return fail(MPPI_E_ARG, "no fused update to read (mppi_chain_rollout with MPPI_FLAG_FUSED_UPDATE)");
+    const int n = c->n, T = c->cfg.T;
+    const char* blk = (const char*)(c->d_step + c->cur);
+    if (hipMemcpyAsync(c->h_buf, blk + offsetof(ChainStep, u), (size_t)T * kCMax * sizeof(double),
+                       hipMemcpyDeviceToHost, c->stream) != hipSuccess ||
+        hipMemcpyAsync(c->h_buf + kCMaxVals, blk + offsetof(ChainStep, u_first), kCMax * sizeof(double),
+                       hipMemcpyDeviceToHost, c->stream) != hipSuccess ||
+        hipStreamSynchronize(c->stream) != hipSuccess)
+        return fail(MPPI_E_HIP, "update read-back");
+    if (int rc = check_tmo(c)) return rc;
+    for (int t = 0; t < T; ++t)
+        for (int d = 0; d < n; ++d) u_out[t * n + d] = c->h_buf[t * kCMax + d];
+    memcpy(c->h_pub, c->h_buf, (size_t)T * kCMax * sizeof(double));
+    c->pub_valid = true;
+    if (traj_out) {
+        // the update before the shift: u_new[0] from the block, u_new[t] = shifted[t - 1] for t >= 1
+        double un[kMaxT * kCMax];
+        for (int d = 0; d < n; ++d) un[d] = c->h_buf[kCMaxVals + d];
+        for (int t = 1; t < T; ++t)
+            for (int d = 0; d < n; ++d) un[t * n + d] = c->h_buf[(t - 1) * kCMax + d];
+        return mppi_chain_optimal_traj_host(c, x0, un, traj_out);
+    }
+    return MPPI_OK;
+}
+
+int mppi_chain_optimal_traj_host(mppi_chain_ctx* c, const double* x0, const double* u_new, double* traj_out) {
+    if (!c || !x0 || !u_new || !traj_out) return fail(MPPI_E_ARG, "null argument");
+#define MPPI_TH(N) chain_traj_host<N>(c->h_dynd, x0, u_new, c->cfg.T, traj_out)
+    MPPI_CHAIN_DISPATCH(c->n, MPPI_TH);
+#undef MPPI_TH
+    return MPPI_OK;
 }
 
 int mppi_chain_rollout_traj(mppi_chain_ctx* c, const double* base_u, const float* noise_dev, int K, float* out_dev) {
@@ -1693,8 +1789,11 @@ int mppi_chain_rollout_traj(mppi_chain_ctx* c, const double* base_u, const float
 int mppi_chain_noise_philox(mppi_chain_ctx* c, unsigned long long seed, unsigned long long step, float* out_dev) {
     if (!c || !out_dev) return fail(MPPI_E_ARG, "null argument");
     const dim3 grid((unsigned)((c->cfg.K_local + kCT - 1) / kCT), (unsigned)c->cfg.T);
-    hipLaunchKernelGGL(chain_philox_kernel, grid, dim3(kCT), 0, c->stream, c->cfg.K_local, c->cfg.T, c->n,
-                       (long long)c->cfg.k_offset, seed, step, c->d_chol, out_dev);
+#define MPPI_PH(N)                                                                                            \
+    hipLaunchKernelGGL(chain_philox_kernel<N>, grid, dim3(kCT), 0, c->stream, c->cfg.K_local, c->cfg.T,         \
+                       (long long)c->cfg.k_offset, seed, step, c->chol, out_dev)
+    MPPI_CHAIN_DISPATCH(c->n, MPPI_PH);
+#undef MPPI_PH
     const hipError_t e = hipGetLastError();
     if (e != hipSuccess) return fail(MPPI_E_HIP, std::string("chain_philox_kernel: ") + hipGetErrorString(e));
     return MPPI_OK;

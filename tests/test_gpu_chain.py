@@ -457,3 +457,51 @@ def test_chain_controller_rereads_its_parameters(paths):
         assert np.array_equal(got[1], want[1]), i
         ref.close()
     c.close()
+
+
+def test_chain_fused_dropin_equals_host_update_path(paths):
+    """ChainMPPIController's one-launch step (update on the device, one read-back, fp64 optimal trajectory on
+    the host, next noise prefetched) against the host-update path (w_eps read back, SciPy median, u += w_eps)
+    from the same state and noise: u, the aliasing and the optimal trajectory bit for bit over a few ticks, one
+    of them after an in-place edit of u_prev (the fused path skips re-staging only an unchanged nominal)."""
+    from mppi_robotarm_amd.chain import ChainMPPIController
+    _, x0, sig, ug = _c5()
+    kw = dict(device=0, verbose=False, noise="device", seed=4)
+    # the oracle side of the trajectory is test_chain_optimal_traj_host_against_oracle
+    fused = ChainMPPIController(0.006, paths["xydq_circle"], 24, 4096, 0.0, 100.0, 0.98, sig, u_init=ug, **kw)
+    host = ChainMPPIController(0.006, paths["xydq_circle"], 24, 4096, 0.0, 100.0, 0.98, sig, u_init=ug,
+                               visualze_sampled_trajs=True, **kw)   # takes the host-update path
+    x = x0.copy()
+    for tick in range(5):
+        if tick == 2:
+            for c in (fused, host):
+                c.u_prev += 0.1                  # an in-place edit of the nominal must be staged, not skipped
+        outs = []
+        for c in (fused, host):
+            u_prev = c.u_prev
+            u0, u_seq, opt, samp = c.calc_control_input(x)
+            assert u_seq is u_prev and np.shares_memory(u0, u_prev)
+            outs.append((u_seq.copy(), opt.copy(), c.prev_waypoints_idx))
+        (ua, oa, ia), (ub, ob, ib) = outs
+        assert ia == ib and np.array_equal(ua, ub), tick
+        assert np.array_equal(oa, ob), tick
+        x = oa[3].copy()
+    fused.close()
+    host.close()
+
+
+def test_chain_optimal_traj_host_against_oracle():
+    """mppi_chain_optimal_traj_host (fp64 ChainStateD on the host) against the fp64 chain oracle's dynamics:
+    x_{t+1} = F(x_t, u_new[t - 1]), u_new[-1] at t = 0 (control.py:129-134), to 1e-12."""
+    P, x0, sig, ug = _c5()
+    T = 20
+    eng = _engine(256, T)
+    u_new = np.tile(ug, (T, 1)) + np.random.default_rng(9).normal(0, 0.5, (T, 7))
+    got = eng.optimal_traj_host(x0, u_new)
+    q, dq = x0[None, :7].copy(), x0[None, 7:].copy()
+    want = np.zeros((T, 14))
+    for t in range(T):
+        q, dq = CO.chain_forward_dynamics(q, dq, u_new[t - 1][None, :], 0.006, CO.ChainParams())
+        want[t, :7], want[t, 7:] = q[0], dq[0]
+    eng.close()
+    np.testing.assert_allclose(got, want, rtol=1e-12, atol=1e-12)
