@@ -355,6 +355,7 @@ class ChainMPPIController:
         self._engine = None
         self._engine_built_for = None
         self._noise_ready = None       # (seed, step) of the device noise already in the buffer
+        self._last_sampled = None      # the previous call's sampled_traj_list (_fresh_sampled)
         self._step_count = 0
         self.keep_costs = False
         self.last_S = None
@@ -374,8 +375,8 @@ class ChainMPPIController:
                 np.asarray(self.terminal_cost_weight, dtype=np.float64).tobytes(), float(self.param_exploration),
                 float(self.delta_t), self.chain, self.precision)
 
-    def _get_engine(self) -> ChainEngine:
-        key = self._engine_key()
+    def _get_engine(self, key=None) -> ChainEngine:
+        key = self._engine_key() if key is None else key
         if self._engine is not None and key != self._engine_built_for:
             self.close()
         if self._engine is None:
@@ -451,8 +452,10 @@ class ChainMPPIController:
             epsilon = self._calc_epsilon(self.Sigma, self.K, self.T, self.dim_u)
         else:
             epsilon = None
-        np.linalg.inv(self.Sigma)
-        eng = self._get_engine()
+        key = self._engine_key()
+        if key != self._engine_built_for:
+            np.linalg.inv(self.Sigma)                      # LinAlgError as control.py:106 (Sigma checked when it changes)
+        eng = self._get_engine(key)
         if epsilon is not None:
             eng.upload_noise(epsilon[eng.k_offset:eng.k_offset + eng.K_local], out=self._noise_dev)
         elif self._noise_ready != (self.seed, self._step_count):
@@ -469,7 +472,7 @@ class ChainMPPIController:
             # add the same fp64 add: the host path's values), one read-back, the optimal trajectory in fp64
             # on the host, the next step's device noise queued behind the launch
             eng.rollout(self._noise_dev, S_out=S_out, fused_update=True)
-            sampled = np.zeros((self.K, self.T, self.dim_x))   # control.py:135, while the launch runs
+            sampled = self._fresh_sampled()                     # control.py:135, while the launch runs
             u_new, traj = eng.wait_outputs(x0 if self.visualize_optimal_traj else None)
             if self.keep_costs:
                 self.last_S = self._S_dev.cpu().numpy()
@@ -505,6 +508,14 @@ class ChainMPPIController:
         self.u_prev[-1] = u[-1]
         self._prefetch_noise(eng)
         return u[0], u, optimal_traj, sampled
+
+    def _fresh_sampled(self) -> np.ndarray:
+        """A fresh writable np.zeros for sampled_traj_list (1.9 GB at config 5, mapped lazily), made while the
+        launch runs; the previous call's array is kept until then, so unmapping it, if the caller dropped it,
+        also happens under the launch rather than after the call returns."""
+        out = np.zeros((self.K, self.T, self.dim_x))
+        self._last_sampled = out
+        return out
 
     def _prefetch_noise(self, eng: ChainEngine) -> None:
         """Device noise: the next step's draw, queued behind every reader of this step's (the
