@@ -343,7 +343,9 @@ int mppi_chain_get_nominal(mppi_chain_ctx *ctx, double *u_host);
  * shifted nominal u_out[T][n] (the drop-in's returned sequence) and, when traj_out
  * is given, the optimal trajectory of control.py:129-134 in fp64 on the host from
  * x0[2n] and the update before its shift, traj_out[T][2n] (q, dq).  Replaces the
- * read-back of w_eps + the host median + u += w_eps + the trajectory launch. */
+ * read-back of w_eps + the host median + u += w_eps + the trajectory launch.
+ * With MPPI_FLAG_HOST_OUT on that launch, the chain queues this read-back right
+ * behind it, so work queued afterwards (the next noise) does not delay the wait. */
 int mppi_chain_wait_outputs(mppi_chain_ctx *ctx, const double *x0, double *u_out, double *traj_out);
 /* control.py:129-134 for the chain on the host in fp64: traj_out[T][2n] from x0[2n]
  * and the updated (not yet shifted) controls u_new[T][n]. */

@@ -211,7 +211,8 @@ class ChainEngine:
         self.exchange_world = int(world)
 
     def rollout(self, noise: torch.Tensor, S_out: torch.Tensor | None = None,
-                partial_out: torch.Tensor | None = None, fused_update: bool = False, exchange: bool = False) -> None:
+                partial_out: torch.Tensor | None = None, fused_update: bool = False, exchange: bool = False,
+                host_out: bool = False) -> None:
         self._sync_stream()
         self._check_noise(noise)
         if S_out is not None:
@@ -222,7 +223,8 @@ class ChainEngine:
                                              C.c_void_p(S_out.data_ptr()) if S_out is not None else None,
                                              C.c_void_p(partial_out.data_ptr()) if partial_out is not None else None,
                                              (N.MPPI_FLAG_FUSED_UPDATE if fused_update else 0)
-                                             | (N.MPPI_FLAG_EXCHANGE if exchange else 0)),
+                                             | (N.MPPI_FLAG_EXCHANGE if exchange else 0)
+                                             | (N.MPPI_FLAG_HOST_OUT if host_out else 0)),
                 "mppi_chain_rollout")
 
     def merge(self, partials: torch.Tensor, n: int, fused_update: bool = False) -> None:
@@ -471,12 +473,14 @@ class ChainMPPIController:
             # the update of control.py:120-149 inside the launch (the median of 10 is a selection and the
             # add the same fp64 add: the host path's values), one read-back, the optimal trajectory in fp64
             # on the host, the next step's device noise queued behind the launch
-            eng.rollout(self._noise_dev, S_out=S_out, fused_update=True)
+            eng.rollout(self._noise_dev, S_out=S_out, fused_update=True, host_out=True)
+            # the next step's draw right behind the launch and its read-back (stream order: it starts once the rollout has read
+            # the buffer), so it runs under the read-back, the host trajectory and the caller's work
+            self._prefetch_noise(eng)
             sampled = self._fresh_sampled()                     # control.py:135, while the launch runs
             u_new, traj = eng.wait_outputs(x0 if self.visualize_optimal_traj else None)
             if self.keep_costs:
                 self.last_S = self._S_dev.cpu().numpy()
-            self._prefetch_noise(eng)
             u[:] = u_new                                        # the shifted nominal, in place (aliasing kept)
             return u[0], u, traj if traj is not None else np.zeros((self.T, self.dim_x)), sampled
         if world == 1:

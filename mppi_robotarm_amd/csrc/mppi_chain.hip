@@ -1203,6 +1203,9 @@ struct mppi_chain_ctx {
     double h_dynd[kCDyn] = {};     // the fp64 constants on the host (the optimal trajectory)
     bool upd_valid = false;        // the current step block holds a fused update's output
     bool pub_valid = false;        // ... and h_pub is its shifted nominal as mppi_chain_wait_outputs returned it
+    double* h_out = nullptr;       // MPPI_FLAG_HOST_OUT: the update's read-back, queued right behind the launch
+    hipEvent_t out_ev = nullptr;   // ... recorded after that copy
+    bool out_posted = false;
     double h_pub[kCMaxVals] = {};
     bool f64 = false;              // cfg.precision == 1
     int lps = 1;                   // lanes per sample: 1, or 4 (fp32 rollout at small K)
@@ -1438,6 +1441,8 @@ int mppi_chain_ctx_create(const mppi_chain_config* cfg, int device, void* stream
         (e = hipHostMalloc(&c->h_tmo, 256, hipHostMallocMapped)) != hipSuccess ||
         (e = hipHostGetDevicePointer((void**)&c->d_tmo, c->h_tmo, 0)) != hipSuccess ||
         (e = hipEventCreateWithFlags(&c->staged, hipEventDisableTiming)) != hipSuccess ||
+        (e = hipEventCreateWithFlags(&c->out_ev, hipEventDisableTiming)) != hipSuccess ||
+        (e = hipHostMalloc(&c->h_out, (kCMaxVals + kCMax) * sizeof(double), hipHostMallocDefault)) != hipSuccess ||
         (e = hipMemset(c->d_counter, 0, ctr_bytes)) != hipSuccess || (e = hipMemset(c->d_slab, 0, slab)) != hipSuccess ||
         (e = hipMemset(c->d_gslab, 0, gslab)) != hipSuccess ||
         (e = hipMemset(c->d_step, 0, 2 * sizeof(ChainStep))) != hipSuccess ||
@@ -1471,6 +1476,8 @@ void mppi_chain_ctx_destroy(mppi_chain_ctx* c) {
     (void)hipFree(c->d_xepoch);
     if (c->h_step) (void)hipHostFree(c->h_step);
     if (c->h_buf) (void)hipHostFree(c->h_buf);
+    if (c->h_out) (void)hipHostFree(c->h_out);
+    if (c->out_ev) (void)hipEventDestroy(c->out_ev);
     if (c->h_base) (void)hipHostFree(c->h_base);
     if (c->h_tmo) (void)hipHostFree(c->h_tmo);
     if (c->staged) (void)hipEventDestroy(c->staged);
@@ -1586,6 +1593,19 @@ int chain_rollout(mppi_chain_ctx* c, const float* noise_dev, double* S_dev, doub
     if (flags & MPPI_FLAG_FUSED_UPDATE) c->cur ^= 1;
     c->upd_valid = (flags & MPPI_FLAG_FUSED_UPDATE) != 0;
     if (flags & MPPI_FLAG_FUSED_UPDATE) c->pub_valid = false;
+    c->out_posted = false;
+    if ((flags & MPPI_FLAG_FUSED_UPDATE) && (flags & MPPI_FLAG_HOST_OUT)) {
+        // the update's read-back right behind the launch, so what the caller queues next (the next
+        // step's noise) does not delay mppi_chain_wait_outputs
+        const char* blk = (const char*)(c->d_step + c->cur);
+        if (hipMemcpyAsync(c->h_out, blk + offsetof(ChainStep, u), (size_t)c->cfg.T * kCMax * sizeof(double),
+                           hipMemcpyDeviceToHost, c->stream) != hipSuccess ||
+            hipMemcpyAsync(c->h_out + kCMaxVals, blk + offsetof(ChainStep, u_first), kCMax * sizeof(double),
+                           hipMemcpyDeviceToHost, c->stream) != hipSuccess ||
+            hipEventRecord(c->out_ev, c->stream) != hipSuccess)
+            return fail(MPPI_E_HIP, "update read-back");
+        c->out_posted = true;
+    }
     return MPPI_OK;
 }
 }  // namespace
@@ -1720,24 +1740,29 @@ int mppi_chain_wait_outputs(mppi_chain_ctx* c, const double* x0, double* u_out, 
     if (!c || !u_out || (traj_out && !x0)) return fail(MPPI_E_ARG, "bad argument");
     if (!c->upd_valid) return fail(MPPI_E_ARG, "no fused update to read (mppi_chain_rollout with MPPI_FLAG_FUSED_UPDATE)");
     const int n = c->n, T = c->cfg.T;
-    const char* blk = (const char*)(c->d_step + c->cur);
-    if (hipMemcpyAsync(c->h_buf, blk + offsetof(ChainStep, u), (size_t)T * kCMax * sizeof(double),
-                       hipMemcpyDeviceToHost, c->stream) != hipSuccess ||
-        hipMemcpyAsync(c->h_buf + kCMaxVals, blk + offsetof(ChainStep, u_first), kCMax * sizeof(double),
-                       hipMemcpyDeviceToHost, c->stream) != hipSuccess ||
-        hipStreamSynchronize(c->stream) != hipSuccess)
-        return fail(MPPI_E_HIP, "update read-back");
+    const double* h = c->h_out;
+    if (c->out_posted) {   // MPPI_FLAG_HOST_OUT: the copy is already queued behind the launch
+        if (hipEventSynchronize(c->out_ev) != hipSuccess) return fail(MPPI_E_HIP, "update read-back");
+    } else {
+        const char* blk = (const char*)(c->d_step + c->cur);
+        if (hipMemcpyAsync(c->h_out, blk + offsetof(ChainStep, u), (size_t)T * kCMax * sizeof(double),
+                           hipMemcpyDeviceToHost, c->stream) != hipSuccess ||
+            hipMemcpyAsync(c->h_out + kCMaxVals, blk + offsetof(ChainStep, u_first), kCMax * sizeof(double),
+                           hipMemcpyDeviceToHost, c->stream) != hipSuccess ||
+            hipStreamSynchronize(c->stream) != hipSuccess)
+            return fail(MPPI_E_HIP, "update read-back");
+    }
     if (int rc = check_tmo(c)) return rc;
     for (int t = 0; t < T; ++t)
-        for (int d = 0; d < n; ++d) u_out[t * n + d] = c->h_buf[t * kCMax + d];
-    memcpy(c->h_pub, c->h_buf, (size_t)T * kCMax * sizeof(double));
+        for (int d = 0; d < n; ++d) u_out[t * n + d] = h[t * kCMax + d];
+    memcpy(c->h_pub, h, (size_t)T * kCMax * sizeof(double));
     c->pub_valid = true;
     if (traj_out) {
         // the update before the shift: u_new[0] from the block, u_new[t] = shifted[t - 1] for t >= 1
         double un[kMaxT * kCMax];
-        for (int d = 0; d < n; ++d) un[d] = c->h_buf[kCMaxVals + d];
+        for (int d = 0; d < n; ++d) un[d] = h[kCMaxVals + d];
         for (int t = 1; t < T; ++t)
-            for (int d = 0; d < n; ++d) un[t * n + d] = c->h_buf[(t - 1) * kCMax + d];
+            for (int d = 0; d < n; ++d) un[t * n + d] = h[(t - 1) * kCMax + d];
         return mppi_chain_optimal_traj_host(c, x0, un, traj_out);
     }
     return MPPI_OK;
