@@ -500,14 +500,16 @@ class ChainMPPIController:
         optimal_traj = np.zeros((self.T, self.dim_x))
         if self.visualize_optimal_traj:
             optimal_traj = eng.optimal_traj_host(x0, u)
-        sampled = np.zeros((self.K, self.T, self.dim_x))
         if self.visualze_sampled_trajs:
             tr = eng.trajectories(base_u=None, noise=self._noise_dev)
             if world > 1:
                 from .distributed import gather_trajectories
+                sampled = np.zeros((self.K, self.T, self.dim_x))
                 gather_trajectories(tr, self.K, sampled, self.process_group)
             else:
-                sampled[:] = tr.double().cpu().numpy()
+                sampled = tr.double().cpu().numpy()   # a fresh array, returned as is (no second copy)
+        else:
+            sampled = np.zeros((self.K, self.T, self.dim_x))
         self.u_prev[:-1] = u[1:]
         self.u_prev[-1] = u[-1]
         self._prefetch_noise(eng)

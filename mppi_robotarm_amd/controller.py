@@ -289,19 +289,28 @@ class MPPIControllerForPathTracking:
         if self.visualize_optimal_traj:
             optimal_traj = eng.optimal_traj_host(x0, u)
 
-        sampled_traj_list = np.zeros((self.K, self.T, self.dim_x))
         if self.visualze_sampled_trajs:
             tr = eng.trajectories(base_u=None, noise=self._noise_dev)   # pre-update u, v[k, t-1]
-            if world > 1:
-                from .distributed import gather_trajectories
-                gather_trajectories(tr, self.K, sampled_traj_list, self.process_group)
-            else:
-                sampled_traj_list[:] = tr.double().cpu().numpy()
+            sampled_traj_list = self._sampled_host(tr, world)
+        else:
+            sampled_traj_list = np.zeros((self.K, self.T, self.dim_x))
 
         self.u_prev[:-1] = u[1:]
         self.u_prev[-1] = u[-1]
         self._prefetch_noise(eng)
         return u[0], u, optimal_traj, sampled_traj_list
+
+    def _sampled_host(self, tr: torch.Tensor, world: int) -> np.ndarray:
+        """sampled_traj_list (K, T, 4) fp64 (control.py:135-145) from the device re-roll: widened to fp64 on
+        the device and read back into a fresh host array that is returned as is (no second 134 MB copy into
+        an np.zeros: 26 -> ~8 ms per call at K = 65536, tools/sampled_latency.py); the ranks' shards
+        gathered into one array with a process group."""
+        if world > 1:
+            from .distributed import gather_trajectories
+            out = np.zeros((self.K, self.T, self.dim_x))
+            gather_trajectories(tr, self.K, out, self.process_group)
+            return out
+        return tr.double().cpu().numpy()
 
     def _fresh_sampled(self) -> np.ndarray:
         """A fresh writable zero array for sampled_traj_list (control.py:137: np.zeros each call, 134 MB at
@@ -419,19 +428,14 @@ class MPPIControllerForPathTracking:
             eng.rollout(self._noise_dev, S_out=S_out, fused_update=True, host_out=True)
         else:
             self._multi_rollout(eng, S_out, fused=True)
-        sampled_traj_list = np.zeros((self.K, self.T, self.dim_x))
         tr = None
         if self.visualze_sampled_trajs:
             tr = eng.trajectories(base_u=u_before, noise=self._noise_dev)   # pre-update u, v[k, t-1]
         u_new, traj = eng.wait_outputs(x0 if self.visualize_optimal_traj else None)
         if self.keep_costs:
             self.last_S = self._S_dev.cpu().numpy()
-        if tr is not None:
-            if world > 1:
-                from .distributed import gather_trajectories
-                gather_trajectories(tr, self.K, sampled_traj_list, self.process_group)
-            else:
-                sampled_traj_list[:] = tr.double().cpu().numpy()
+        sampled_traj_list = (self._sampled_host(tr, world) if tr is not None
+                             else np.zeros((self.K, self.T, self.dim_x)))
         # next step's noise after the last read-back: the draw overlaps the caller's
         # work between ticks instead of sitting in front of this call's wait
         self._prefetch_noise(eng)
