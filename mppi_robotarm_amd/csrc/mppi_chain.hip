@@ -1718,7 +1718,8 @@ namespace {
 // the same ChainStateD step as the fp64 rollout.  One sequential trajectory: the host's fp64 is ~5x the
 // device's single lane here (~1.7 us per step of dependent VALU on one wave).
 template <int N>
-void chain_traj_host(const double* kd, const double* x0, const double* u_new, int T, double* out) {
+__attribute__((always_inline)) inline void chain_traj_body(const double* kd, const double* x0, const double* u_new,
+                                                           int T, double* out) {
     ChainStateD<N> x;
     x.load(x0);
     for (int t = 0; t < T; ++t) {
@@ -1731,6 +1732,19 @@ void chain_traj_host(const double* kd, const double* x0, const double* u_new, in
             out[(size_t)t * 2 * N + N + a] = x.dq[a];
         }
     }
+}
+// The step's fma() calls as the hardware instruction where the CPU has it (the baseline x86-64 target calls
+// libm's fma ~600 times per step set); fma is correctly rounded either way, so the results are the same bits.
+template <int N>
+__attribute__((target("fma"))) void chain_traj_host_fma(const double* kd, const double* x0, const double* u_new,
+                                                        int T, double* out) {
+    chain_traj_body<N>(kd, x0, u_new, T, out);
+}
+template <int N>
+void chain_traj_host(const double* kd, const double* x0, const double* u_new, int T, double* out) {
+    static const bool hw_fma = __builtin_cpu_supports("fma");
+    if (hw_fma) chain_traj_host_fma<N>(kd, x0, u_new, T, out);
+    else chain_traj_body<N>(kd, x0, u_new, T, out);
 }
 }  // namespace
 
