@@ -469,11 +469,12 @@ class ChainMPPIController:
         S_out = self._S_dev if self.keep_costs else None
         if world > 1 and self._xmode is None:
             self._multi_setup(eng, float(epsilon[0, 0, 0] + epsilon[-1, -1, -1]) if epsilon is not None else None)
-        if world == 1 and self.T >= 5 and not self.visualze_sampled_trajs:
+        if self.T >= 5 and not self.visualze_sampled_trajs and (world == 1 or self._xmode == "launch"):
             # the update of control.py:120-149 inside the launch (the median of 10 is a selection and the
             # add the same fp64 add: the host path's values), one read-back, the optimal trajectory in fp64
-            # on the host, the next step's device noise queued behind the launch
-            eng.rollout(self._noise_dev, S_out=S_out, fused_update=True, host_out=True)
+            # on the host, the next step's device noise queued behind the launch; with a process group the
+            # same launch trades the ranks' rows first (the in-launch exchange)
+            eng.rollout(self._noise_dev, S_out=S_out, fused_update=True, exchange=world > 1, host_out=True)
             # the next step's draw right behind the launch and its read-back (stream order: it starts once the rollout has read
             # the buffer), so it runs under the read-back, the host trajectory and the caller's work
             self._prefetch_noise(eng)

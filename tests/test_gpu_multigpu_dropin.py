@@ -121,13 +121,13 @@ def _device_ticks(pg, exchange):
     return out
 
 
-def _chain_step(pg, exchange):
+def _chain_step(pg, exchange, sampled=True):
     from mppi_robotarm_amd.chain import ChainMPPIController, ChainParams
     g, paths = load_step("runpy_k100_t30"), load_paths()
     c = ChainMPPIController(float(g["delta_t"]), paths[str(g["path"])], int(g["T"]), int(g["K"]),
                             float(g["param_exploration"]), float(g["param_lambda"]), float(g["param_alpha"]),
                             g["sigma"], g["stage_cost_weight"], g["terminal_cost_weight"],
-                            visualze_sampled_trajs=True, chain=ChainParams.from_arm2(), u_init=g["u_prev"],
+                            visualze_sampled_trajs=sampled, chain=ChainParams.from_arm2(), u_init=g["u_prev"],
                             process_group=pg, exchange=exchange)
     c.prev_waypoints_idx = int(g["prev_idx"])
     np.random.seed(int(g["seed"]))
@@ -142,6 +142,8 @@ SCENARIOS = {
     "loop_auto": (_loop, "auto"),
     "dev_auto": (_device_ticks, "auto"), "dev_rccl": (_device_ticks, "rccl"),
     "chain_auto": (_chain_step, "auto"), "chain_rccl": (_chain_step, "rccl"),
+    # no sampled re-roll: the chain's fused step (update in the launch, after the in-launch exchange)
+    "chainfused_auto": (lambda pg, ex: _chain_step(pg, ex, sampled=False), "auto"),
 }
 
 
@@ -220,11 +222,14 @@ def test_device_noise_ticks_take_the_one_call_native_tick(ranks):
     assert bool(r["bound"]), "the multi-GPU drop-in did not reach mppi_dropin_tick"
 
 
-@pytest.mark.parametrize("mode", ["auto", "rccl"])
+@pytest.mark.parametrize("mode", ["auto", "rccl", "fused"])
 def test_sharded_chain_n2_matches_reference_fixture(ranks, mode):
     g = load_step("runpy_k100_t30")
-    r = _get(ranks[0], f"chain_{mode}")
+    r = _get(ranks[0], "chainfused_auto" if mode == "fused" else f"chain_{mode}")
     assert _urel(r["u_seq"], g["u_seq"]) < U_TOL
     assert int(r["prev"]) == int(g["prev_idx_after"])
     np.testing.assert_allclose(r["opt"], g["optimal_traj"], rtol=1e-4, atol=1e-4)
-    np.testing.assert_allclose(r["samp"], g["sampled_traj"], rtol=1e-4, atol=1e-4)
+    if mode == "fused":
+        assert not np.any(r["samp"])                  # control.py:135 zeros without the re-roll
+    else:
+        np.testing.assert_allclose(r["samp"], g["sampled_traj"], rtol=1e-4, atol=1e-4)
