@@ -475,8 +475,8 @@ class ChainMPPIController:
             # on the host, the next step's device noise queued behind the launch; with a process group the
             # same launch trades the ranks' rows first (the in-launch exchange)
             eng.rollout(self._noise_dev, S_out=S_out, fused_update=True, exchange=world > 1, host_out=True)
-            # the next step's draw right behind the launch and its read-back (stream order: it starts once the rollout has read
-            # the buffer), so it runs under the read-back, the host trajectory and the caller's work
+            # the next step's draw right behind the launch and its read-back (stream order: it starts once
+            # the rollout has read the buffer), so it runs under the host trajectory and the caller's work
             self._prefetch_noise(eng)
             sampled = self._fresh_sampled()                     # control.py:135, while the launch runs
             u_new, traj = eng.wait_outputs(x0 if self.visualize_optimal_traj else None)
