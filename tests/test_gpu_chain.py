@@ -505,3 +505,30 @@ def test_chain_optimal_traj_host_against_oracle():
         want[t, :7], want[t, 7:] = q[0], dq[0]
     eng.close()
     np.testing.assert_allclose(got, want, rtol=1e-12, atol=1e-12)
+
+
+def test_chain_debug_and_output_entry_points_refuse_misuse(paths):
+    """The new chain entry points fail loudly with the reference's exception classes (MPPI_E_ARG ->
+    ValueError): the fused outputs without a fused launch, after the nominal was re-staged, and the
+    slot-recording build on a chain it is not built for (only 7 links)."""
+    P, x0, sig, ug = _c5()
+    eng = _engine(512, 8)
+    win = paths["xydq_circle"][:30]
+    u = np.tile(ug, (8, 1))
+    eng.set_step_inputs(x0, win, u)
+    noise = eng.philox_noise(1, 0)
+    eng.rollout(noise)                                   # no fused update
+    with pytest.raises(ValueError, match="fused"):
+        eng.wait_outputs()
+    eng.rollout(noise, fused_update=True, host_out=True)
+    got, _ = eng.wait_outputs()
+    assert got.shape == (8, 7) and np.all(np.isfinite(got))
+    eng.set_step_inputs(x0, win, u + 1.0)                # a different nominal staged: no update to read
+    with pytest.raises(ValueError, match="fused"):
+        eng.wait_outputs()
+    eng.close()
+    from mppi_robotarm_amd.chain import ChainEngine, ChainParams
+    e2 = ChainEngine(256, 8, 0.006, 100.0, 0.98, np.eye(2) * 20.0, W, TW, 0.0, ChainParams.from_arm2(), device=0)
+    with pytest.raises(ValueError, match="7-link"):
+        e2.debug_slots(e2.philox_noise(1, 0))
+    e2.close()
