@@ -23,7 +23,7 @@ import torch
 from scipy.ndimage import median_filter
 
 from . import _native as N
-from .controller import first_min_index
+from .controller import PinnedReadback, first_min_index
 from .distributed import attach_exchange, check_exchange, exchange_partials, same_on_all_ranks, shard_geometry
 
 SEARCH_IDX_LEN = 30  # control.py:203
@@ -358,6 +358,7 @@ class ChainMPPIController:
         self._engine_built_for = None
         self._noise_ready = None       # (seed, step) of the device noise already in the buffer
         self._last_sampled = None      # the previous call's sampled_traj_list (_fresh_sampled)
+        self._sampled_pool = PinnedReadback()   # sampled_traj_list's read-back buffers
         self._step_count = 0
         self.keep_costs = False
         self.last_S = None
@@ -508,7 +509,7 @@ class ChainMPPIController:
                 sampled = np.zeros((self.K, self.T, self.dim_x))
                 gather_trajectories(tr, self.K, sampled, self.process_group)
             else:
-                sampled = tr.double().cpu().numpy()   # a fresh array, returned as is (no second copy)
+                sampled = self._sampled_pool(tr)   # the caller's alone, as a fresh array (PinnedReadback)
         else:
             sampled = np.zeros((self.K, self.T, self.dim_x))
         self.u_prev[:-1] = u[1:]
@@ -538,3 +539,4 @@ class ChainMPPIController:
         self._engine_built_for = None
         self._noise_ready = None       # a new engine's noise buffer is fresh: draw again
         self._xmode = None
+        self._sampled_pool.clear()

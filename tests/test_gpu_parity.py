@@ -829,3 +829,38 @@ def test_random_configs_against_c_oracle(i, K, T, lam, lps, expl, prev, paths):
     _, ref_weps = coracle.weighted_noise(ref_S, eps_tk, lam, layout="TK")
     assert _urel(w_eps, ref_weps) < U_TOL
     eng.close()
+
+
+def test_sampled_trajs_arrays_stay_the_callers_across_calls(paths):
+    """sampled_traj_list comes from pinned read-back buffers (PinnedReadback): every call's array matches the
+    reference's (control.py:135-145) and no later call writes into an array the caller still holds, written to
+    or viewed; dropped arrays' buffers come back."""
+    g = load_step("runpy_k100_t30")
+    assert "sampled_traj" in g
+    c = _ctrl(g, paths)
+    eps = g["eps"].astype(np.float64)
+    c._calc_epsilon = lambda *a, **k: eps
+
+    def call():
+        c.prev_waypoints_idx = int(g["prev_idx"])
+        c.u_prev[:] = g["u_prev"]
+        samp = c.calc_control_input(g["x0"])[3]
+        np.testing.assert_allclose(samp, g["sampled_traj"], rtol=1e-4, atol=1e-4)
+        return samp
+
+    held = [call() for _ in range(5)]            # 3 pinned buffers, then plain read-backs
+    ref = held[0].copy()
+    for i, a in enumerate(held):
+        assert a.flags.writeable and a.dtype == np.float64
+        assert not any(np.shares_memory(a, b) for b in held[i + 1:])
+    held[1][:] = -7.0                            # the caller's to write
+    view = held[2][3:, 5]
+    del held[2:]
+    for _ in range(4):
+        a = call()
+        assert not np.shares_memory(a, held[0]) and not np.shares_memory(a, held[1])
+        assert not np.shares_memory(a, view)
+    np.testing.assert_array_equal(held[0], ref)
+    assert np.all(held[1] == -7.0)
+    np.testing.assert_array_equal(view, ref[3:, 5])
+    c.close()

@@ -238,3 +238,32 @@ def test_host_nearest_waypoint_skips_nan_rows(paths):
     assert c._get_nearest_waypoint(x0[0], x0[1])[0] == want
     path[0] = np.nan                            # a NaN in row 0 of the window: chosen
     assert c._get_nearest_waypoint(x0[0], x0[1])[0] == 0
+
+
+def test_sampled_readback_buffers_are_never_shared_with_a_live_array():
+    """sampled_traj_list comes from a pool of read-back buffers (page-locked on the GPU); a buffer is reused only
+    once the caller holds neither its array nor any view of it, so each returned array behaves as the fresh
+    np.zeros of control.py:137 (CPU tensors here: the pool logic without pinning)."""
+    import torch
+    from mppi_robotarm_amd.controller import PinnedReadback
+    rb = PinnedReadback()
+    tr = [torch.full((6, 5, 4), float(i) + 0.25, dtype=torch.float32) for i in range(8)]
+    a1 = rb(tr[1])
+    assert a1.dtype == np.float64 and a1.shape == (6, 5, 4) and a1.flags.writeable and np.all(a1 == 1.25)
+    a2 = rb(tr[2])
+    assert not np.shares_memory(a1, a2) and np.all(a1 == 1.25)
+    p1 = a1.__array_interface__["data"][0]
+    del a1
+    a3 = rb(tr[3])                                 # a1's buffer is free again
+    assert a3.__array_interface__["data"][0] == p1 and np.all(a3 == 3.25) and np.all(a2 == 2.25)
+    v = a2[2:, 1]                                  # a view keeps a2's buffer out of reuse
+    del a2
+    a4 = rb(tr[4])
+    assert np.all(v == 2.25) and not np.shares_memory(a4, v) and not np.shares_memory(a4, a3)
+    a5 = rb(tr[5])                                 # pool full (3 held): a plain read-back
+    assert np.all(a5 == 5.25) and len(rb) == 3
+    assert not any(np.shares_memory(a5, x) for x in (a3, a4, v))
+    a5[:] = -1.0                                   # writable, and nobody else's
+    assert np.all(a3 == 3.25) and np.all(a4 == 4.25) and np.all(v == 2.25)
+    a6 = rb(torch.zeros((3, 5, 4)))                # K changed: new buffers, held arrays intact
+    assert a6.shape == (3, 5, 4) and np.all(a3 == 3.25) and np.all(v == 2.25)
