@@ -15,6 +15,8 @@ ROOT = os.path.dirname(HERE)
 CSRC = os.path.join(HERE, "csrc")
 SRCS = [os.path.join(CSRC, "mppi_rocm.hip"), os.path.join(CSRC, "mppi_chain.hip")]
 OUT = os.path.join(HERE, "_lib", "libmppi_rocm.so")
+HOST_RNG_SRC = os.path.join(CSRC, "np_legacy_gauss.c")
+HOST_RNG_OUT = os.path.join(HERE, "_lib", "libmppi_hostrng.so")
 ARCH = os.environ.get("MPPI_OFFLOAD_ARCH", "gfx950")
 
 
@@ -50,5 +52,16 @@ def build_native(force: bool = False, extra_flags: list[str] | None = None, out:
     return out
 
 
+def build_host_rng(force: bool = False) -> str:
+    """csrc/np_legacy_gauss.c -> _lib/libmppi_hostrng.so: host C, no contraction, so its values equal NumPy's."""
+    if not force and os.path.exists(HOST_RNG_OUT) and os.path.getmtime(HOST_RNG_OUT) >= os.path.getmtime(HOST_RNG_SRC):
+        return HOST_RNG_OUT
+    os.makedirs(os.path.dirname(HOST_RNG_OUT), exist_ok=True)
+    subprocess.run(["gcc", "-O3", "-fPIC", "-shared", "-ffp-contract=off", "-fno-fast-math", "-pthread", "-o",
+                    HOST_RNG_OUT, HOST_RNG_SRC, "-lm"], check=True)
+    return HOST_RNG_OUT
+
+
 if __name__ == "__main__":
     print(build_native(force=True))
+    print(build_host_rng(force=True))

@@ -6,7 +6,8 @@ spelling), same ``calc_control_input(observed_x)`` contract (control.py:67-152):
   * host, fp64 NumPy (O(T) work, exactly as the reference):
       nearest-waypoint update + end-of-path ``IndexError`` (control.py:75-78),
       noise draw ``np.random.multivariate_normal`` on the legacy global RNG
-      (control.py:154-164, same stream as the reference),
+      (control.py:154-164, same stream as the reference; its standard-normal
+      stream threaded in C with the same values, ``hostrng``),
       ``np.linalg.inv(Sigma)`` (``LinAlgError`` as at control.py:106),
       and the aliasing return (``u0`` is a view of the shifted ``u_prev``;
       ``u_seq is self.u_prev``);
@@ -51,6 +52,7 @@ from scipy.ndimage import median_filter
 
 import dataclasses
 
+from . import hostrng
 from .distributed import attach_exchange, check_exchange, exchange_partials, same_on_all_ranks, shard_geometry
 from .engine import RolloutEngine
 from .params import ArmParams
@@ -509,7 +511,7 @@ class MPPIControllerForPathTracking:
         """sample epsilon (control.py:154-164) — the reference's RNG stream"""
         self._check_sigma(sigma, size_dim_u)
         mu = np.full((size_dim_u), 0.0)
-        return np.random.multivariate_normal(mu, sigma, (size_sample, size_time_step))
+        return hostrng.multivariate_normal(mu, sigma, (size_sample, size_time_step))   # NumPy's values, threaded
 
     def _g(self, v: np.ndarray) -> float:
         """clamp input (disabled in the reference, control.py:166-172)"""

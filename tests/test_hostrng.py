@@ -1,0 +1,67 @@
+"""The drop-in's NumPy-stream noise (control.py:154-164): hostrng.multivariate_normal, whose standard-normal
+stream is threaded in C (csrc/np_legacy_gauss.c), equals np.random.multivariate_normal value for value and
+leaves the global RNG in the state NumPy leaves (the next draws agree too)."""
+import numpy as np
+import pytest
+
+from mppi_robotarm_amd import hostrng
+from mppi_robotarm_amd.build import build_host_rng
+
+build_host_rng()   # gcc, under a second; a no-op when the library is current
+
+
+def _state_eq(a, b):
+    return a[0] == b[0] and np.array_equal(a[1], b[1]) and a[2] == b[2] and a[3] == b[3] and a[4] == b[4]
+
+
+def test_library_is_built_and_used():
+    np.random.seed(5)
+    assert hostrng.legacy_standard_normal(1 << 16) is not None
+
+
+@pytest.mark.parametrize("seed,size,cov", [
+    (0, (16384, 64), np.eye(2) * 20.0),                       # run.py's Sigma
+    (3, (4097, 31), np.array([[20.0, 5.0], [5.0, 10.0]])),    # non-diagonal, odd count of pairs
+    (7, (20001, 3), np.eye(7) * 3.0 + 0.5),                   # the 7-link chain's dimension, odd total
+    (11, (1 << 15, 1), np.eye(1) * 2.0),
+    (13, (1000, 7), np.eye(2)),                               # below the threshold: NumPy itself
+])
+@pytest.mark.parametrize("pre", [0, 1, 1001])                 # stream position; an odd pre leaves a cached Gaussian
+def test_equals_numpy_multivariate_normal(seed, size, cov, pre):
+    mu = np.zeros(cov.shape[0])
+    np.random.seed(seed)
+    np.random.standard_normal(pre)
+    a = np.random.multivariate_normal(mu, cov, size)
+    sa = np.random.get_state()
+    na = np.random.standard_normal(5)
+    np.random.seed(seed)
+    np.random.standard_normal(pre)
+    b = hostrng.multivariate_normal(mu, cov, size)
+    sb = np.random.get_state()
+    nb = np.random.standard_normal(5)
+    assert a.shape == b.shape and a.dtype == b.dtype
+    assert np.array_equal(a, b)
+    assert _state_eq(sa, sb)
+    assert np.array_equal(na, nb)
+
+
+def test_state_at_block_boundaries_and_retry_sizes():
+    """Positions at 0 / 623 / 624 within the key array and draws that end at every parity."""
+    for pos_skip in (0, 623, 624, 1248):
+        for n in (1 << 15, (1 << 15) + 1, (1 << 15) + 2, 100003):
+            np.random.seed(17)
+            np.random.randint(0, 2**31, size=pos_skip, dtype=np.int64)   # advance the word position
+            s0 = np.random.get_state()
+            a = np.random.standard_normal(n)
+            sa = np.random.get_state()
+            np.random.set_state(s0)
+            b = hostrng.legacy_standard_normal(n)
+            assert b is not None and np.array_equal(a, b)
+            assert _state_eq(sa, np.random.get_state())
+
+
+def test_errors_are_numpys():
+    with pytest.raises(ValueError):
+        hostrng.multivariate_normal(np.zeros(2), np.eye(3), (40000, 2))
+    with pytest.warns(RuntimeWarning):
+        hostrng.multivariate_normal(np.zeros(2), np.array([[1.0, 2.0], [0.0, 1.0]]), (40000, 2))
