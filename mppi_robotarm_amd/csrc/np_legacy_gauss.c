@@ -199,6 +199,11 @@ int mppi_np_legacy_gauss(uint32_t* key, int* pos, int* has_gauss, double* gauss,
                          int nthreads) {
     pthread_mutex_lock(&g_mu);
     const int rc = legacy_gauss_locked(key, pos, has_gauss, gauss, out, n, nthreads);
+    if (g_cap * MT_N * (int64_t)sizeof(uint32_t) > ((int64_t)256 << 20)) {   // not kept past 256 MB (config 5's
+        free(g_blocks);                                                        // 1.2 GB draw buffer)
+        g_blocks = NULL;
+        g_cap = 0;
+    }
     pthread_mutex_unlock(&g_mu);
     return rc;
 }
