@@ -316,6 +316,8 @@ typedef struct {
                                                (for spread weights: see DESIGN §3b)       */
     int lanes_per_sample;                   /* 0 = auto; 1, or 4 (fp32: a quad per sample,
                                                lane p the link pair (2p, 2p+1))           */
+    double param_gamma;                     /* as mppi_config.param_gamma: control.py:45's
+                                               gamma as given; NaN = lambda (1 - alpha)  */
 } mppi_chain_config;
 
 typedef struct mppi_chain_ctx mppi_chain_ctx;
@@ -347,6 +349,13 @@ int mppi_chain_get_nominal(mppi_chain_ctx *ctx, double *u_host);
  * With MPPI_FLAG_HOST_OUT on that launch, the chain queues this read-back right
  * behind it, so work queued afterwards (the next noise) does not delay the wait. */
 int mppi_chain_wait_outputs(mppi_chain_ctx *ctx, const double *x0, double *u_out, double *traj_out);
+/* The spread of the last step's weights (control.py:297-314): eta = sum_k
+ * exp(-(S_k - min S) / lambda) of the update read by mppi_chain_wait_outputs or
+ * the weighted noise read by mppi_chain_get_weighted_noise (NaN before either);
+ * eta >= 1, and eta - 1 is the weight outside the best sample (0: one-hot).
+ * ChainMPPIController's precision="auto" re-runs a step in fp64 when it exceeds
+ * 1e-6. */
+int mppi_chain_last_eta(const mppi_chain_ctx *ctx, double *eta);
 /* control.py:129-134 for the chain on the host in fp64: traj_out[T][2n] from x0[2n]
  * and the updated (not yet shifted) controls u_new[T][n]. */
 int mppi_chain_optimal_traj_host(mppi_chain_ctx *ctx, const double *x0, const double *u_new, double *traj_out);

@@ -42,7 +42,7 @@ EXPORTS = (
     "mppi_chain_exchange_attach",
     "mppi_chain_get_weighted_noise", "mppi_chain_get_nominal", "mppi_chain_rollout_traj",
     "mppi_chain_noise_philox", "mppi_chain_sync", "mppi_chain_debug_set_buffer", "mppi_chain_debug_slots",
-    "mppi_chain_wait_outputs", "mppi_chain_optimal_traj_host",
+    "mppi_chain_wait_outputs", "mppi_chain_optimal_traj_host", "mppi_chain_last_eta",
 )
 
 
@@ -87,7 +87,13 @@ class ChainConfigC(C.Structure):
         ("param_exploration", C.c_double), ("sigma", C.c_double * (CHAIN_MAX_DOF * CHAIN_MAX_DOF)),
         ("stage_cost_weight", C.c_double * 4), ("terminal_cost_weight", C.c_double * 4),
         ("chain", ChainParamsC), ("precision", C.c_int), ("lanes_per_sample", C.c_int),
+        ("param_gamma", C.c_double),
     ]
+
+    def __init__(self, *args, **kw):
+        super().__init__(*args, **kw)
+        if "param_gamma" not in kw and len(args) < len(self._fields_):
+            self.param_gamma = float("nan")   # gamma = lambda (1 - alpha), control.py:45
 
 
 class MPPIError(RuntimeError):
@@ -152,6 +158,7 @@ def open_library(path: str):
         "mppi_chain_debug_slots": ([vp, fp, vp, vp], C.c_int),
         "mppi_chain_wait_outputs": ([vp, dp, dp, dp], C.c_int),
         "mppi_chain_optimal_traj_host": ([vp, dp, dp, dp], C.c_int),
+        "mppi_chain_last_eta": ([vp, dp], C.c_int),
     }
     for name, (args, res) in sig.items():
         if not hasattr(L, name):   # an older diagnostic build (tools/ab.py); load() checks the product's exports

@@ -34,10 +34,10 @@ def build_native(force: bool = False, extra_flags: list[str] | None = None, out:
             all(os.path.getmtime(out) >= os.path.getmtime(d) for d in deps):
         return out
     os.makedirs(os.path.dirname(out), exist_ok=True)
-    # -amdgpu-mfma-vgpr-form: MFMA results straight into VGPRs (the window-key MFMAs of the
-    # opt-in SearchMFMA are read by VALU; the AGPR form adds a v_accvgpr_read per key)
+    # host side without contraction: the fp64 host steps (waypoint update, optimal trajectories) fuse only
+    # their explicit fma() calls, whatever the CPU target (the chain's target("fma") instance included)
     flags = [f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-I", os.path.join(ROOT, "include"),
-             "-mllvm", "-amdgpu-mfma-vgpr-form"]
+             "-Xarch_host", "-ffp-contract=off"]
     flags += list(extra_flags or [])
     objs, procs = [], []
     for src in SRCS:

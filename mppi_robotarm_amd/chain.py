@@ -103,7 +103,8 @@ class ChainEngine:
     def __init__(self, K_local: int, T: int, delta_t: float, param_lambda: float, param_alpha: float, sigma,
                  stage_cost_weight, terminal_cost_weight, param_exploration: float = 0.0,
                  chain: ChainParams = ChainParams(), K_total: int | None = None, k_offset: int = 0,
-                 device: int | torch.device | None = None, precision: str = "f32", lanes_per_sample: int = 0):
+                 device: int | torch.device | None = None, precision: str = "f32", lanes_per_sample: int = 0,
+                 param_gamma: float | None = None):
         self._lib = N.load()
         if precision not in ("f32", "f64"):
             raise ValueError("precision must be 'f32' or 'f64'")
@@ -135,6 +136,8 @@ class ChainEngine:
         cfg.chain.g = float(chain.g)
         cfg.precision = 1 if precision == "f64" else 0
         cfg.lanes_per_sample = int(lanes_per_sample)
+        # gamma as given (control.py:45 fixes it at construction); None: lambda (1 - alpha)
+        cfg.param_gamma = float("nan") if param_gamma is None else float(param_gamma)
         with torch.cuda.device(self.device):
             self.stream = torch.cuda.current_stream(self.device)
             ctx = C.c_void_p()
@@ -271,6 +274,13 @@ class ChainEngine:
                 "mppi_chain_wait_outputs")
         return u, traj
 
+    def last_eta(self) -> float:
+        """eta = sum_k exp(-(S_k - min S) / lambda) of the last update (wait_outputs) or weighted noise
+        (weighted_noise) read back: 1 for one-hot weights, eta - 1 the weight outside the best sample."""
+        v = C.c_double()
+        N.check(self._lib.mppi_chain_last_eta(self._ctx, C.byref(v)), "mppi_chain_last_eta")
+        return v.value
+
     def optimal_traj_host(self, x0, u_new) -> np.ndarray:
         """(T, 2n) fp64 optimal trajectory of control.py:129-134 from the updated, not yet shifted
         controls u_new (T, n), on the host (mppi_chain_optimal_traj_host)."""
@@ -330,7 +340,17 @@ class ChainEngine:
 
 
 class ChainMPPIController:
-    """control.py:20-152 for the n-link chain (dim_u = n, dim_x = 2n)."""
+    """control.py:20-152 for the n-link chain (dim_u = n, dim_x = 2n).
+
+    ``precision``: the rollout arithmetic.  "f32" (fastest) or "f64" (ChainStateD, ~2.9x the time), or "auto"
+    (the default): fp32 while the weights are one-hot, fp64 where they spread.  In fp32 a nearest-waypoint tie
+    of a weighted sample can move its S by a whole stage-cost step, which reaches w_eps only when
+    more than one sample carries weight; so after each fp32 step the spread of its weights, eta - 1 =
+    sum_k exp(-(S_k - min S) / lambda) - 1 (mppi_chain_last_eta), is checked, and a step whose weights spread
+    (eta - 1 > ETA_TOL) is run again in fp64 from the same inputs, as are the steps after it until the weights
+    are one-hot again.  run.py's lambda = 100 keeps them one-hot (eta - 1 ~ 0): the fp32 step alone."""
+
+    ETA_TOL = 1e-6   # weight outside the best sample above which precision="auto" takes the fp64 rollout
 
     def __init__(self, delta_t: float = 0.006, ref_path=0, horizon_step_T: int = 128,
                  number_of_samples_K: int = 131072, param_exploration: float = 0.0, param_lambda: float = 100.0,
@@ -339,14 +359,15 @@ class ChainMPPIController:
                  terminal_cost_weight: np.ndarray = np.array([5.0, 5.0, 50.0, 50.0]),
                  visualize_optimal_traj=True, visualze_sampled_trajs=False, *, chain: ChainParams = ChainParams(),
                  u_init=None, device: int | None = None, verbose: bool = False, noise: str = "numpy", seed: int = 0,
-                 process_group=None, exchange: str = "auto", precision: str = "f32") -> None:
+                 process_group=None, exchange: str = "auto", precision: str = "auto") -> None:
         self.chain = chain
-        self.precision = precision   # rollout arithmetic: "f64" where the weights are spread
+        if precision not in ("auto", "f32", "f64"):
+            raise ValueError("precision must be 'auto', 'f32' or 'f64'")
+        self.precision = precision
         self.dim_u, self.dim_x = chain.n, 2 * chain.n
         self.T, self.K = horizon_step_T, number_of_samples_K
         self.param_exploration, self.param_lambda, self.param_alpha = param_exploration, param_lambda, param_alpha
         self.param_gamma = self.param_lambda * (1.0 - self.param_alpha)
-        self._lambda0 = self.param_lambda
         self.Sigma = np.asarray(sigma, dtype=np.float64)
         self.stage_cost_weight, self.terminal_cost_weight = stage_cost_weight, terminal_cost_weight
         self.visualize_optimal_traj, self.visualze_sampled_trajs = visualize_optimal_traj, visualze_sampled_trajs
@@ -361,16 +382,36 @@ class ChainMPPIController:
         if exchange not in ("auto", "launch", "rccl"):
             raise ValueError("exchange must be 'auto', 'launch' or 'rccl'")
         self.exchange = exchange      # multi-GPU: as MPPIControllerForPathTracking
-        self._xmode = None
         self._device = device
+        self._slots = {}               # rollout precision -> the parked state of its engine (_SLOT fields)
+        self._active = None            # the precision whose engine the fields below hold
         self._engine = None
         self._engine_built_for = None
+        self._xmode = None
         self._noise_ready = None       # (seed, step) of the device noise already in the buffer
+        self._spread = False           # precision="auto": the last step's weights were spread (next step fp64)
+        self.last_precision = None     # the rollout precision of the last step's result
+        self.last_eta = None           # and the spread of its weights (eta, mppi_chain_last_eta)
         self._last_sampled = None      # the previous call's sampled_traj_list (_fresh_sampled)
         self._sampled_pool = PinnedReadback()   # sampled_traj_list's read-back buffers
         self._step_count = 0
         self.keep_costs = False
         self.last_S = None
+
+    # the per-engine fields: the active engine's live here, the others' are parked in _slots
+    _SLOT = ("_engine", "_engine_built_for", "_xmode", "_noise_ready", "_noise_dev", "_partial", "_S_dev",
+             "_gathered")
+
+    def _activate(self, precision: str) -> None:
+        """Make the engine of `precision` (built on first use) the one the fields above refer to."""
+        if self._active == precision:
+            return
+        if self._active is not None:
+            self._slots[self._active] = {f: getattr(self, f, None) for f in self._SLOT}
+        parked = self._slots.pop(precision, {})
+        for f in self._SLOT:
+            setattr(self, f, parked.get(f))
+        self._active = precision
 
     def _shard(self):
         if self.process_group is None:
@@ -385,23 +426,22 @@ class ChainMPPIController:
         return (int(self.K), int(self.T), np.asarray(self.Sigma, dtype=np.float64).tobytes(), float(self.param_lambda),
                 float(self.param_gamma), np.asarray(self.stage_cost_weight, dtype=np.float64).tobytes(),
                 np.asarray(self.terminal_cost_weight, dtype=np.float64).tobytes(), float(self.param_exploration),
-                float(self.delta_t), self.chain, self.precision)
+                float(self.delta_t), self.chain, self._active)
 
     def _get_engine(self, key=None) -> ChainEngine:
         key = self._engine_key() if key is None else key
         if self._engine is not None and key != self._engine_built_for:
-            self.close()
+            self._close_active()
         if self._engine is None:
             world, rank = self._shard()
             K_local, k_offset = shard_geometry(self.K, world, rank)
             device = self._device if self._device is not None else torch.cuda.current_device()
-            # gamma stays the constructor's (control.py:45) when lambda changes: the engine takes alpha
-            alpha = (self.param_alpha if self.param_lambda == self._lambda0 or self.param_lambda == 0
-                     else 1.0 - self.param_gamma / self.param_lambda)
-            self._engine = ChainEngine(K_local, self.T, self.delta_t, self.param_lambda, alpha, self.Sigma,
+            # gamma is fixed at construction in the reference (control.py:45) while lambda is
+            # re-read per call: the engine takes gamma as given, as the 2-link engine does
+            self._engine = ChainEngine(K_local, self.T, self.delta_t, self.param_lambda, self.param_alpha, self.Sigma,
                                        self.stage_cost_weight, self.terminal_cost_weight, self.param_exploration,
                                        self.chain, K_total=self.K, k_offset=k_offset, device=device,
-                                       precision=self.precision)
+                                       precision=self._active, param_gamma=self.param_gamma)
             self._noise_dev = self._engine.new_noise()
             self._partial = self._engine.new_partial()
             self._S_dev = torch.empty(K_local, dtype=torch.float64, device=self._engine.device)
@@ -464,21 +504,40 @@ class ChainMPPIController:
             epsilon = self._calc_epsilon(self.Sigma, self.K, self.T, self.dim_u)
         else:
             epsilon = None
+        step = self._step_count
+        self._step_count += 1
+        window = self.ref_path[self.prev_waypoints_idx:(self.prev_waypoints_idx + SEARCH_IDX_LEN)]
+        auto = self.precision == "auto"
+        prec = ("f64" if self._spread else "f32") if auto else self.precision
+        out = self._device_step(prec, x0, window, u, epsilon, step)
+        if auto:
+            self._spread = self.last_eta - 1.0 > self.ETA_TOL
+            if self._spread and prec == "f32":
+                # the weights spread: this step again in fp64 from the same inputs (u is not updated yet)
+                out = self._device_step("f64", x0, window, u, epsilon, step)
+                self._spread = self.last_eta - 1.0 > self.ETA_TOL
+        u_new, optimal_traj, sampled = out
+        u[:] = u_new                                        # the shifted nominal, in place (aliasing kept)
+        return u[0], u, optimal_traj, sampled
+
+    def _device_step(self, prec: str, x0, window, u, epsilon, step: int):
+        """control.py:81-149 of one step on the engine of rollout precision `prec`: the shifted updated
+        nominal (T, n), the optimal trajectory and sampled_traj_list.  u (self.u_prev) is only read."""
+        self._activate(prec)
         key = self._engine_key()
         if key != self._engine_built_for:
             np.linalg.inv(self.Sigma)                      # LinAlgError as control.py:106 (Sigma checked when it changes)
         eng = self._get_engine(key)
         if epsilon is not None:
             eng.upload_noise(epsilon[eng.k_offset:eng.k_offset + eng.K_local], out=self._noise_dev)
-        elif self._noise_ready != (self.seed, self._step_count):
-            eng.philox_noise(self.seed, self._step_count, out=self._noise_dev)
-        self._step_count += 1
-        window = self.ref_path[self.prev_waypoints_idx:(self.prev_waypoints_idx + SEARCH_IDX_LEN)]
+        elif self._noise_ready != (self.seed, step):
+            eng.philox_noise(self.seed, step, out=self._noise_dev)
         eng.set_step_inputs(x0, window, u)
         world, _ = self._shard()
         S_out = self._S_dev if self.keep_costs else None
         if world > 1 and self._xmode is None:
             self._multi_setup(eng, float(epsilon[0, 0, 0] + epsilon[-1, -1, -1]) if epsilon is not None else None)
+        self.last_precision = prec
         if self.T >= 5 and not self.visualze_sampled_trajs and (world == 1 or self._xmode == "launch"):
             # the update of control.py:120-149 inside the launch (the median of 10 is a selection and the
             # add the same fp64 add: the host path's values), one read-back, the optimal trajectory in fp64
@@ -490,10 +549,10 @@ class ChainMPPIController:
             self._prefetch_noise(eng)
             sampled = self._fresh_sampled()                     # control.py:135, while the launch runs
             u_new, traj = eng.wait_outputs(x0 if self.visualize_optimal_traj else None)
+            self.last_eta = eng.last_eta()
             if self.keep_costs:
                 self.last_S = self._S_dev.cpu().numpy()
-            u[:] = u_new                                        # the shifted nominal, in place (aliasing kept)
-            return u[0], u, traj if traj is not None else np.zeros((self.T, self.dim_x)), sampled
+            return u_new, traj if traj is not None else np.zeros((self.T, self.dim_x)), sampled
         if world == 1:
             eng.rollout(self._noise_dev, S_out=S_out)
         elif self._xmode == "launch":
@@ -503,14 +562,15 @@ class ChainMPPIController:
             exchange_partials(self._partial, self._gathered, self.process_group)
             eng.merge(self._gathered, world)
         w_epsilon = eng.weighted_noise()
+        self.last_eta = eng.last_eta()
         if self.keep_costs:
             self.last_S = self._S_dev.cpu().numpy()
         w_epsilon = np.stack([median_filter(w_epsilon[:, d], size=10, mode="reflect")
                               for d in range(self.dim_u)], axis=1)   # control.py:319-327
-        u += w_epsilon
+        un = u + w_epsilon                                            # control.py:126 (u itself untouched here)
         optimal_traj = np.zeros((self.T, self.dim_x))
         if self.visualize_optimal_traj:
-            optimal_traj = eng.optimal_traj_host(x0, u)
+            optimal_traj = eng.optimal_traj_host(x0, un)
         if self.visualze_sampled_trajs:
             tr = eng.trajectories(base_u=None, noise=self._noise_dev)
             if world > 1:
@@ -521,10 +581,8 @@ class ChainMPPIController:
                 sampled = self._sampled_pool(tr)   # the caller's alone, as a fresh array (PinnedReadback)
         else:
             sampled = np.zeros((self.K, self.T, self.dim_x))
-        self.u_prev[:-1] = u[1:]
-        self.u_prev[-1] = u[-1]
         self._prefetch_noise(eng)
-        return u[0], u, optimal_traj, sampled
+        return np.concatenate([un[1:], un[-1:]]), optimal_traj, sampled   # control.py:148-149
 
     def _fresh_sampled(self) -> np.ndarray:
         """A fresh writable np.zeros for sampled_traj_list (1.9 GB at config 5, mapped lazily), made while the
@@ -541,11 +599,18 @@ class ChainMPPIController:
             eng.philox_noise(self.seed, self._step_count, out=self._noise_dev)
             self._noise_ready = (self.seed, self._step_count)
 
-    def close(self):
+    def _close_active(self):
         if self._engine is not None:
             self._engine.close()
             self._engine = None
         self._engine_built_for = None
         self._noise_ready = None       # a new engine's noise buffer is fresh: draw again
         self._xmode = None
+
+    def close(self):
+        self._close_active()
+        for parked in self._slots.values():
+            if parked.get("_engine") is not None:
+                parked["_engine"].close()
+        self._slots = {}
         self._sampled_pool.clear()

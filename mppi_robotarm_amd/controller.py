@@ -76,19 +76,32 @@ class PinnedReadback:
     buffer is reused only when nothing outside the pool refers to its array (views of it included: their base
     is that array), so every returned array is the caller's alone, as control.py:137's fresh np.zeros is.  The
     DMA into locked pages skips the pageable copy's staging and the first touch of a fresh array (134 MB at
-    K = 65536, T = 64: 10.4-13.3 -> 2.5 ms per call).  With every pooled buffer still held by the caller, a
-    plain pageable read-back."""
+    K = 65536, T = 64: 10.4-13.3 -> 2.5 ms per call).
 
-    MAX = 3   # buffers held at most (run.py's loop holds one array across a call, so it cycles through two)
+    Page-locked memory is bounded: at most MAX buffers and MAX_BYTES in all (a buffer larger than that, e.g.
+    the chain's 1.9 GB at config 5, is never pinned).  Past the bound, or when pinning fails, the plain
+    pageable read-back.  clear() drops the pool and returns the freed blocks that torch's caching host
+    allocator keeps to the system."""
+
+    MAX = 3                 # buffers held at most (run.py's loop holds one array across a call: it cycles through two)
+    MAX_BYTES = 768 << 20   # page-locked bytes held at most (3 x 134 MB at K = 65536, T = 64 fit)
 
     def __init__(self):
         self._pool = []   # (tensor, array over it)
 
     def clear(self) -> None:
+        had = bool(self._pool)
         self._pool = []   # arrays the caller still holds keep their tensors alive
+        if had and hasattr(torch._C, "_host_emptyCache"):
+            torch._C._host_emptyCache()   # freed page-locked blocks back to the system, not kept cached
 
     def __len__(self) -> int:
         return len(self._pool)
+
+    @staticmethod
+    def _pageable(tr: torch.Tensor) -> np.ndarray:
+        out = tr.double().cpu()
+        return (out.clone() if out.data_ptr() == tr.data_ptr() else out).numpy()   # never the caller's tensor
 
     def __call__(self, tr: torch.Tensor) -> np.ndarray:
         shape = tuple(tr.shape)
@@ -101,9 +114,12 @@ class PinnedReadback:
                 buf, arr = pool[i]
                 buf.copy_(tr.double())
                 return arr
-        if len(pool) >= self.MAX:
-            return tr.double().cpu().numpy()
-        buf = torch.empty(shape, dtype=torch.float64, pin_memory=tr.is_cuda)
+        if len(pool) >= self.MAX or (len(pool) + 1) * tr.numel() * 8 > self.MAX_BYTES:
+            return self._pageable(tr)
+        try:
+            buf = torch.empty(shape, dtype=torch.float64, pin_memory=tr.is_cuda)
+        except RuntimeError:          # page-locking refused (host limits): the pageable read-back
+            return self._pageable(tr)
         buf.copy_(tr.double())
         arr = buf.numpy()
         pool.append((buf, arr))
@@ -354,13 +370,6 @@ class MPPIControllerForPathTracking:
             gather_trajectories(tr, self.K, out, self.process_group)
             return out
         return self._sampled_pool(tr)
-        if len(pool) >= self._SAMPLED_POOL_MAX:
-            return tr.double().cpu().numpy()
-        buf = torch.empty(shape, dtype=torch.float64, pin_memory=tr.is_cuda)
-        buf.copy_(tr.double())
-        arr = buf.numpy()
-        pool.append((buf, arr))
-        return arr
 
     def _fresh_sampled(self) -> np.ndarray:
         """A fresh writable zero array for sampled_traj_list (control.py:137: np.zeros each call, 134 MB at
@@ -430,16 +439,20 @@ class MPPIControllerForPathTracking:
         self._step_count += 1
         rc = eng.dropin_tick_launch(self._step_count)
         self.prev_waypoints_idx = self._idx_buf.item(0)
-        if self.verbose:
-            print(f"0     prev_idx = {int(self._idx_buf[1])}")
-            print(f"0     nearest_idx = {self.prev_waypoints_idx}")
-            print("======================updated=======================")
         if rc != 0:                                        # MPPI_E_PATH_END: nothing was launched
+            if self.verbose:
+                self._print_update(int(self._idx_buf[1]), self.prev_waypoints_idx)
             self._step_count -= 1
             print("[ERROR] Reached the end of the reference path.")
             raise IndexError
-        sampled = self._fresh_sampled()                     # control.py:135, allocated while the launch runs
-        eng.dropin_tick_wait()
+        # the launched step is always consumed (its wait runs whatever is raised in between: a failing
+        # print or allocation, KeyboardInterrupt), so the next launch never finds a tick still pending
+        try:
+            if self.verbose:
+                self._print_update(int(self._idx_buf[1]), self.prev_waypoints_idx)
+            sampled = self._fresh_sampled()                 # control.py:135, allocated while the launch runs
+        finally:
+            eng.dropin_tick_wait()
         self._noise_ready = (self.seed, self._step_count)
         if self.keep_costs:
             self.last_S = self._S_dev.cpu().numpy()
@@ -531,11 +544,16 @@ class MPPIControllerForPathTracking:
         ref_dq2 = self.ref_path[nearest_idx, 3]
         if update_prev_idx:
             if self.verbose:
-                print(f"0     prev_idx = {prev_idx}")
-                print(f"0     nearest_idx = {nearest_idx}")
-                print("======================updated=======================")
+                self._print_update(prev_idx, nearest_idx)
             self.prev_waypoints_idx = nearest_idx
         return nearest_idx, ref_x, ref_y, ref_dq1, ref_dq2
+
+    @staticmethod
+    def _print_update(prev_idx: int, nearest_idx: int) -> None:
+        """the three progress lines of control.py:227-229"""
+        print(f"0     prev_idx = {prev_idx}")
+        print(f"0     nearest_idx = {nearest_idx}")
+        print("======================updated=======================")
 
     def _moving_median_filter(self, xx: np.ndarray, window_size: int) -> np.ndarray:
         """median smoothing per input dimension (control.py:319-327)"""

@@ -60,6 +60,7 @@ struct alignas(16) ChainStep {
     double u[kMaxT][kCMax];                // nominal control sequence, fp64
     double a[kMaxT][kCMax];                // a_t in fp64 (fp64 rollout)
     double u_first[kCMax];                 // fused update: u_new[0], the element the shift drops (optimal_traj)
+    double eta;                            // fused update: the merge's eta (read back with u_first)
 };
 
 // Launch constants (kernel argument, by value).
@@ -460,6 +461,7 @@ __device__ void chain_update_block(ChainStep* nxt, const ChainConst& c, CScratch
     }
     __syncthreads();
     if (tid < N) nxt->u_first[tid] = sm.unew[tid];
+    if (tid == 0) nxt->eta = sm.eta;
     if (tid < T) {
         const int src = tid + 1 < T ? tid + 1 : T - 1;
         double u[N];
@@ -1044,6 +1046,7 @@ __global__ __launch_bounds__(kCT) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
     STAMP(11, NOW());
     STAMP(6, (unsigned long long)sm.nrel);
     if (flags & MPPI_FLAG_EXCHANGE) exchange_merge<kCT, kCMaxCh>(xd, geo, c.inv_lambda, sm, w_eps_out, tmo);
+    if (tid == 0 && w_eps_out) w_eps_out[nval] = sm.eta;   // the weights' spread (mppi_chain_last_eta)
     if (flags & MPPI_FLAG_FUSED_UPDATE) chain_update_block<N>(nxt, c, sm, u_cur);
     STAMP(7, NOW());
 }
@@ -1064,6 +1067,7 @@ __global__ __launch_bounds__(kCT) void chain_merge_kernel(const ChainConst c, co
     const __amdgpu_buffer_rsrc_t r = rows_rsrc(parts, n * geo.stride * 8);
     merge_rows_block<kCT, kCMaxCh, true, false>(r, 0, n, geo, c.inv_lambda, sm, nullptr, 0, nullptr, w_eps_out, 0u,
                                                 nullptr);
+    if (tid == 0 && w_eps_out) w_eps_out[T * N] = sm.eta;
     if (flags & MPPI_FLAG_FUSED_UPDATE) chain_update_block<N>(nxt, c, sm, u_cur);
 }
 
@@ -1206,6 +1210,7 @@ struct mppi_chain_ctx {
     double* h_out = nullptr;       // MPPI_FLAG_HOST_OUT: the update's read-back, queued right behind the launch
     hipEvent_t out_ev = nullptr;   // ... recorded after that copy
     bool out_posted = false;
+    double last_eta = NAN;         // the weights' spread of the last update / weighted noise read back
     double h_pub[kCMaxVals] = {};
     bool f64 = false;              // cfg.precision == 1
     int lps = 1;                   // lanes per sample: 1, or 4 (fp32 rollout at small K)
@@ -1389,7 +1394,8 @@ int mppi_chain_ctx_create(const mppi_chain_config* cfg, int device, void* stream
     memcpy(c->h_dynd, dynd, sizeof(dynd));
     k.lambda = cfg->param_lambda;
     k.inv_lambda = 1.0 / cfg->param_lambda;
-    k.gamma = cfg->param_lambda * (1.0 - cfg->param_alpha);
+    // control.py:45 fixes gamma at construction; the caller passes it as given (NaN: lambda (1 - alpha))
+    k.gamma = isnan(cfg->param_gamma) ? cfg->param_lambda * (1.0 - cfg->param_alpha) : cfg->param_gamma;
     for (int i = 0; i < n * n; ++i) k.sig_inv[i] = Si[i];
 
     auto cleanup_fail = [&](int rc) {
@@ -1431,7 +1437,7 @@ int mppi_chain_ctx_create(const mppi_chain_config* cfg, int device, void* stream
         (e = hipMalloc(&c->d_slab, slab)) != hipSuccess || (e = hipMalloc(&c->d_gslab, gslab)) != hipSuccess ||
         (e = hipMalloc(&c->d_counter, ctr_bytes)) != hipSuccess ||
         (e = hipMalloc(&c->d_runmin, 256)) != hipSuccess || (e = hipMemset(c->d_runmin, 0xFF, 256)) != hipSuccess ||
-        (e = hipMalloc(&c->d_weps, kCMaxVals * sizeof(double))) != hipSuccess ||
+        (e = hipMalloc(&c->d_weps, (kCMaxVals + 1) * sizeof(double))) != hipSuccess ||
         (e = hipMalloc(&c->d_base, kCMaxVals * sizeof(float))) != hipSuccess ||
         (e = hipMalloc(&c->d_dyn, kDynF64Off * sizeof(float) + sizeof(dynd))) != hipSuccess ||
         (e = hipMemcpy(c->d_dyn + kDynF64Off, dynd, sizeof(dynd), hipMemcpyHostToDevice)) != hipSuccess ||
@@ -1442,11 +1448,11 @@ int mppi_chain_ctx_create(const mppi_chain_config* cfg, int device, void* stream
         (e = hipHostGetDevicePointer((void**)&c->d_tmo, c->h_tmo, 0)) != hipSuccess ||
         (e = hipEventCreateWithFlags(&c->staged, hipEventDisableTiming)) != hipSuccess ||
         (e = hipEventCreateWithFlags(&c->out_ev, hipEventDisableTiming)) != hipSuccess ||
-        (e = hipHostMalloc(&c->h_out, (kCMaxVals + kCMax) * sizeof(double), hipHostMallocDefault)) != hipSuccess ||
+        (e = hipHostMalloc(&c->h_out, (kCMaxVals + kCMax + 1) * sizeof(double), hipHostMallocDefault)) != hipSuccess ||
         (e = hipMemset(c->d_counter, 0, ctr_bytes)) != hipSuccess || (e = hipMemset(c->d_slab, 0, slab)) != hipSuccess ||
         (e = hipMemset(c->d_gslab, 0, gslab)) != hipSuccess ||
         (e = hipMemset(c->d_step, 0, 2 * sizeof(ChainStep))) != hipSuccess ||
-        (e = hipMemset(c->d_weps, 0, kCMaxVals * sizeof(double))) != hipSuccess ||
+        (e = hipMemset(c->d_weps, 0, (kCMaxVals + 1) * sizeof(double))) != hipSuccess ||
         (e = hipMemcpy(c->d_dyn, k.dyn, sizeof(k.dyn), hipMemcpyHostToDevice)) != hipSuccess ||
         (e = hipDeviceSynchronize()) != hipSuccess)
         return cleanup_fail(fail(MPPI_E_HIP, std::string("allocation: ") + hipGetErrorString(e)));
@@ -1600,7 +1606,7 @@ int chain_rollout(mppi_chain_ctx* c, const float* noise_dev, double* S_dev, doub
         const char* blk = (const char*)(c->d_step + c->cur);
         if (hipMemcpyAsync(c->h_out, blk + offsetof(ChainStep, u), (size_t)c->cfg.T * kCMax * sizeof(double),
                            hipMemcpyDeviceToHost, c->stream) != hipSuccess ||
-            hipMemcpyAsync(c->h_out + kCMaxVals, blk + offsetof(ChainStep, u_first), kCMax * sizeof(double),
+            hipMemcpyAsync(c->h_out + kCMaxVals, blk + offsetof(ChainStep, u_first), (kCMax + 1) * sizeof(double),
                            hipMemcpyDeviceToHost, c->stream) != hipSuccess ||
             hipEventRecord(c->out_ev, c->stream) != hipSuccess)
             return fail(MPPI_E_HIP, "update read-back");
@@ -1692,10 +1698,11 @@ int mppi_chain_merge_partials(mppi_chain_ctx* c, const double* partials_dev, int
 int mppi_chain_get_weighted_noise(mppi_chain_ctx* c, double* w_eps_host) {
     if (!c || !w_eps_host) return fail(MPPI_E_ARG, "null argument");
     const size_t bytes = (size_t)c->cfg.T * c->n * sizeof(double);
-    if (hipMemcpyAsync(c->h_buf, c->d_weps, bytes, hipMemcpyDeviceToHost, c->stream) != hipSuccess ||
+    if (hipMemcpyAsync(c->h_buf, c->d_weps, bytes + sizeof(double), hipMemcpyDeviceToHost, c->stream) != hipSuccess ||
         hipStreamSynchronize(c->stream) != hipSuccess)
         return fail(MPPI_E_HIP, "weighted noise read-back");
     memcpy(w_eps_host, c->h_buf, bytes);
+    c->last_eta = c->h_buf[(size_t)c->cfg.T * c->n];
     return check_tmo(c);
 }
 
@@ -1709,6 +1716,12 @@ int mppi_chain_get_nominal(mppi_chain_ctx* c, double* u_host) {
     for (int t = 0; t < T; ++t)
         for (int d = 0; d < n; ++d) u_host[t * n + d] = c->h_buf[t * kCMax + d];
     return check_tmo(c);
+}
+
+int mppi_chain_last_eta(const mppi_chain_ctx* c, double* eta) {
+    if (!c || !eta) return fail(MPPI_E_ARG, "null argument");
+    *eta = c->last_eta;
+    return MPPI_OK;
 }
 
 }  // extern "C"
@@ -1734,7 +1747,9 @@ __attribute__((always_inline)) inline void chain_traj_body(const double* kd, con
     }
 }
 // The step's fma() calls as the hardware instruction where the CPU has it (the baseline x86-64 target calls
-// libm's fma ~600 times per step set); fma is correctly rounded either way, so the results are the same bits.
+// libm's fma ~600 times per step set); fma is correctly rounded either way, and the host side of this file is
+// compiled with -ffp-contract=off (build.py), so no other multiply-add is fused in either instance: the same
+// bits (MPPI_HOST_FMA=0 forces the baseline instance; tests/test_gpu_chain.py compares the two).
 template <int N>
 __attribute__((target("fma"))) void chain_traj_host_fma(const double* kd, const double* x0, const double* u_new,
                                                         int T, double* out) {
@@ -1743,7 +1758,8 @@ __attribute__((target("fma"))) void chain_traj_host_fma(const double* kd, const 
 template <int N>
 void chain_traj_host(const double* kd, const double* x0, const double* u_new, int T, double* out) {
     static const bool hw_fma = __builtin_cpu_supports("fma");
-    if (hw_fma) chain_traj_host_fma<N>(kd, x0, u_new, T, out);
+    const char* force = getenv("MPPI_HOST_FMA");
+    if (hw_fma && !(force && force[0] == '0')) chain_traj_host_fma<N>(kd, x0, u_new, T, out);
     else chain_traj_body<N>(kd, x0, u_new, T, out);
 }
 }  // namespace
@@ -1761,12 +1777,13 @@ int mppi_chain_wait_outputs(mppi_chain_ctx* c, const double* x0, double* u_out, 
         const char* blk = (const char*)(c->d_step + c->cur);
         if (hipMemcpyAsync(c->h_out, blk + offsetof(ChainStep, u), (size_t)T * kCMax * sizeof(double),
                            hipMemcpyDeviceToHost, c->stream) != hipSuccess ||
-            hipMemcpyAsync(c->h_out + kCMaxVals, blk + offsetof(ChainStep, u_first), kCMax * sizeof(double),
+            hipMemcpyAsync(c->h_out + kCMaxVals, blk + offsetof(ChainStep, u_first), (kCMax + 1) * sizeof(double),
                            hipMemcpyDeviceToHost, c->stream) != hipSuccess ||
             hipStreamSynchronize(c->stream) != hipSuccess)
             return fail(MPPI_E_HIP, "update read-back");
     }
     if (int rc = check_tmo(c)) return rc;
+    c->last_eta = h[kCMaxVals + kCMax];
     for (int t = 0; t < T; ++t)
         for (int d = 0; d < n; ++d) u_out[t * n + d] = h[t * kCMax + d];
     memcpy(c->h_pub, h, (size_t)T * kCMax * sizeof(double));

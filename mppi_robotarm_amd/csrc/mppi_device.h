@@ -454,6 +454,7 @@ struct MergeScratch {
     double unew[MAXV];
     double rho[kDirectRows];  // direct merge: the rows' rho, polled by wave 0
     double part[2 * kDirectRows];  // direct merge: per row-group column sums (one group per ncol threads)
+    double eta;                    // the final merge's eta = sum_k e^{-(S_k - rho)/lambda} (>= 1; 1: one-hot)
     int nrel;
 };
 
@@ -490,6 +491,7 @@ __device__ __forceinline__ void put_final(double rho, const double (&acc)[MAXCH]
         if (col >= geo.ncol) continue;
         if (col == 0) {
             sm.nrel = nrel;
+            sm.eta = eta;
             if (out_row) {
                 out_row[0] = rho;
                 out_row[1] = acc[ch];

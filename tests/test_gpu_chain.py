@@ -24,6 +24,8 @@ slot it picked at every step, and the fp64 cost recomputed with those picks
 must equal the device's S to 1e-4, with every pick that differs from the fp64
 argmin a tie within PICK_GAP_M; the other link counts use the flip search.
 """
+import os
+
 import numpy as np
 import pytest
 
@@ -372,6 +374,40 @@ def test_chain_c5_spread_weights(paths):
     assert ess >= 10.0
     assert errs["f64"][0] < U_TOL and errs["f64"][1] < 1e-11
 
+    # the default controller (precision="auto") on the same step: its fp32 rollout sees eta - 1 > ETA_TOL and
+    # the step is run again in fp64, so the update holds 1e-4 against the oracle's; the next step, still
+    # spread, goes straight to fp64.  Wall time per call recorded beside fp32 alone (the switch's cost).
+    import time
+
+    from scipy.ndimage import median_filter
+    from mppi_robotarm_amd.chain import ChainMPPIController
+    wm = np.stack([median_filter(wr[:, d], size=10, mode="reflect") for d in range(7)], axis=1)
+    un = u + wm
+    u_ref = np.concatenate([un[1:], un[-1:]])          # control.py:126, 148-149
+    kw = dict(device=0, verbose=False, noise="device", seed=11, u_init=u.copy())
+    ctl = {p: ChainMPPIController(0.006, paths["xydq_circle"], T, K, 0.0, lam, 0.98, sig, precision=p, **kw)
+           for p in ("auto", "f32")}
+    res, wall = {}, {}
+    for p, c in ctl.items():
+        c._step_count = 2                                  # the stream position of the draw above (seed 11, step 2)
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        _, u_seq, _, _ = c.calc_control_input(x0.copy())
+        wall[p] = [time.perf_counter() - t0]
+        res[p] = (_urel(u_seq, u_ref), c.last_precision, c.last_eta)
+        for _ in range(3):                                 # the following steps, back to back
+            t0 = time.perf_counter()
+            c.calc_control_input(x0.copy())
+            wall[p].append(time.perf_counter() - t0)
+        c.close()
+    print(f"auto controller: u rel-err {res['auto'][0]:.2e} ({res['auto'][1]}, eta {res['auto'][2]:.3f}), "
+          f"f32 controller {res['f32'][0]:.2e}; wall ms auto {[round(w * 1e3, 2) for w in wall['auto']]} "
+          f"f32 {[round(w * 1e3, 2) for w in wall['f32']]}")
+    record("chain_c5_spread_auto", u_rel_err_auto=res["auto"][0], u_rel_err_f32=res["f32"][0], eta=res["auto"][2],
+           wall_ms_auto=[w * 1e3 for w in wall["auto"]], wall_ms_f32=[w * 1e3 for w in wall["f32"]])
+    assert res["auto"][1] == "f64" and res["auto"][2] - 1.0 > ChainMPPIController.ETA_TOL
+    assert res["auto"][0] < U_TOL
+
 
 def test_chain_lanes_per_sample_agree(paths):
     """A quad per sample and one lane per sample on the same inputs: S within fp32 rounding of each other (the
@@ -503,8 +539,16 @@ def test_chain_optimal_traj_host_against_oracle():
     for t in range(T):
         q, dq = CO.chain_forward_dynamics(q, dq, u_new[t - 1][None, :], 0.006, CO.ChainParams())
         want[t, :7], want[t, 7:] = q[0], dq[0]
+    # the hardware-fma instance and the baseline x86-64 one give the same bits (fma is exact in both,
+    # nothing else is contracted on the host)
+    os.environ["MPPI_HOST_FMA"] = "0"
+    try:
+        base = eng.optimal_traj_host(x0, u_new)
+    finally:
+        del os.environ["MPPI_HOST_FMA"]
     eng.close()
     np.testing.assert_allclose(got, want, rtol=1e-12, atol=1e-12)
+    assert np.array_equal(got.view(np.uint64), base.view(np.uint64))
 
 
 def test_chain_debug_and_output_entry_points_refuse_misuse(paths):
