@@ -258,6 +258,27 @@ def sampled_latency(K, T, device, calls=20, warm=5):
     return float(np.median(ts[warm:])) * 1e3
 
 
+def numpy_noise_latency(K, T, device, calls=20, warm=5):
+    """calc_control_input back to back (ms, median) with the drop-in's default noise="numpy": the reference's
+    own draw, np.random.multivariate_normal on the legacy global RNG (control.py:154-164), NumPy's values and
+    state (the standard normals threaded in C, hostrng; the transform on the device for run.py's Sigma)."""
+    from mppi_robotarm_amd.controller import MPPIControllerForPathTracking
+    from mppi_robotarm_amd.params import runpy_config
+    path = np.load(os.path.join(ROOT, "tests", "golden", "paths.npz"))["xydq_circle"][:, :4]
+    kw = runpy_config()
+    kw.update(number_of_samples_K=K, horizon_step_T=T, visualze_sampled_trajs=False)
+    c = MPPIControllerForPathTracking(ref_path=path, noise="numpy", verbose=False, device=device, **kw)
+    np.random.seed(0)
+    ts = []
+    for i in range(warm + calls):
+        c.prev_waypoints_idx = 0
+        t0 = time.perf_counter()
+        c.calc_control_input(X0_RUNPY)
+        ts.append(time.perf_counter() - t0)
+    c.close()
+    return float(np.median(ts[warm:])) * 1e3
+
+
 def chain_dropin_latency(K, T, device, precision="f32", calls=40, warm=10):
     """The chain drop-in's calc_control_input back to back (ms, median) from the config-5 start state, the
     start nominal re-staged before each call (the bench loop's reset: no plant between calls)."""
@@ -547,6 +568,7 @@ def main():
             out["control_step_latency_p90_ms"] = p90
             out["control_step_latency_back_to_back_ms"] = b2b
             out["control_step_latency_sampled_trajs_ms"] = sampled_latency(K, T, local_rank)
+            out["control_step_latency_numpy_noise_ms"] = numpy_noise_latency(K, T, local_rank)
             out["control_step_latency_def"] = (
                 "median wall time of MPPIControllerForPathTracking.calc_control_input (drop-in, noise='device') "
                 "in run.py's closed loop at this K, T: stage inputs, one fused launch (rollouts, soft-min, "
@@ -556,7 +578,9 @@ def main():
                 "also waits for the previous draw). Steady state: 200 ticks each, after 100 uncounted. These "
                 "two run with visualze_sampled_trajs=False; sampled_trajs: back to back with run.py's own "
                 "visualze_sampled_trajs=True, i.e. also the (K, T, 4) fp64 sampled_traj_list (134 MB at K = "
-                "65536) re-rolled on the device and read back every call. "
+                "65536) re-rolled on the device and read back every call; numpy_noise: back to back with the "
+                "drop-in's default noise='numpy', the reference's own np.random.multivariate_normal stream "
+                "(NumPy's values and RNG state) drawn on the host every call. "
                 "ms_per_step is the device-resident loop")
         if world == 1 and c5:
             out["control_step_latency_back_to_back_ms"] = chain_dropin_latency(K, T, local_rank, args.precision)

@@ -31,6 +31,10 @@ extern "C" {
 #define MPPI_E_HIP -2        /* HIP runtime error (message says which call)            */
 #define MPPI_E_SINGULAR -3   /* singular Sigma: the reference raises LinAlgError at   */
                              /* control.py:106 (np.linalg.inv)                          */
+#define MPPI_E_EXCHANGE -5   /* multi-GPU in-launch exchange: a rank's row missed the poll
+                                bound (MPPI_EXCHANGE_SPINS, default ~1 s) on some rank of the
+                                step; every rank of the step reports it and none applied the
+                                update (the nominal is the one before the step)              */
 #define MPPI_E_PATH_END -4   /* mppi_dropin_tick: the updated waypoint index reached   */
                              /* the end of the path (control.py:76-78: the reference   */
                              /* prints "[ERROR] ..." and raises IndexError)           */

@@ -19,6 +19,7 @@ MPPI_E_ARG = -1
 MPPI_E_HIP = -2
 MPPI_E_SINGULAR = -3
 MPPI_E_PATH_END = -4
+MPPI_E_EXCHANGE = -5
 MPPI_FLAG_FUSED_UPDATE = 1
 MPPI_FLAG_EXCHANGE = 2
 MPPI_FLAG_HOST_OUT = 4
@@ -98,6 +99,12 @@ class ChainConfigC(C.Structure):
 
 class MPPIError(RuntimeError):
     """A failed C-ABI call (message from mppi_last_error)."""
+
+
+class ExchangeError(MPPIError):
+    """MPPI_E_EXCHANGE: the in-launch multi-GPU exchange of a step missed its poll bound on some rank.  Every
+    rank of that step raises it and none applied the update (the controllers then run the step again over
+    the collective fallback)."""
 
 
 _lib = None
@@ -189,4 +196,6 @@ def check(rc: int, what: str) -> None:
             raise np.linalg.LinAlgError(msg)
         if rc == MPPI_E_ARG:
             raise ValueError(f"{what}: {msg}")
+        if rc == MPPI_E_EXCHANGE:
+            raise ExchangeError(f"{what}: {msg}")
         raise MPPIError(f"{what} failed ({rc}): {msg}")

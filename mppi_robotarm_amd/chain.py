@@ -24,7 +24,7 @@ from scipy.ndimage import median_filter
 
 from . import _native as N
 from . import hostrng
-from .controller import PinnedReadback, first_min_index
+from .controller import PinnedReadback, _noise_check, _pinned_zbuf, first_min_index
 from .distributed import attach_exchange, check_exchange, exchange_partials, same_on_all_ranks, shard_geometry
 
 SEARCH_IDX_LEN = 30  # control.py:203
@@ -193,6 +193,11 @@ class ChainEngine:
         stage.copy_(torch.from_numpy(eps))
         out.copy_(stage.permute(1, 2, 0))
         return out
+
+    def upload_std_noise(self, noise, z: torch.Tensor, out: torch.Tensor) -> torch.Event:
+        """As RolloutEngine.upload_std_noise, into the chain's [T][n][K_local] layout."""
+        from .engine import _upload_std
+        return _upload_std(self, noise, z, out, (1, 2, 0))
 
     def set_step_inputs(self, x0, window, u=None) -> None:
         self._sync_stream()
@@ -486,6 +491,20 @@ class ChainMPPIController:
             self.prev_waypoints_idx = nearest_idx
         return nearest_idx
 
+    def _reference_noise(self):
+        """control.py:84 as MPPIControllerForPathTracking._reference_noise: the standard normals into a
+        page-locked buffer and the transform on the device when Sigma allows it (the chain's diagonal Sigma
+        does), else _calc_epsilon's array."""
+        if "_calc_epsilon" in self.__dict__ or type(self)._calc_epsilon is not ChainMPPIController._calc_epsilon:
+            return self._calc_epsilon(self.Sigma, self.K, self.T, self.dim_u)
+        sigma = self.Sigma
+        if sigma.shape[0] != sigma.shape[1] or sigma.shape[0] != self.dim_u or self.dim_u < 1:
+            return self._calc_epsilon(sigma, self.K, self.T, self.dim_u)   # raises as the reference
+        self._zbuf, self._zbuf_ev = _pinned_zbuf(getattr(self, "_zbuf", None), getattr(self, "_zbuf_ev", None),
+                                                 self.K * self.T * self.dim_u)
+        std = hostrng.multivariate_normal_std(np.zeros(self.dim_u), sigma, (self.K, self.T), self._zbuf.numpy())
+        return std if std is not None else self._calc_epsilon(sigma, self.K, self.T, self.dim_u)
+
     def _calc_epsilon(self, sigma, size_sample, size_time_step, size_dim_u):
         """control.py:154-164 — NumPy's legacy global RNG, n-dimensional"""
         if sigma.shape[0] != sigma.shape[1] or sigma.shape[0] != size_dim_u or size_dim_u < 1:
@@ -501,7 +520,7 @@ class ChainMPPIController:
             print("[ERROR] Reached the end of the reference path.")
             raise IndexError
         if self.noise_source == "numpy":
-            epsilon = self._calc_epsilon(self.Sigma, self.K, self.T, self.dim_u)
+            epsilon = self._reference_noise()
         else:
             epsilon = None
         step = self._step_count
@@ -509,16 +528,26 @@ class ChainMPPIController:
         window = self.ref_path[self.prev_waypoints_idx:(self.prev_waypoints_idx + SEARCH_IDX_LEN)]
         auto = self.precision == "auto"
         prec = ("f64" if self._spread else "f32") if auto else self.precision
-        out = self._device_step(prec, x0, window, u, epsilon, step)
+        out = self._device_step_x(prec, x0, window, u, epsilon, step)
         if auto:
             self._spread = self.last_eta - 1.0 > self.ETA_TOL
             if self._spread and prec == "f32":
                 # the weights spread: this step again in fp64 from the same inputs (u is not updated yet)
-                out = self._device_step("f64", x0, window, u, epsilon, step)
+                out = self._device_step_x("f64", x0, window, u, epsilon, step)
                 self._spread = self.last_eta - 1.0 > self.ETA_TOL
         u_new, optimal_traj, sampled = out
         u[:] = u_new                                        # the shifted nominal, in place (aliasing kept)
         return u[0], u, optimal_traj, sampled
+
+    def _device_step_x(self, prec: str, x0, window, u, epsilon, step: int):
+        """_device_step; after an ExchangeError (raised on every rank of the step, no update applied) the same
+        step again over the all-gather, which waits for the late rank, and the all-gather from then on."""
+        try:
+            return self._device_step(prec, x0, window, u, epsilon, step)
+        except N.ExchangeError:
+            self._xmode = "rccl"
+            self._noise_ready = None   # the fused step queues the next draw into the buffer: draw this one again
+            return self._device_step(prec, x0, window, u, epsilon, step)
 
     def _device_step(self, prec: str, x0, window, u, epsilon, step: int):
         """control.py:81-149 of one step on the engine of rollout precision `prec`: the shifted updated
@@ -528,7 +557,9 @@ class ChainMPPIController:
         if key != self._engine_built_for:
             np.linalg.inv(self.Sigma)                      # LinAlgError as control.py:106 (Sigma checked when it changes)
         eng = self._get_engine(key)
-        if epsilon is not None:
+        if isinstance(epsilon, hostrng.StdNoise):
+            self._zbuf_ev = eng.upload_std_noise(epsilon, self._zbuf, self._noise_dev)
+        elif epsilon is not None:
             eng.upload_noise(epsilon[eng.k_offset:eng.k_offset + eng.K_local], out=self._noise_dev)
         elif self._noise_ready != (self.seed, step):
             eng.philox_noise(self.seed, step, out=self._noise_dev)
@@ -536,7 +567,7 @@ class ChainMPPIController:
         world, _ = self._shard()
         S_out = self._S_dev if self.keep_costs else None
         if world > 1 and self._xmode is None:
-            self._multi_setup(eng, float(epsilon[0, 0, 0] + epsilon[-1, -1, -1]) if epsilon is not None else None)
+            self._multi_setup(eng, _noise_check(epsilon, self.K, self.T, self.dim_u))
         self.last_precision = prec
         if self.T >= 5 and not self.visualze_sampled_trajs and (world == 1 or self._xmode == "launch"):
             # the update of control.py:120-149 inside the launch (the median of 10 is a selection and the

@@ -52,7 +52,7 @@ from scipy.ndimage import median_filter
 
 import dataclasses
 
-from . import hostrng
+from . import _native, hostrng
 from .distributed import attach_exchange, check_exchange, exchange_partials, same_on_all_ranks, shard_geometry
 from .engine import RolloutEngine
 from .params import ArmParams
@@ -68,6 +68,30 @@ def first_min_index(d: np.ndarray) -> int:
     if d[j] != d[j]:                                   # a NaN somewhere: Python's rule
         j = 0 if d[0] != d[0] else int(np.nanargmin(d))
     return j
+
+
+def _pinned_zbuf(buf, ev, n: int):
+    """(buffer, None): a float64 host tensor of at least n values, page-locked where the host allows it,
+    reused across calls once the event of the last DMA out of it has completed."""
+    if ev is not None:
+        ev.synchronize()
+    if buf is None or buf.numel() < n:
+        buf = None   # the old one is released first
+        try:
+            buf = torch.empty(n, dtype=torch.float64, pin_memory=True)
+        except RuntimeError:
+            buf = torch.empty(n, dtype=torch.float64)
+    return buf, None
+
+
+def _noise_check(epsilon, K: int, T: int, du: int):
+    """The value the ranks compare to agree on the noise stream: eps[0, 0, 0] + eps[-1, -1, -1] of the draw
+    (an array, a hostrng.StdNoise, or None for device noise)."""
+    if epsilon is None:
+        return None
+    if isinstance(epsilon, hostrng.StdNoise):
+        return epsilon.eps(0, 0, 0) + epsilon.eps(K - 1, T - 1, du - 1)
+    return float(epsilon[0, 0, 0] + epsilon[-1, -1, -1])
 
 
 class PinnedReadback:
@@ -287,6 +311,35 @@ class MPPIControllerForPathTracking:
     # ------------------------------------------------------------ API
     def calc_control_input(self, observed_x: np.ndarray) -> Tuple[float, np.ndarray]:
         """calculate optimal control input (control.py:67-152)"""
+        if self.process_group is not None and self._xmode == "launch":
+            # the in-launch exchange can fail on a late rank (ExchangeError on every rank of the step, no update
+            # applied anywhere): every rank then restores what the call changed and runs it again over the
+            # all-gather, which waits for the late rank, and stays on it
+            saved = (self.prev_waypoints_idx, self._step_count,
+                     np.random.get_state() if self.noise_source == "numpy" else None)
+            try:
+                return self._calc_control_input(observed_x)
+            except _native.ExchangeError:
+                self.prev_waypoints_idx, self._step_count, rng = saved
+                if rng is not None:
+                    np.random.set_state(rng)
+                self._exchange_failed()
+                verbose, self.verbose = self.verbose, False     # the call's three lines are printed already
+                try:
+                    return self._calc_control_input(observed_x)
+                finally:
+                    self.verbose = verbose
+        return self._calc_control_input(observed_x)
+
+    def _exchange_failed(self) -> None:
+        """After an ExchangeError (every rank): the collective exchange from now on, no native tick, and the
+        device noise drawn again for the step (the tick queues the next step's draw into the same buffer)."""
+        self._xmode = "rccl"
+        self._fast = None
+        self._bound = None
+        self._noise_ready = None
+
+    def _calc_control_input(self, observed_x: np.ndarray) -> Tuple[float, np.ndarray]:
         f = self._fast
         if (f is not None and f[0] is self.ref_path and f[1] is self.u_prev and f[2] is self.Sigma
                 and f[3] is self.stage_cost_weight and f[4] is self.terminal_cost_weight and f[5] is self._engine
@@ -308,7 +361,7 @@ class MPPIControllerForPathTracking:
             raise ValueError("zero-size array to reduction operation minimum which has no identity")
 
         if self.noise_source == "numpy":
-            epsilon = self._calc_epsilon(self.Sigma, self.K, self.T, self.dim_u)
+            epsilon = self._reference_noise()
         else:
             epsilon = None
             self._check_sigma(self.Sigma, self.dim_u)
@@ -316,7 +369,9 @@ class MPPIControllerForPathTracking:
         if key != self._engine_built_for:
             np.linalg.inv(self.Sigma)                      # LinAlgError exactly as control.py:106
         eng = self._get_engine(key)
-        if epsilon is not None:
+        if isinstance(epsilon, hostrng.StdNoise):
+            self._zbuf_ev = eng.upload_std_noise(epsilon, self._zbuf, self._noise_dev)
+        elif epsilon is not None:
             lo = eng.k_offset
             eng.upload_noise(epsilon[lo:lo + eng.K_local], out=self._noise_dev)
         elif self._noise_ready != (self.seed, self._step_count):
@@ -329,7 +384,7 @@ class MPPIControllerForPathTracking:
             return self._dropin_step(eng, x0, window, u)
         eng.set_step_inputs(np.asarray(x0, dtype=np.float64), window, u)
         if world > 1 and self._xmode is None:
-            check = float(epsilon[0, 0, 0] + epsilon[-1, -1, -1]) if epsilon is not None else None
+            check = _noise_check(epsilon, self.K, self.T, self.dim_u)
             self._multi_setup(eng, check)
         if not self.host_update:
             return self._fused_step(eng, x0, u, world)
@@ -519,6 +574,27 @@ class MPPIControllerForPathTracking:
         if sigma.shape[0] != sigma.shape[1] or sigma.shape[0] != size_dim_u or size_dim_u < 1:
             print("[ERROR] sigma must be a square matrix with the size of size_dim_u.")
             raise ValueError
+
+    def _reference_noise(self):
+        """control.py:84, the reference's draw on the legacy global RNG.  When _calc_epsilon is the reference's
+        (not replaced on the instance or a subclass) and Sigma's transform is a scaled column permutation
+        (run.py's 20 I), the draw stops at its standard normals: NumPy's values, written into a page-locked
+        buffer that goes to the device in one DMA, where the same fp64 multiply and add make the noise
+        (hostrng.multivariate_normal_std, engine.upload_std_noise) instead of NumPy's np.dot and `x += mean`
+        over the 67 MB draw and a pageable copy.  Otherwise _calc_epsilon's array."""
+        cls = MPPIControllerForPathTracking
+        if "_calc_epsilon" in self.__dict__ or type(self)._calc_epsilon is not cls._calc_epsilon:
+            return self._calc_epsilon(self.Sigma, self.K, self.T, self.dim_u)
+        self._check_sigma(self.Sigma, self.dim_u)
+        std = hostrng.multivariate_normal_std(np.full((self.dim_u), 0.0), self.Sigma, (self.K, self.T),
+                                              self._zbuf_numpy(self.K * self.T * self.dim_u))
+        return std if std is not None else self._calc_epsilon(self.Sigma, self.K, self.T, self.dim_u)
+
+    def _zbuf_numpy(self, n: int) -> np.ndarray:
+        """The page-locked buffer of the standard normals (>= n values), free to be rewritten: the DMA of the
+        previous draw out of it has completed."""
+        self._zbuf, self._zbuf_ev = _pinned_zbuf(getattr(self, "_zbuf", None), getattr(self, "_zbuf_ev", None), n)
+        return self._zbuf.numpy()
 
     def _calc_epsilon(self, sigma: np.ndarray, size_sample: int, size_time_step: int, size_dim_u: int) -> np.ndarray:
         """sample epsilon (control.py:154-164) — the reference's RNG stream"""

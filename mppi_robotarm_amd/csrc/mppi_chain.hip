@@ -562,17 +562,21 @@ template <int Q>
 __device__ __forceinline__ float qbc(float v) {
     return dpp_f32<Q * 0x55>(v);   // quad_perm [Q, Q, Q, Q]
 }
-// sum over the lanes p' < p of the quad (m1 = p >= 1, m2 = p >= 2 as 1.f / 0.f)
-__device__ __forceinline__ float q_excl_prefix(float x, float m1, float m2) {
-    const float e = dpp_f32<0x90>(x) * m1;          // quad_perm [0, 0, 1, 2]: x_{p-1}
-    const float f = fmaf(dpp_f32<0x90>(e), m1, e);  // x_{p-1} + x_{p-2}
-    return fmaf(dpp_f32<0x40>(f), m2, f);          // quad_perm [0, 0, 0, 1]: + f_{p-2}
+// sum over the lanes p' < p of the quad (m1 = p >= 1 as 1.f / 0.f): the shift with a zero at lane 0 (its
+// own x times 0), then two Hillis-Steele steps whose out-of-range reads land on that 0 — no mask after the
+// first step, so every DPP move folds into its v_mul / v_add (v_mul_f32_dpp, v_add_f32_dpp)
+__device__ __forceinline__ float q_excl_prefix(float x, float m1) {
+#pragma clang fp contract(off)   // a contracted e + dpp(e) would re-read x through an unfolded move
+    const float e = dpp_f32<0x90>(x) * m1;   // quad_perm [0, 0, 1, 2]: (0, x0, x1, x2)
+    const float f = e + dpp_f32<0x90>(e);    // + e_{p-1}: (0, x0, x0 + x1, x1 + x2)
+    return f + dpp_f32<0x40>(f);            // quad_perm [0, 0, 0, 1]: + f_{p-2}
 }
-// sum over the lanes p' > p of the quad (u1 = p <= 2, u2 = p <= 1)
-__device__ __forceinline__ float q_excl_suffix(float x, float u1, float u2) {
-    const float e = dpp_f32<0xF9>(x) * u1;          // quad_perm [1, 2, 3, 3]: x_{p+1}
-    const float f = fmaf(dpp_f32<0xF9>(e), u1, e);  // x_{p+1} + x_{p+2}
-    return fmaf(dpp_f32<0xFE>(f), u2, f);          // quad_perm [2, 3, 3, 3]: + f_{p+2}
+// sum over the lanes p' > p of the quad (u1 = p <= 2), the mirror image: the zero sits at lane 3
+__device__ __forceinline__ float q_excl_suffix(float x, float u1) {
+#pragma clang fp contract(off)
+    const float e = dpp_f32<0xF9>(x) * u1;   // quad_perm [1, 2, 3, 3]: (x1, x2, x3, 0)
+    const float f = e + dpp_f32<0xF9>(e);    // + e_{p+1}
+    return f + dpp_f32<0xFE>(f);            // quad_perm [2, 3, 3, 3]: + f_{p+2}
 }
 __device__ __forceinline__ float q_sum(float x) {
     x += dpp_f32<0xB1>(x);   // quad_perm xor 1
@@ -605,8 +609,7 @@ __device__ __forceinline__ double chain_horizon_lps4(const ChainConst& c, const 
     Search<4, true> sr;
     sr.load(st->key, st->ctr, sub);
     const int a0 = 2 * sub, a1 = 2 * sub + 1;   // this lane's links
-    const float m1 = sub >= 1 ? 1.f : 0.f, m2 = sub >= 2 ? 1.f : 0.f;
-    const float u1 = sub <= 2 ? 1.f : 0.f, u2 = sub <= 1 ? 1.f : 0.f;
+    const float m1 = sub >= 1 ? 1.f : 0.f, u1 = sub <= 2 ? 1.f : 0.f;
     const float own = sub == 0 ? 1.f : 0.f;
     const f32x2 pad = {a0 < N ? 1.f : 0.f, a1 < N ? 1.f : 0.f};
     const f32x2 l2 = {dyn[kOffL + a0], dyn[kOffL + a1]}, nu2 = {dyn[kOffNu + a0], dyn[kOffNu + a1]};
@@ -635,7 +638,7 @@ __device__ __forceinline__ double chain_horizon_lps4(const ChainConst& c, const 
     f32x2 C, Sn;
     auto angles = [&]() {
         const float t = Q.x + Q.y;
-        const float e = q_excl_prefix(t, m1, m2);
+        const float e = q_excl_prefix(t, m1);
         float s0, c0, s1, c1;
         sincos_f32(e + Q.x, &s0, &c0);
         sincos_f32(e + t, &s1, &c1);
@@ -670,14 +673,14 @@ __device__ __forceinline__ double chain_horizon_lps4(const ChainConst& c, const 
         f32x2 w;
         {
             const float t2 = DQ.x + DQ.y;
-            const float e = q_excl_prefix(t2, m1, m2);
+            const float e = q_excl_prefix(t2, m1);
             w = f32x2{e + DQ.x, e + t2};
             w = w * w;   // thdot^2
         }
         const f32x2 lc = l2 * C, ls = l2 * Sn, vc = nu2 * C, vs = nu2 * Sn;
         const f32x2 wvc = w * vc, wvs = w * vs, wlc = w * lc, wls = w * ls;
-        const float sC = q_excl_suffix(wvc.x + wvc.y, u1, u2), sS = q_excl_suffix(wvs.x + wvs.y, u1, u2);
-        const float pC = q_excl_prefix(wlc.x + wlc.y, m1, m2), pS = q_excl_prefix(wls.x + wls.y, m1, m2);
+        const float sC = q_excl_suffix(wvc.x + wvc.y, u1), sS = q_excl_suffix(wvs.x + wvs.y, u1);
+        const float pC = q_excl_prefix(wlc.x + wlc.y, m1), pS = q_excl_prefix(wls.x + wls.y, m1);
         const f32x2 Cs = {wvc.y + sC, sC}, Ss = {wvs.y + sS, sS};
         const f32x2 Cp = {pC, wlc.x + pC}, Sp = {pS, wls.x + pS};
         const f32x2 X = __builtin_elementwise_fma(l2, Cs, nu2 * Cp);
@@ -759,6 +762,193 @@ __device__ __forceinline__ double chain_horizon_lps4(const ChainConst& c, const 
     return q_sum_f64(S);
 }
 
+// The same quad, stepped in absolute angles (theta_a = q_1 + ... + q_a, kept in
+// revolutions, the unit of v_sin_f32 / v_cos_f32) and their rates: the solve
+// gives theta_ddot directly, so the per-step prefix sums of q and q_dot (two
+// 4-lane scans on the serial path before the sincos), the difference of the
+// solution and its pad mask drop out; the joint rates the damping needs are one
+// difference (theta_dot of link a0 - 1 from the lane below).  Software-pipelined
+// at one wave per SIMD, where every latency is exposed: the per-step constants
+// come from a 2-deep register ring like the noise rows, and the window row of
+// step t is read from LDS right after its search but consumed only after step
+// t + 1's dynamics (deferred cost; the stage cost goes into S in step order).
+// The stage cost is lane 0's alone (own), so it needs no broadcast.
+template <int N>
+__device__ __forceinline__ double chain_horizon_q4(const ChainConst& c, const ChainStep* st, const float* dyn,
+                                                   const float* noise, int k, float exf, float4* s_ua4,
+                                                   float4* s_win, int* slots) {
+    static_assert(N <= 8, "four link pairs");
+    const int tid = threadIdx.x, sub = tid & 3, K = c.K_local, T = c.T;
+    if (tid < kSlots) s_win[tid] = st->win[tid];
+    for (int i = tid; i < (T + kCPF) * 4; i += kCT) {
+        const int t = min(i >> 2, T - 1), p = i & 3;
+        const float* r = st->ua[t];
+        s_ua4[i] = make_float4(r[2 * p], r[2 * p + 1], r[kCMax + 2 * p], r[kCMax + 2 * p + 1]);
+    }
+    Search<4, true> sr;
+    sr.load(st->key, st->ctr, sub);
+    const int a0 = 2 * sub, a1 = 2 * sub + 1;   // this lane's links
+    const float m1 = sub >= 1 ? 1.f : 0.f, u1 = sub <= 2 ? 1.f : 0.f;
+    const float own = sub == 0 ? 1.f : 0.f;
+    const f32x2 pad = {a0 < N ? 1.f : 0.f, a1 < N ? 1.f : 0.f};
+    const f32x2 l2 = {dyn[kOffL + a0], dyn[kOffL + a1]}, nu2 = {dyn[kOffNu + a0], dyn[kOffNu + a1]};
+    const f32x2 damp2 = {dyn[kOffDamp + a0], dyn[kOffDamp + a1]}, fk2 = {dyn[kOffFk + a0], dyn[kOffFk + a1]};
+    const float dt = dyn[kOffDt], g = dyn[kOffG];
+    constexpr float kRev = 0.15915494309189535f;   // 1 / (2 pi)
+    const float dtr = dt * kRev;
+    float sw[4], tw[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        sw[i] = dyn[kOffSw + i];
+        tw[i] = dyn[kOffTw + i];
+    }
+    f32x2 corr[N];   // as chain_horizon_lps4
+    {
+        const float dc0 = dyn[kOffDd + a0] - l2.x * nu2.x, dc1 = dyn[kOffDd + a1] - l2.y * nu2.y;
+        const float j0 = a0 >= 1 ? dyn[kOffJ + 2 * (a0 - 1) + (a0 & 1)] : 0.f;
+        const float j1 = dyn[kOffJ + 2 * (a1 - 1) + (a1 & 1)];
+#pragma unroll
+        for (int a = 0; a < N; ++a)
+            corr[a] = f32x2{a0 == a ? dc0 : (a0 == a + 1 ? j0 : 0.f), a1 == a ? dc1 : (a1 == a + 1 ? j1 : 0.f)};
+    }
+    // absolute angles (revolutions) and rates of this lane's pair from x0 = (q, q_dot)
+    f32x2 TH, THD, C, Sn;
+    {
+        const f32x2 Q = {a0 < N ? st->x0[a0] : 0.f, a1 < N ? st->x0[a1] : 0.f};
+        const f32x2 DQ = {a0 < N ? st->x0[N + a0] : 0.f, a1 < N ? st->x0[N + a1] : 0.f};
+        const float tq = Q.x + Q.y, e = q_excl_prefix(tq, m1);
+        const float td = DQ.x + DQ.y, ed = q_excl_prefix(td, m1);
+        TH = f32x2{e + Q.x, e + tq} * splat(kRev);
+        THD = f32x2{ed + DQ.x, ed + td};
+    }
+    auto angles = [&]() {
+        C = f32x2{__builtin_amdgcn_cosf(TH.x), __builtin_amdgcn_cosf(TH.y)};
+        Sn = f32x2{__builtin_amdgcn_sinf(TH.x), __builtin_amdgcn_sinf(TH.y)};
+    };
+    angles();
+    const unsigned o0 = (unsigned)(min(a0, N - 1) * K + k) * 4u, o1 = (unsigned)(min(a1, N - 1) * K + k) * 4u;
+    auto nrow = [&](int t) {
+        const char* row = (const char*)(noise + (size_t)min(t, T - 1) * N * K);
+        return f32x2{*(const float*)(row + o0), *(const float*)(row + o1)};
+    };
+    f32x2 ring[kCPF];
+#pragma unroll
+    for (int j = 0; j < kCPF; ++j) ring[j] = nrow(j);
+    __syncthreads();
+    float4 uar[kCPF];
+#pragma unroll
+    for (int j = 0; j < kCPF; ++j) uar[j] = s_ua4[j * 4 + sub];
+
+    double S = 0.0;
+    float S4 = 0.f;
+    f32x2 G2 = {0.f, 0.f};   // this lane's (gamma u^T Sigma^-1) v terms
+    // the pending stage cost (the previous step's): position, lane 0's joint rates 1 and 2, its window row;
+    // all zero before the first step, so the first "pending" cost is exactly 0
+    float ppx = 0.f, ppy = 0.f, pd1 = 0.f, pd2 = 0.f;
+    float4 prw = make_float4(0.f, 0.f, 0.f, 0.f);
+    auto step = [&](int t, auto slot_c) {
+        constexpr int slot = decltype(slot_c)::value;
+        // the slot's values are taken here (volatile asm keeps its place against the previous step's
+        // PIN_LOADS): left free, the scheduler hoists their uses into the previous step, where waiting for
+        // them means waiting for every load in flight (as rollout_kernel's dstep)
+        f32x2 nz = ring[slot];
+        f32x4 ua = {uar[slot].x, uar[slot].y, uar[slot].z, uar[slot].w};
+        asm volatile("" : "+v"(nz), "+v"(ua));
+        const f32x2 v = __builtin_elementwise_fma(splat(exf), f32x2{ua.x, ua.y}, nz) * pad;  // control.py:99-101
+        G2 = __builtin_elementwise_fma(f32x2{ua.z, ua.w}, v, G2);                          // control.py:106
+        ring[slot] = nrow(t + kCPF);
+        uar[slot] = s_ua4[(t + kCPF) * 4 + sub];
+        PIN_LOADS();
+        // ---- dynamics in absolute angles: bias, D' rows (a0, a1), Cholesky with the forward solve
+        const f32x2 w = THD * THD;   // thdot^2
+        const f32x2 lc = l2 * C, ls = l2 * Sn, vc = nu2 * C, vs = nu2 * Sn;
+        const f32x2 wvc = w * vc, wvs = w * vs, wlc = w * lc, wls = w * ls;
+        const float sC = q_excl_suffix(wvc.x + wvc.y, u1), sS = q_excl_suffix(wvs.x + wvs.y, u1);
+        const float pC = q_excl_prefix(wlc.x + wlc.y, m1), pS = q_excl_prefix(wls.x + wls.y, m1);
+        const f32x2 Cs = {wvc.y + sC, sC}, Ss = {wvs.y + sS, sS};
+        const f32x2 Cp = {pC, wlc.x + pC}, Sp = {pS, wls.x + pS};
+        const f32x2 X = __builtin_elementwise_fma(l2, Cs, nu2 * Cp);
+        const f32x2 Y = __builtin_elementwise_fma(l2, Ss, nu2 * Sp);
+        const float thd_prev = dpp_f32<0x90>(THD.y) * m1;                // theta_dot of link a0 - 1 (0 at the base)
+        const f32x2 qd = THD - f32x2{thd_prev, THD.x};                   // joint rates q_dot of (a0, a1)
+        const f32x2 ve = __builtin_elementwise_fma(-damp2, qd, v);
+        const float ve_next = dpp_f32<0xF9>(ve.x) * u1;                 // link a1 + 1 (0 past the quad)
+        f32x2 r = {ve.x - ve.y, ve.y - ve_next};                         // tau
+        r = __builtin_elementwise_fma(C, Y, __builtin_elementwise_fma(-Sn, X, __builtin_elementwise_fma(splat(-g), vc, r)));
+        f32x2 col[N];
+        unroll_seq([&](auto a_c) {
+            constexpr int a = decltype(a_c)::value;
+            const float la = qbc<a / 2>(elem<a>(lc)), sa = qbc<a / 2>(elem<a>(ls));
+            col[a] = __builtin_elementwise_fma(splat(la), vc, __builtin_elementwise_fma(splat(sa), vs, corr[a]));
+        }, std::make_integer_sequence<int, N>{});
+        float inv[N], L[N][N], y[N];
+        unroll_seq([&](auto j_c) {
+            constexpr int j = decltype(j_c)::value;
+            inv[j] = __builtin_amdgcn_rsqf(qbc<j / 2>(elem<j>(col[j])));
+            col[j] = col[j] * splat(inv[j]);
+            y[j] = qbc<j / 2>(elem<j>(r) * inv[j]);
+            r = __builtin_elementwise_fma(splat(-y[j]), col[j], r);
+            unroll_seq([&](auto k_c) {
+                constexpr int kk = decltype(k_c)::value;
+                if constexpr (kk > j) {
+                    L[kk][j] = qbc<kk / 2>(elem<kk>(col[j]));
+                    col[kk] = __builtin_elementwise_fma(splat(-L[kk][j]), col[j], col[kk]);
+                }
+            }, std::make_integer_sequence<int, N>{});
+        }, std::make_integer_sequence<int, N>{});
+        float x[N];   // L^T x = y: theta_ddot, redundantly in every lane
+#pragma unroll
+        for (int i = N - 1; i >= 0; --i) {
+            float e = y[i];
+#pragma unroll
+            for (int kk = N - 1; kk > i; --kk) e = fmaf(-L[kk][i], x[kk], e);
+            x[i] = e * inv[i];
+        }
+        auto xs = [&](int i) { return i < N ? x[i] : 0.f; };
+        const bool b0 = sub & 1, b1 = sub & 2;
+        const float xa = b1 ? (b0 ? xs(6) : xs(4)) : (b0 ? xs(2) : xs(0));
+        const float xb = b1 ? (b0 ? xs(7) : xs(5)) : (b0 ? xs(3) : xs(1));
+        THD = __builtin_elementwise_fma(f32x2{xa, xb}, splat(dt), THD);  // semi-implicit Euler (chain_oracle.py)
+        TH = __builtin_elementwise_fma(THD, splat(dtr), TH);
+        angles();
+        // ---- the previous step's stage cost: its window row has long arrived (control.py:174-185); the
+        // row is taken only now (the asm needs TH, this step's last dynamics result): left free, the
+        // scheduler pulls the cost up next to the lookup and waits on the LDS round trip there
+        {
+            f32x4 rw = {prw.x, prw.y, prw.z, prw.w};
+            asm volatile("" : "+v"(rw) : "v"(TH));
+            S4 = fmaf(own, weighted_sq(ppx - rw.x, ppy - rw.y, pd1 - rw.z, pd2 - rw.w, sw), S4);
+        }
+        // ---- end effector and nearest waypoint of this step; its row is read now, used next step
+        const f32x2 fx = fk2 * C, fy = fk2 * Sn;
+        ppx = q_sum(fx.x + fx.y);
+        ppy = q_sum(fy.x + fy.y);
+        pd1 = THD.x;            // lane 0: q_dot_1 = theta_dot_1
+        pd2 = THD.y - THD.x;    //         q_dot_2 = theta_dot_2 - theta_dot_1
+        const unsigned j = sr.nearest(ppx, ppy);
+        if (slots && sub == 0) slots[(size_t)k * T + t] = (int)j;   // debug instances only
+        prw = s_win[j];
+        if constexpr (slot == kCPF - 1) {
+            S += (double)(S4 + (G2.x + G2.y));
+            S4 = 0.f;
+            G2 = f32x2{0.f, 0.f};
+        }
+    };
+    static_assert(kCPF == 2, "unrolled for a 2-deep ring");
+    int t = 0;
+    for (; t + 2 <= T; t += 2) {
+        step(t, std::integral_constant<int, 0>{});
+        step(t + 1, std::integral_constant<int, 1>{});
+    }
+    if (t < T) step(t, std::integral_constant<int, 0>{});
+    // the last step's stage cost and the terminal cost on the same state (control.py:106-109)
+    const float ex = ppx - prw.x, ey = ppy - prw.y, e1 = pd1 - prw.z, e2 = pd2 - prw.w;
+    S4 = fmaf(own, weighted_sq(ex, ey, e1, e2, sw), S4);
+    S += (double)(S4 + (G2.x + G2.y));
+    S += (double)(own * weighted_sq(ex, ey, e1, e2, tw));
+    return q_sum_f64(S);
+}
+
 // POLL / counter hand-off and the merges as in rollout_kernel (mppi_rocm.hip).
 // SLOTS (debug instances, mppi_chain_debug_slots): dbg receives the window slot
 // each sample picked at each step, int32 [k][t].
@@ -810,7 +1000,11 @@ __global__ __launch_bounds__(kCT) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
     if constexpr (F64) {
         S = chain_horizon_f64<N>(c, st, (cdouble*)(dyn + kDynF64Off), noise, k, exf, s_wind, slots);
     } else if constexpr (LPS == 4) {
+#ifdef MPPI_CHAIN_Q_OLD
         S = chain_horizon_lps4<N>(c, st, dyn, noise, k, exf, s_ua4, s_win, slots);
+#else
+        S = chain_horizon_q4<N>(c, st, dyn, noise, k, exf, s_ua4, s_win, slots);
+#endif
     } else {
     if (tid < kSlots) s_win[tid] = st->win[tid];
     // window keys in LDS (broadcast reads): the 90 key registers would cost the
@@ -1045,9 +1239,10 @@ __global__ __launch_bounds__(kCT) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
     }
     STAMP(11, NOW());
     STAMP(6, (unsigned long long)sm.nrel);
-    if (flags & MPPI_FLAG_EXCHANGE) exchange_merge<kCT, kCMaxCh>(xd, geo, c.inv_lambda, sm, w_eps_out, tmo);
+    const bool xok = (flags & MPPI_FLAG_EXCHANGE)
+                         ? exchange_merge<kCT, kCMaxCh>(xd, geo, c.inv_lambda, sm, w_eps_out, tmo) : true;
     if (tid == 0 && w_eps_out) w_eps_out[nval] = sm.eta;   // the weights' spread (mppi_chain_last_eta)
-    if (flags & MPPI_FLAG_FUSED_UPDATE) chain_update_block<N>(nxt, c, sm, u_cur);
+    if ((flags & MPPI_FLAG_FUSED_UPDATE) && xok) chain_update_block<N>(nxt, c, sm, u_cur);   // failed: no update
     STAMP(7, NOW());
 }
 
@@ -1210,6 +1405,7 @@ struct mppi_chain_ctx {
     double* h_out = nullptr;       // MPPI_FLAG_HOST_OUT: the update's read-back, queued right behind the launch
     hipEvent_t out_ev = nullptr;   // ... recorded after that copy
     bool out_posted = false;
+    bool x_flipped = false;        // the last launch flipped the ping-pong and exchanged (undone on MPPI_E_EXCHANGE)
     double last_eta = NAN;         // the weights' spread of the last update / weighted noise read back
     double h_pub[kCMaxVals] = {};
     bool f64 = false;              // cfg.precision == 1
@@ -1228,6 +1424,7 @@ struct mppi_chain_ctx {
 
 namespace {
 
+using mppi_host::exchange_spins;
 using mppi_host::fail;
 
 template <int N, bool P, bool F64, int LPS>
@@ -1266,13 +1463,21 @@ int chain_auto_lps(int K_local, bool f64) {
 }
 
 int check_tmo(mppi_chain_ctx* c) {
-    if (c->h_tmo && __atomic_load_n(c->h_tmo, __ATOMIC_ACQUIRE)) {
-        *c->h_tmo = 0;
-        // an aborted merge left the running minimum set: clear it for the next launch
-        (void)hipMemsetAsync(c->d_runmin, 0xFF, sizeof(unsigned long long), c->stream);
-        return fail(MPPI_E_HIP, "in-launch hand-off timed out (workgroups not co-resident?); results invalid");
+    const unsigned v = c->h_tmo ? __atomic_load_n(c->h_tmo, __ATOMIC_ACQUIRE) : 0u;
+    if (!v) return MPPI_OK;
+    *c->h_tmo = 0;
+    if (v == kTmoExchange) {   // as the 2-link engine's check_timeout: the nominal before the launch
+        if (c->x_flipped) c->cur ^= 1;
+        c->x_flipped = false;
+        c->upd_valid = false;
+        c->pub_valid = false;
+        c->out_posted = false;
+        return fail(MPPI_E_EXCHANGE, "multi-GPU exchange: a rank's row did not arrive within the bound on every "
+                                     "rank of this step; no rank applied the update (run the step again)");
     }
-    return MPPI_OK;
+    // an aborted merge left the running minimum set: clear it for the next launch
+    (void)hipMemsetAsync(c->d_runmin, 0xFF, sizeof(unsigned long long), c->stream);
+    return fail(MPPI_E_HIP, "in-launch hand-off timed out (workgroups not co-resident?); results invalid");
 }
 
 }  // namespace
@@ -1597,6 +1802,7 @@ int chain_rollout(mppi_chain_ctx* c, const float* noise_dev, double* S_dev, doub
     const hipError_t e = hipGetLastError();
     if (e != hipSuccess) return fail(MPPI_E_HIP, std::string("chain_rollout_kernel: ") + hipGetErrorString(e));
     if (flags & MPPI_FLAG_FUSED_UPDATE) c->cur ^= 1;
+    c->x_flipped = (flags & MPPI_FLAG_FUSED_UPDATE) && (flags & MPPI_FLAG_EXCHANGE);   // undone on MPPI_E_EXCHANGE
     c->upd_valid = (flags & MPPI_FLAG_FUSED_UPDATE) != 0;
     if (flags & MPPI_FLAG_FUSED_UPDATE) c->pub_valid = false;
     c->out_posted = false;
@@ -1634,7 +1840,7 @@ int mppi_chain_exchange_handle(mppi_chain_ctx* c, int world, void* handle_out) {
     if (c->d_inbox && c->xworld_alloc != world) return fail(MPPI_E_ARG, "inbox already sized for another world");
     const int stride = 2 + c->cfg.T * c->n;
     if (!c->d_inbox) {
-        const size_t bytes = (size_t)2 * world * stride * 16;
+        const size_t bytes = (size_t)2 * world * (stride + 1) * 16;   // rows and statuses, two parities
         hipError_t e;
         if ((e = hipSetDevice(c->device)) != hipSuccess ||
             (e = hipExtMallocWithFlags(&c->d_inbox, bytes, hipDeviceMallocUncached)) != hipSuccess ||
@@ -1673,6 +1879,7 @@ int mppi_chain_exchange_attach(mppi_chain_ctx* c, int rank, int world, const voi
     c->xd.epoch = c->d_xepoch;
     c->xd.rank = rank;
     c->xd.world = world;
+    c->xd.spin_max = exchange_spins();
     return MPPI_OK;
 }
 
@@ -1690,6 +1897,7 @@ int mppi_chain_merge_partials(mppi_chain_ctx* c, const double* partials_dev, int
     const hipError_t e = hipGetLastError();
     if (e != hipSuccess) return fail(MPPI_E_HIP, std::string("chain_merge_kernel: ") + hipGetErrorString(e));
     if (flags & MPPI_FLAG_FUSED_UPDATE) c->cur ^= 1;
+    c->x_flipped = (flags & MPPI_FLAG_FUSED_UPDATE) && (flags & MPPI_FLAG_EXCHANGE);   // undone on MPPI_E_EXCHANGE
     c->upd_valid = (flags & MPPI_FLAG_FUSED_UPDATE) != 0;
     if (flags & MPPI_FLAG_FUSED_UPDATE) c->pub_valid = false;
     return MPPI_OK;

@@ -64,9 +64,18 @@ __device__ __forceinline__ void sincos_f32(float x, float* s, float* c) {
 #endif
 }
 
+// Every control used here (quad_perm, row_mirror, row_half_mirror, row_ror) reads
+// a valid lane, so bound_ctrl changes no value; set, it lets the compiler fold the
+// move into a VOP1 / VOP2 consumer (v_mul_f32_dpp, v_add_f32_dpp, v_rsq_f32_dpp:
+// GCNDPPCombine takes a move with an undefined old value only under bound_ctrl).
+#ifdef MPPI_DPP_NOBC
+constexpr bool kDppBC = false;
+#else
+constexpr bool kDppBC = true;
+#endif
 template <int CTRL>
 __device__ __forceinline__ float dpp_f32(float v) {
-    return __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), CTRL, 0xF, 0xF, false));
+    return __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), CTRL, 0xF, 0xF, kDppBC));
 }
 
 __device__ __forceinline__ int lanes_below(unsigned long long mask) {
@@ -76,8 +85,8 @@ __device__ __forceinline__ int lanes_below(unsigned long long mask) {
 template <int CTRL>
 __device__ __forceinline__ double dpp_f64(double v) {
     const long long b = __double_as_longlong(v);
-    const int lo = __builtin_amdgcn_mov_dpp((int)b, CTRL, 0xF, 0xF, false);
-    const int hi = __builtin_amdgcn_mov_dpp((int)(b >> 32), CTRL, 0xF, 0xF, false);
+    const int lo = __builtin_amdgcn_mov_dpp((int)b, CTRL, 0xF, 0xF, kDppBC);
+    const int hi = __builtin_amdgcn_mov_dpp((int)(b >> 32), CTRL, 0xF, 0xF, kDppBC);
     return __longlong_as_double(((long long)hi << 32) | (unsigned)lo);
 }
 
@@ -428,11 +437,14 @@ constexpr unsigned kSpinMax = 1u << 20;
 __device__ __forceinline__ void report_timeout(unsigned* tmo) {
     if (tmo) __hip_atomic_store(tmo, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
 }
-#define MPPI_SPIN_OR_GIVE_UP(spins, tmo, lane)        \
-    if (spins >= kSpinMax) {                          \
-        if ((lane) == 0) report_timeout(tmo);         \
-        break;                                        \
-    }                                                 \
+#define MPPI_SPIN_OR_GIVE_UP(spins, tmo, lane) MPPI_SPIN_OR_GIVE_UP_L(spins, kSpinMax, tmo, lane, (void)0)
+// with a bound of its own and a statement run when it gives up (the exchange's polls)
+#define MPPI_SPIN_OR_GIVE_UP_L(spins, lim, tmo, lane, on_give_up) \
+    if (spins >= (lim)) {                                         \
+        if ((lane) == 0) report_timeout(tmo);                     \
+        on_give_up;                                               \
+        break;                                                    \
+    }                                                             \
     __builtin_amdgcn_s_sleep(1)
 
 // Order-preserving 64-bit key of a double (unsigned order == numeric order; NaN
@@ -529,7 +541,9 @@ template <int NT, int MAXCH, bool final, bool GRAN, class SM>
 __device__ __forceinline__ void merge_rows_block(__amdgpu_buffer_rsrc_t rows, int row0, int n, const RowGeo& geo,
                                                  double inv_lambda, SM& sm, const __amdgpu_buffer_rsrc_t* out_wt,
                                                  int out_idx, double* out_row, double* w_eps_out, unsigned tag,
-                                                 unsigned* tmo) {
+                                                 unsigned* tmo, unsigned spin_max = kSpinMax,
+                                                 bool* failed = nullptr) {
+    // spin_max / failed: the polls' bound, and (when given) whether any poll of the workgroup gave up (uniform)
     constexpr bool EAGER = !GRAN && MAXCH == 1;  // one round trip per round of 32 rows
     constexpr int LB = EAGER ? 32 : 16;         // loads per batch per thread
     constexpr int RB = LB / MAXCH;              // rows per load batch
@@ -541,6 +555,7 @@ __device__ __forceinline__ void merge_rows_block(__amdgpu_buffer_rsrc_t rows, in
 #pragma unroll
     for (int ch = 0; ch < MAXCH; ++ch) acc[ch] = 0.0;
     int nrel = 0;
+    bool gave_up = false;
     for (int r0 = 0; r0 < n; r0 += R1) {
         const int nr = min(R1, n - r0);   // uniform
         const int rb = row0 + r0;
@@ -552,7 +567,7 @@ __device__ __forceinline__ void merge_rows_block(__amdgpu_buffer_rsrc_t rows, in
                 asm volatile("" ::: "memory");
                 gr = ld_gran(rows, lrow);
                 if (__all(lane >= nr || gran_ok(gr, tag))) break;
-                MPPI_SPIN_OR_GIVE_UP(spins, tmo, lane);
+                MPPI_SPIN_OR_GIVE_UP_L(spins, spin_max, tmo, lane, gave_up = true);
             }
             rho_r = gran_val(gr);
         } else if constexpr (!EAGER) {
@@ -617,7 +632,7 @@ __device__ __forceinline__ void merge_rows_block(__amdgpu_buffer_rsrc_t rows, in
                             ok = ok && (!on || gran_ok(gv[j], tag));
                         }
                         if (__all(ok)) break;
-                        MPPI_SPIN_OR_GIVE_UP(spins, tmo, lane);
+                        MPPI_SPIN_OR_GIVE_UP_L(spins, spin_max, tmo, lane, gave_up = true);
                     }
                     if (b0 == 0) eta_l = gran_val(ge);
 #pragma unroll
@@ -644,6 +659,7 @@ __device__ __forceinline__ void merge_rows_block(__amdgpu_buffer_rsrc_t rows, in
             }
         }
     }
+    if (failed) *failed = __syncthreads_or(gave_up);
     if constexpr (final) {
         put_final<NT, MAXCH>(rho, acc, eta, nrel, geo, sm, out_row, w_eps_out);
     } else {
@@ -979,8 +995,10 @@ struct XDesc {
     const void* peer[kMaxWorld];   // inbox base of every rank (own rank: local memory)
     double* row;                   // this rank's merged row, written by the launch's final merge
     unsigned* epoch;               // this rank's exchange epoch
-    int rank, world, bytes;        // bytes: inbox size (2 x world rows of `stride` granules)
+    int rank, world, bytes;        // bytes: inbox size (2 x world rows of `stride` granules, 2 x world statuses)
+    unsigned spin_max;             // the exchange polls' bound (MPPI_EXCHANGE_SPINS at attach; default kSpinMax)
 };
+constexpr unsigned kTmoLocal = 1u, kTmoExchange = 2u;   // host timeout word: in-launch hand-off / exchange
 __device__ __forceinline__ void st_gran_sys(__amdgpu_buffer_rsrc_t r, int idx, double v, unsigned tag) {
     const unsigned long long b = (unsigned long long)__double_as_longlong(v);
     const u32x4 x = {(unsigned)b, tag, (unsigned)(b >> 32), tag};
@@ -989,20 +1007,57 @@ __device__ __forceinline__ void st_gran_sys(__amdgpu_buffer_rsrc_t r, int idx, d
 
 // Called by the final workgroup after its merge wrote x.row (put_final ends with
 // a barrier, so the row is visible to the whole workgroup).
+//
+// Failure semantics (a rank late past the bound, or gone): after the row round,
+// every rank writes a status granule (+1: it had every row in time, -1: not) to
+// every inbox and polls all of them; the step holds only if every rank reports
+// +1.  A rank that gave up wrote its -1 before leaving, so a late rank, whenever
+// it arrives, finds that status next to the rows it needs: every rank of the
+// step reaches the same verdict.  On failure the launch reports kTmoExchange
+// (the host raises MPPI_E_EXCHANGE and keeps the nominal: no update is applied)
+// and the caller runs the step again over the collective fallback.  The epoch
+// advances either way, so the ranks stay in step for the next exchange.
 template <int NT, int MAXCH, class SM>
-__device__ __forceinline__ void exchange_merge(const XDesc& x, const RowGeo& geo, double inv_lambda, SM& sm,
+__device__ __forceinline__ bool exchange_merge(const XDesc& x, const RowGeo& geo, double inv_lambda, SM& sm,
                                                double* w_eps_out, unsigned* tmo) {
     // the previous exchange launch's final store; kernel boundaries order it
     const unsigned tag = (unsigned)__builtin_amdgcn_readfirstlane((int)*x.epoch) + 1u;
     const int par = (int)(tag & 1u), stride = geo.stride;
+    const unsigned lim = x.spin_max ? x.spin_max : kSpinMax;
     for (int idx = threadIdx.x; idx < stride; idx += NT) {
         const double v = x.row[idx];
         for (int p = 0; p < x.world; ++p)
             st_gran_sys(rows_rsrc(x.peer[p], x.bytes), (par * x.world + x.rank) * stride + idx, v, tag);
     }
+    bool late = false;
     merge_rows_block<NT, MAXCH, true, true>(rows_rsrc(x.peer[x.rank], x.bytes), par * x.world, x.world, geo,
-                                            inv_lambda, sm, nullptr, 0, nullptr, w_eps_out, tag, tmo);
-    if (threadIdx.x == 0) *x.epoch = tag;
+                                            inv_lambda, sm, nullptr, 0, nullptr, w_eps_out, tag, nullptr, lim, &late);
+    // this rank's own row is invalid if an in-launch hand-off of this launch timed out
+    late = __syncthreads_or(late || (threadIdx.x == 0 && tmo &&
+                                     __hip_atomic_load(tmo, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) == kTmoLocal));
+    // status round
+    const int sbase = 2 * x.world * stride + par * x.world;   // status granules follow the rows: [parity][rank]
+    const int tid = threadIdx.x, lane = tid & 63;
+    if (tid < x.world) st_gran_sys(rows_rsrc(x.peer[tid], x.bytes), sbase + x.rank, late ? -1.0 : 1.0, tag);
+    bool bad = false;
+    if (tid < 64) {   // wave 0 polls every rank's status (world <= 64)
+        const __amdgpu_buffer_rsrc_t own = rows_rsrc(x.peer[x.rank], x.bytes);
+        u32x4 g;
+        bool missing = false;
+        for (unsigned spins = 0;; ++spins) {
+            asm volatile("" ::: "memory");
+            g = ld_gran(own, lane < x.world ? sbase + lane : kOffRange);
+            if (__all(lane >= x.world || gran_ok(g, tag))) break;
+            MPPI_SPIN_OR_GIVE_UP_L(spins, lim, nullptr, lane, missing = true);
+        }
+        bad = __any(lane < x.world && !(gran_ok(g, tag) && gran_val(g) > 0.0)) || missing;
+    }
+    bad = __syncthreads_or(bad);
+    if (tid == 0) {
+        if (bad) __hip_atomic_store(tmo, kTmoExchange, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        *x.epoch = tag;
+    }
+    return !bad;
 }
 
 }  // namespace mppi

@@ -607,8 +607,17 @@ __global__ __launch_bounds__(NT) void rollout_kernel(
     }
     STAMP(11, NOW());
     STAMP(6, (unsigned long long)sm.nrel);
-    if (flags & MPPI_FLAG_EXCHANGE) exchange_merge<NT, 1>(xd, geo, c.inv_lambda, sm, w_eps_out, tmo);
-    if (flags & MPPI_FLAG_FUSED_UPDATE) nominal_update_block<NT>(nxt, c, sm, u_cur, u_first, upd, ho);
+    const bool xok = (flags & MPPI_FLAG_EXCHANGE) ? exchange_merge<NT, 1>(xd, geo, c.inv_lambda, sm, w_eps_out, tmo)
+                                                  : true;
+    if (flags & MPPI_FLAG_FUSED_UPDATE) {
+        if (xok) {
+            nominal_update_block<NT>(nxt, c, sm, u_cur, u_first, upd, ho);
+        } else if (ho.p) {   // the exchange failed: no update; the host's wait ends and reads the timeout word
+            __syncthreads();
+            if (threadIdx.x == 0)
+                __hip_atomic_store(reinterpret_cast<unsigned*>(ho.p), ho.seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+        }
+    }
     STAMP(7, NOW());
 }
 
@@ -769,6 +778,7 @@ struct mppi_ctx {
     // the current device nominal is the one the last MPPI_FLAG_HOST_OUT launch
     // published (h_dout): a drop-in step whose u equals it uploads nothing
     bool nominal_published = false;
+    bool x_flipped = false;          // the last launch flipped the ping-pong and exchanged (undone on MPPI_E_EXCHANGE)
     double* h_dout = nullptr;       // coherent host-mapped drop-in outputs (HostOut layout)
     double* d_dout = nullptr;       // its device view
     unsigned dseq = 0;
@@ -813,9 +823,15 @@ int fail(int code, const std::string& msg) {
     return code;
 }
 const char* last_error() { return g_err.c_str(); }
+unsigned exchange_spins() {
+    const char* e = getenv("MPPI_EXCHANGE_SPINS");
+    const long v = e ? strtol(e, nullptr, 10) : 0;
+    return v > 0 ? (unsigned)v : 0u;
+}
 }  // namespace mppi_host
 
 namespace {
+using mppi_host::exchange_spins;
 using mppi_host::fail;
 
 #define HIP_TRY(expr)                                                                 \
@@ -837,11 +853,19 @@ int occupancy(int* per_cu) {
 }
 
 int check_timeout(mppi_ctx* c) {
-    if (c->h_tmo && __atomic_load_n(c->h_tmo, __ATOMIC_ACQUIRE)) {
-        *c->h_tmo = 0;
-        return fail(MPPI_E_HIP, "in-launch hand-off timed out (workgroups not co-resident?); results invalid");
+    const unsigned v = c->h_tmo ? __atomic_load_n(c->h_tmo, __ATOMIC_ACQUIRE) : 0u;
+    if (!v) return MPPI_OK;
+    *c->h_tmo = 0;
+    if (v == kTmoExchange) {
+        // every rank of the step reports it and none applied the update: back to the nominal before the launch
+        if (c->x_flipped) c->cur ^= 1;
+        c->x_flipped = false;
+        c->upd_valid = false;
+        c->nominal_published = false;
+        return fail(MPPI_E_EXCHANGE, "multi-GPU exchange: a rank's row did not arrive within the bound on every "
+                                     "rank of this step; no rank applied the update (run the step again)");
     }
-    return MPPI_OK;
+    return fail(MPPI_E_HIP, "in-launch hand-off timed out (workgroups not co-resident?); results invalid");
 }
 
 int auto_lps(int K_local) {
@@ -1136,8 +1160,10 @@ int wait_host_out(mppi_ctx* c) {
         __builtin_ia32_pause();
     }
     c->stage_pending = false;   // the launch ran, so every staging copy before it did too
+    if (int rc = check_timeout(c)) return rc;
     c->nominal_published = true;
-    return check_timeout(c);
+    c->x_flipped = false;
+    return MPPI_OK;
 }
 
 // _F (control.py:234-263) in fp64 on the host: the mass matrix as written, its
@@ -1225,6 +1251,7 @@ int launch_rollout(mppi_ctx* c, const float* noise_dev, double* S_dev, double* p
         c->cur ^= 1;
         c->upd_valid = true;
         c->nominal_published = false;   // until wait_host_out sees this launch's outputs
+        c->x_flipped = (flags & MPPI_FLAG_EXCHANGE) != 0;   // undone if the exchange fails (check_timeout)
     }
     return rc;
 }
@@ -1237,7 +1264,7 @@ int mppi_exchange_handle(mppi_ctx* c, int world, void* handle_out) {
     if (c->d_inbox && c->xworld_alloc != world) return fail(MPPI_E_ARG, "inbox already sized for another world");
     const int stride = 2 + 2 * c->cfg.T;
     if (!c->d_inbox) {
-        const size_t bytes = (size_t)2 * world * stride * 16;
+        const size_t bytes = (size_t)2 * world * (stride + 1) * 16;   // rows and statuses, two parities
         HIP_TRY(hipSetDevice(c->device));
         HIP_TRY(hipExtMallocWithFlags(&c->d_inbox, bytes, hipDeviceMallocUncached));
         HIP_TRY(hipMemset(c->d_inbox, 0, bytes));
@@ -1272,6 +1299,7 @@ int mppi_exchange_attach(mppi_ctx* c, int rank, int world, const void* handles) 
     c->xd.epoch = c->d_xepoch;
     c->xd.rank = rank;
     c->xd.world = world;
+    c->xd.spin_max = exchange_spins();
     return MPPI_OK;
 }
 

@@ -13,6 +13,18 @@
 // (-ffp-contract=off), so every value equals NumPy's; the state left behind
 // (key, pos, the cached Gaussian) is the one NumPy would leave.
 //
+// The twist itself runs in parallel too: MT19937 is linear over GF(2), so the
+// key array of any later block is a polynomial in the step map applied to the
+// current one (jump-ahead: Haramoto, Matsumoto, Nishimura, L'Ecuyer, Panneton,
+// "Efficient jump ahead for F2-linear random number generators", 2008).  The
+// characteristic polynomial P of the per-word step is found once per process
+// by Berlekamp-Massey on the generator's own output; a jump by J words is
+// x^J mod P (binary powering, cached per J) evaluated on the state by Horner's
+// rule; each thread jumps to the block before its range, twists once (which
+// also fixes the 31 low bits of the oldest word, outside the 19937-bit state)
+// and twists its own range.  A self-test against the sequential twist guards
+// it; on any failure the twist stays sequential.
+//
 // Host code, never on the device path; the Python side (controller.py,
 // legacy_multivariate_normal) does the rest of multivariate_normal with
 // NumPy's own calls.
@@ -25,9 +37,16 @@
 #define MT_N 624
 #define MT_M 397
 
+// AVX2 instances of the integer-only loops where the CPU has it (the same bits either way)
+#if defined(__x86_64__) && defined(__GNUC__) && !defined(__clang__)
+#define MT_CLONES __attribute__((target_clones("avx2", "default")))
+#else
+#define MT_CLONES
+#endif
+
 // next key array from the previous one, out of place (no aliasing: the loops vectorize); the same values as
 // NumPy's in-place mt19937_gen
-static void mt_twist_to(const uint32_t* __restrict__ o, uint32_t* __restrict__ k) {
+MT_CLONES static void mt_twist_to(const uint32_t* __restrict__ o, uint32_t* __restrict__ k) {
     const uint32_t A = 0x9908b0dfu, UP = 0x80000000u, LO = 0x7fffffffu;
     for (int i = 0; i < MT_N - MT_M; i++) {
         const uint32_t y = (o[i] & UP) | (o[i + 1] & LO);
@@ -56,6 +75,280 @@ static inline uint32_t temper(uint32_t y) {
 
 static inline double legacy_double(uint32_t a, uint32_t b) {
     return ((a >> 5) * 67108864.0 + (b >> 6)) / 9007199254740992.0;
+}
+
+// ------------------------------------------------------------------ jump-ahead
+#define MT_DEG 19937                       // dimension of the state (the oldest word's top bit + 623 words)
+#define PW ((MT_DEG + 64) / 64)            // 64-bit words of a polynomial of degree <= MT_DEG
+typedef struct {
+    int ready;                             // 1: P below is valid; -1: unavailable (sequential twist)
+    uint64_t p[PW];                        // the characteristic polynomial, bit e = coefficient of x^e
+    int nterms;                            // its terms below x^MT_DEG
+    int terms[MT_DEG];
+} CharPoly;
+static CharPoly g_cp;
+
+static inline int bit_get(const uint64_t* a, int64_t i) { return (int)((a[i >> 6] >> (i & 63)) & 1u); }
+static inline void bit_flip(uint64_t* a, int64_t i) { a[i >> 6] ^= 1ull << (i & 63); }
+// 64 bits of a starting at bit i (bits past nwords*64 read as 0)
+static inline uint64_t bits64(const uint64_t* a, int64_t nwords, int64_t i) {
+    const int64_t w = i >> 6;
+    const int sh = (int)(i & 63);
+    const uint64_t lo = w < nwords ? a[w] : 0, hi = w + 1 < nwords ? a[w + 1] : 0;
+    return sh ? (lo >> sh) | (hi << (64 - sh)) : lo;
+}
+
+// Berlekamp-Massey over GF(2) on the bit-0 sequence of the untempered words from a seeded state: the minimal
+// polynomial of that sequence is the characteristic polynomial of the step map (irreducible for MT19937,
+// degree 19937).  P(x) = x^L C(1/x) for the connection polynomial C.
+static int char_poly_init(void) {
+    enum { NB = 2 * MT_DEG + 128, CW = (NB + 63) / 64 + 2 };
+    static uint64_t seq[CW], C[CW], B[CW], T[CW];
+    const int nblk = NB / MT_N + 3;
+    uint32_t* w = (uint32_t*)malloc((size_t)nblk * MT_N * sizeof(uint32_t));
+    if (!w) return -1;
+    w[0] = 5489u;   // init_genrand(5489)
+    for (int i = 1; i < MT_N; ++i) w[i] = 1812433253u * (w[i - 1] ^ (w[i - 1] >> 30)) + (uint32_t)i;
+    for (int b = 1; b < nblk; ++b) mt_twist_to(w + (size_t)(b - 1) * MT_N, w + (size_t)b * MT_N);
+    // s_n = bit 0 of word MT_N + n (generated words only), stored reversed: seq bit j = s_{NB-1-j}
+    memset(seq, 0, sizeof(seq));
+    for (int64_t n = 0; n < NB; ++n)
+        if (w[MT_N + n] & 1u) bit_flip(seq, NB - 1 - n);
+    free(w);
+    memset(C, 0, sizeof(C));
+    memset(B, 0, sizeof(B));
+    C[0] = B[0] = 1;
+    int64_t L = 0, m = 1;
+    for (int64_t n = 0; n < NB; ++n) {
+        // d = sum_{i=0..L} c_i s_{n-i} = parity of C[0..L] & seq[NB-1-n ..]
+        const int64_t off = NB - 1 - n, words = (L + 64) / 64;
+        uint64_t acc = 0;
+        for (int64_t q = 0; q < words; ++q) {
+            uint64_t c = C[q];
+            if (q == words - 1 && ((L + 1) & 63)) c &= (1ull << ((L + 1) & 63)) - 1;
+            acc ^= c & bits64(seq, CW, off + 64 * q);
+        }
+        if (!(__builtin_popcountll(acc) & 1)) {
+            ++m;
+            continue;
+        }
+        const int ws = (int)(m >> 6), bs = (int)(m & 63);
+        if (2 * L <= n) memcpy(T, C, sizeof(C));
+        for (int64_t q = CW - 1; q >= ws; --q) {   // C ^= B << m
+            const uint64_t v = (B[q - ws] << bs) | (bs && q - ws - 1 >= 0 ? B[q - ws - 1] >> (64 - bs) : 0);
+            C[q] ^= v;
+        }
+        if (2 * L <= n) {
+            L = n + 1 - L;
+            memcpy(B, T, sizeof(C));
+            m = 1;
+        } else {
+            ++m;
+        }
+    }
+    if (L != MT_DEG) return -1;
+    memset(g_cp.p, 0, sizeof(g_cp.p));
+    g_cp.nterms = 0;
+    for (int64_t i = 0; i <= L; ++i)
+        if (bit_get(C, i)) {   // c_i x^i  ->  x^(L - i)
+            bit_flip(g_cp.p, L - i);
+            if (L - i < MT_DEG) g_cp.terms[g_cp.nterms++] = (int)(L - i);
+        }
+    return bit_get(g_cp.p, MT_DEG) && bit_get(g_cp.p, 0) ? 0 : -1;
+}
+
+// a (bits 0 .. 2 MT_DEG, 2 PW words) reduced mod P in place: each set bit i >= MT_DEG is replaced by the
+// terms of P below x^MT_DEG shifted by i - MT_DEG (the leading term cancels it); top down, so bits flipped
+// at or above MT_DEG are handled after.
+static void reduce_mod(uint64_t* a) {
+    for (int64_t i = 2 * MT_DEG; i >= MT_DEG; --i) {
+        if (!bit_get(a, i)) continue;
+        bit_flip(a, i);
+        const int64_t sh = i - MT_DEG;
+        for (int e = 0; e < g_cp.nterms; ++e) bit_flip(a, sh + g_cp.terms[e]);
+    }
+}
+
+// x^J mod P by binary powering (squaring is the bit spread; multiplying by x a shift)
+static void pow_x_mod(uint64_t J, uint64_t* out /* PW words */) {
+    uint64_t r[2 * PW], t[2 * PW];
+    memset(r, 0, sizeof(r));
+    r[0] = 1;
+    int top = 63;
+    while (top > 0 && !((J >> top) & 1)) --top;
+    for (int b = top; b >= 0; --b) {
+        memset(t, 0, sizeof(t));   // t = r^2: bit i -> bit 2i
+        for (int q = 0; q < PW; ++q) {
+            uint64_t v = r[q];
+            while (v) {
+                const int k = __builtin_ctzll(v);
+                v &= v - 1;
+                bit_flip(t, 2 * (64 * (int64_t)q + k));
+            }
+        }
+        reduce_mod(t);
+        memcpy(r, t, sizeof(r));
+        if ((J >> b) & 1) {   // r *= x
+            for (int q = 2 * PW - 1; q > 0; --q) r[q] = (r[q] << 1) | (r[q - 1] >> 63);
+            r[0] <<= 1;
+            reduce_mod(r);
+        }
+    }
+    memcpy(out, r, PW * sizeof(uint64_t));
+}
+
+// jump polynomials already computed, keyed by J (words); guarded by g_jmu
+#define JCACHE 128
+static uint64_t g_jkey[JCACHE];
+static uint64_t* g_jpoly[JCACHE];
+static int g_jn = 0;
+static pthread_mutex_t g_jmu = PTHREAD_MUTEX_INITIALIZER;     // the cache
+static pthread_mutex_t g_initmu = PTHREAD_MUTEX_INITIALIZER;  // jump_init_locked
+
+static const uint64_t* jump_poly(uint64_t J) {
+    pthread_mutex_lock(&g_jmu);
+    for (int i = 0; i < g_jn; ++i)
+        if (g_jkey[i] == J) {
+            const uint64_t* p = g_jpoly[i];
+            pthread_mutex_unlock(&g_jmu);
+            return p;
+        }
+    pthread_mutex_unlock(&g_jmu);
+    uint64_t* p = (uint64_t*)malloc(PW * sizeof(uint64_t));   // computed outside the lock (threads in parallel)
+    if (!p) return NULL;
+    pow_x_mod(J, p);
+    pthread_mutex_lock(&g_jmu);
+    if (g_jn == JCACHE) {   // full: start over (the drop-in uses a handful of draw sizes)
+        for (int i = 0; i < g_jn; ++i) free(g_jpoly[i]);
+        g_jn = 0;
+    }
+    g_jkey[g_jn] = J;
+    g_jpoly[g_jn++] = p;
+    pthread_mutex_unlock(&g_jmu);
+    return p;
+}
+
+// The key array J words-steps after `key` (J = 624 b: the key array of block b), up to the 31 low bits of its
+// oldest word, which lie outside the state: Horner's rule sum_d phi_d F^d(key) with F the one-word step on a
+// circular array (F: word i <- word i + M ^ twist(word i, word i + 1), i advances).
+MT_CLONES static void jump_state(const uint32_t* key, const uint64_t* phi, uint32_t* out) {
+    uint32_t r[MT_N];
+    memset(r, 0, sizeof(r));
+    int idx = 0;   // r's logical word 0
+    int d = MT_DEG;
+    while (d > 0 && !bit_get(phi, d)) --d;
+    const uint32_t A = 0x9908b0dfu, UP = 0x80000000u, LO = 0x7fffffffu;
+    for (; d >= 0; --d) {
+        // r = F(r)
+        const int i1 = idx + 1 == MT_N ? 0 : idx + 1, iM = idx + MT_M >= MT_N ? idx + MT_M - MT_N : idx + MT_M;
+        const uint32_t y = (r[idx] & UP) | (r[i1] & LO);
+        r[idx] = r[iM] ^ (y >> 1) ^ (-(y & 1u) & A);
+        idx = i1;
+        if (bit_get(phi, d)) {   // r ^= key, aligned at the logical start
+            const int n1 = MT_N - idx;
+            for (int q = 0; q < n1; ++q) r[idx + q] ^= key[q];
+            for (int q = n1; q < MT_N; ++q) r[q - n1] ^= key[q];
+        }
+    }
+    for (int q = 0; q < MT_N; ++q) out[q] = r[(idx + q) % MT_N];
+}
+
+// once per process (under g_initmu): P, then a self-test of two jumps (to blocks 3 and 1000) against the
+// sequential twist
+static void jump_init_locked(void) {
+    if (g_cp.ready) return;
+    if (char_poly_init() != 0) {
+        g_cp.ready = -1;
+        return;
+    }
+    g_cp.ready = 1;
+    enum { NBT = 1001 };
+    uint32_t* w = (uint32_t*)malloc((size_t)NBT * MT_N * sizeof(uint32_t));
+    uint32_t j[MT_N], k[MT_N];
+    if (!w) {
+        g_cp.ready = -1;
+        return;
+    }
+    w[0] = 19650218u;
+    for (int i = 1; i < MT_N; ++i) w[i] = 1812433253u * (w[i - 1] ^ (w[i - 1] >> 30)) + (uint32_t)i;
+    for (int b = 1; b < NBT; ++b) mt_twist_to(w + (size_t)(b - 1) * MT_N, w + (size_t)b * MT_N);
+    const int tb[2] = {3, NBT - 1};
+    for (int q = 0; q < 2; ++q) {
+        const uint64_t* phi = jump_poly((uint64_t)MT_N * (tb[q] - 1));
+        if (!phi) {
+            g_cp.ready = -1;
+            break;
+        }
+        jump_state(w, phi, j);   // block tb - 1, up to its oldest word's low bits
+        mt_twist_to(j, k);       // block tb, exactly
+        if (memcmp(k, w + (size_t)tb[q] * MT_N, sizeof(k)) != 0) g_cp.ready = -1;
+    }
+    free(w);
+}
+
+typedef struct {
+    uint32_t* blocks;
+    int64_t b0, b1;   // blocks [b0, b1) to fill; block b0 - 1 from a jump when b0 > 1
+    int ok;
+} GenWork;
+
+static void* gen_pass(void* p) {
+    GenWork* g = (GenWork*)p;
+    uint32_t prev[MT_N];
+    const uint32_t* src = g->blocks + (size_t)(g->b0 - 1) * MT_N;
+    if (g->b0 > 1) {   // the block before the range: a jump from block 0 to block b0 - 2, one twist
+        const uint64_t* phi = jump_poly((uint64_t)MT_N * (uint64_t)(g->b0 - 2));
+        if (!phi) return NULL;
+        uint32_t j[MT_N];
+        if (g->b0 - 2 > 0) jump_state(g->blocks, phi, j);
+        else memcpy(j, g->blocks, sizeof(j));
+        mt_twist_to(j, prev);
+        src = prev;
+    }
+    for (int64_t b = g->b0; b < g->b1; ++b) {
+        mt_twist_to(src, g->blocks + (size_t)b * MT_N);
+        src = g->blocks + (size_t)b * MT_N;
+    }
+    g->ok = 1;
+    return NULL;
+}
+
+// blocks 1 .. nblk - 1 from block 0; in parallel when there are enough of them
+static int g_jump_min_blocks = 4096;   // below this the sequential twist (~0.5 us per block) is as fast
+
+static void twist_blocks(uint32_t* blocks, int64_t nblk, int nthreads) {
+    int nt = nthreads;
+    if (nblk < g_jump_min_blocks || nt < 2) nt = 1;
+    if (nt > 1) {
+        pthread_mutex_lock(&g_initmu);
+        jump_init_locked();
+        const int ready = g_cp.ready;
+        pthread_mutex_unlock(&g_initmu);
+        if (ready != 1) nt = 1;
+    }
+    if (nt == 1) {
+        for (int64_t b = 1; b < nblk; ++b) mt_twist_to(blocks + (b - 1) * MT_N, blocks + b * MT_N);
+        return;
+    }
+    GenWork gw[64];
+    pthread_t th[64];
+    // blocks per thread rounded up to a multiple of 64, so that the jump lengths (cached per length) stay the
+    // same from draw to draw although the state's position moves the block count by one
+    const int64_t per = ((nblk - 1 + nt - 1) / nt + 63) / 64 * 64;
+    for (int t = 0; t < nt; ++t) {
+        gw[t].blocks = blocks;
+        gw[t].b0 = 1 + per * t < nblk ? 1 + per * t : nblk;
+        gw[t].b1 = 1 + per * (t + 1) < nblk ? 1 + per * (t + 1) : nblk;
+        gw[t].ok = 0;
+    }
+    for (int t = 1; t < nt; ++t) pthread_create(&th[t], NULL, gen_pass, &gw[t]);
+    gen_pass(&gw[0]);
+    for (int t = 1; t < nt; ++t) pthread_join(th[t], NULL);
+    for (int t = 0; t < nt; ++t)
+        if (!gw[t].ok) {   // a failed allocation: the sequential twist
+            for (int64_t b = 1; b < nblk; ++b) mt_twist_to(blocks + (b - 1) * MT_N, blocks + b * MT_N);
+            return;
+        }
 }
 
 typedef struct {
@@ -143,7 +436,7 @@ static int legacy_gauss_locked(uint32_t* key, int* pos, int* has_gauss, double* 
         }
         uint32_t* blocks = g_blocks;
         memcpy(blocks, key, MT_N * sizeof(uint32_t));
-        for (int64_t b = 1; b < nblk; ++b) mt_twist_to(blocks + (b - 1) * MT_N, blocks + b * MT_N);
+        twist_blocks(blocks, nblk, nthreads);
         Work wk[64];
         pthread_t th[64];
         const int nt = (int)(A < nthreads * 4096 ? 1 : nthreads);
@@ -206,4 +499,17 @@ int mppi_np_legacy_gauss(uint32_t* key, int* pos, int* has_gauss, double* gauss,
     }
     pthread_mutex_unlock(&g_mu);
     return rc;
+}
+
+// Tests: the block count from which the twist runs in parallel (jump-ahead), and whether the jump machinery
+// passed its self-test (1), failed (-1) or has not run (0).
+int mppi_np_jump_config(int min_blocks) {
+    pthread_mutex_lock(&g_mu);
+    if (min_blocks > 0) g_jump_min_blocks = min_blocks;
+    pthread_mutex_lock(&g_initmu);
+    jump_init_locked();
+    const int r = g_cp.ready;
+    pthread_mutex_unlock(&g_initmu);
+    pthread_mutex_unlock(&g_mu);
+    return r;
 }

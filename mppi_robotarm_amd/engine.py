@@ -28,6 +28,34 @@ def _dptr(a: np.ndarray):
     return a.ctypes.data_as(C.POINTER(C.c_double))
 
 
+def _upload_std(eng, noise, z: torch.Tensor, out: torch.Tensor, perm) -> torch.Event:
+    """RolloutEngine / ChainEngine.upload_std_noise: rows [k_offset, k_offset + K_local) of the (K, T, du)
+    standard normals in the page-locked z, to the device, transformed there, into out (layout `perm` of
+    (K_local, T, du))."""
+    eng._sync_stream()
+    K, T, du = noise.z.shape
+    lo, kl = eng.k_offset, eng.K_local
+    zz = z[:K * T * du].view(K, T, du)[lo:lo + kl]
+    stage = getattr(eng, "_noise_stage", None)
+    if stage is None or tuple(stage.shape) != (kl, T, du):
+        stage = eng._noise_stage = torch.empty((kl, T, du), dtype=torch.float64, device=eng.device)
+    stage.copy_(zz, non_blocking=True)
+    ev = torch.cuda.Event()
+    ev.record()
+    key = (noise.src.tobytes(), noise.scale.tobytes(), noise.mean.tobytes())
+    if getattr(eng, "_std_key", None) != key:
+        eng._std_key = key
+        eng._std_t = (torch.from_numpy(noise.src).to(eng.device), torch.from_numpy(noise.scale).to(eng.device),
+                      torch.from_numpy(noise.mean).to(eng.device),
+                      bool(np.array_equal(noise.src, np.arange(du))))
+    src, scale, mean, ident = eng._std_t
+    x = stage if ident else stage.index_select(2, src)
+    x = torch.mul(x, scale)          # the np.dot with one nonzero per column: exact products
+    x.add_(mean)                     # x += mean
+    out.copy_(x.permute(*perm))      # transpose + fp64 -> fp32 (round to nearest, as astype)
+    return ev
+
+
 class RolloutEngine:
     """Owns one ``mppi_ctx`` (one device, one shard of samples)."""
 
@@ -126,6 +154,14 @@ class RolloutEngine:
         stage.copy_(torch.from_numpy(eps))
         out.copy_(stage.permute(1, 0, 2))
         return out
+
+    def upload_std_noise(self, noise, z: torch.Tensor, out: torch.Tensor) -> torch.Event:
+        """The reference's draw from its standard normals (hostrng.StdNoise `noise`, whose z lives in the
+        page-locked tensor `z`; this shard's K_local rows from k_offset): one DMA, then the transform
+        x = z[..., src] * scale + mean as NumPy's (separate fp64 multiply and add: exact, so the values equal
+        np.random.multivariate_normal's) and the transpose with the rounding to fp32 (upload_noise).  Returns
+        the event after the DMA: z must not be rewritten before it."""
+        return _upload_std(self, noise, z, out, (1, 0, 2))
 
     # -- the hot path -------------------------------------------------------
     def set_step_inputs(self, x0, window, u=None) -> None:

@@ -37,9 +37,10 @@ def _threads() -> int:
     return max(1, min(16, n))
 
 
-def legacy_standard_normal(n: int) -> np.ndarray | None:
-    """n values of np.random.standard_normal(n) from the global state, advancing it as NumPy would; None when
-    this path does not apply (the caller then uses NumPy)."""
+def legacy_standard_normal(n: int, out: np.ndarray | None = None) -> np.ndarray | None:
+    """n values of np.random.standard_normal(n) from the global state, advancing it as NumPy would, into `out`
+    (a C-contiguous float64 array of at least n values, e.g. page-locked) or a fresh array; None when this path
+    does not apply (the caller then uses NumPy; the state is untouched)."""
     if n < _MIN_NORMALS:
         return None
     lib = _load()
@@ -50,7 +51,12 @@ def legacy_standard_normal(n: int) -> np.ndarray | None:
         return None
     key = np.array(st[1], dtype=np.uint32, copy=True)
     pos, has_gauss, gauss = C.c_int(int(st[2])), C.c_int(int(st[3])), C.c_double(float(st[4]))
-    out = np.empty(n, dtype=np.float64)
+    if out is None:
+        out = np.empty(n, dtype=np.float64)
+    else:
+        if out.dtype != np.float64 or not out.flags.c_contiguous or out.size < n or not out.flags.writeable:
+            raise ValueError("out must be a writable C-contiguous float64 array of at least n values")
+        out = out.reshape(-1)[:n]
     rc = lib.mppi_np_legacy_gauss(key.ctypes.data, C.byref(pos), C.byref(has_gauss), C.byref(gauss),
                                   out.ctypes.data, n, _threads())
     if rc != 0:
@@ -82,3 +88,63 @@ def multivariate_normal(mean, cov, size) -> np.ndarray:
     x += mean
     x.shape = tuple(final_shape)
     return x
+
+
+def monomial_transform(mean, cov):
+    """multivariate_normal's transform x = z @ (sqrt(s)[:, None] * v) + mean (NumPy's svd of cov, its
+    positive-semidefinite check and warning) when that matrix has at most one nonzero per column: then
+    x[..., j] = z[..., src[j]] * scale[j] + mean[j] exactly (the other products are exact zeros), so the
+    device can apply it to the standard normals.  Returns (src, scale, mean) as float64 / int64 arrays, or None
+    for another shape of transform (the caller keeps NumPy's np.dot).  Run.py's Sigma = 20 I and the chain's
+    diagonal Sigma are of this kind."""
+    mean = np.array(mean)
+    cov = np.array(cov)
+    if len(mean.shape) != 1 or len(cov.shape) != 2 or cov.shape[0] != cov.shape[1] or mean.shape[0] != cov.shape[0]:
+        return None
+    cov = cov.astype(np.double)
+    (u, s, v) = np.linalg.svd(cov)
+    m = np.sqrt(s)[:, None] * v
+    nz = m != 0
+    if not np.all(nz.sum(axis=0) <= 1):   # a zero column (singular cov) is x = mean: z * 0 + mean
+        return None
+    psd = np.allclose(np.dot(v.T * s, v), cov, rtol=1e-8, atol=1e-8)
+    if not psd:
+        warnings.warn("covariance is not symmetric positive-semidefinite.", RuntimeWarning)
+    src = np.argmax(nz, axis=0).astype(np.int64)
+    return src, m[src, np.arange(m.shape[1])].astype(np.float64), mean.astype(np.float64)
+
+
+class StdNoise:
+    """multivariate_normal(mean, cov, size) left untransformed: the standard normals z (final shape, NumPy's
+    values, in the caller's buffer) and the scaled column permutation that makes them the draw.  eps(idx)
+    evaluates one element of the draw as the device does."""
+
+    def __init__(self, z: np.ndarray, src: np.ndarray, scale: np.ndarray, mean: np.ndarray):
+        self.z, self.src, self.scale, self.mean = z, src, scale, mean
+
+    def eps(self, k: int, t: int, d: int) -> float:
+        return float(self.z[k, t, self.src[d]] * self.scale[d] + self.mean[d])
+
+
+def multivariate_normal_std(mean, cov, size, out: np.ndarray) -> StdNoise | None:
+    """np.random.multivariate_normal(mean, cov, size) for a caller that applies the transform itself (on the
+    device): when the transform is a scaled column permutation (monomial_transform; NumPy's checks and
+    warning included), the standard normals are drawn into `out` (float64, C-contiguous, at least the draw's
+    size: e.g. page-locked) exactly as NumPy draws them, and StdNoise is returned; otherwise None and nothing
+    is drawn (the caller then takes multivariate_normal).  The global RNG state moves as NumPy's would."""
+    mean_a = np.array(mean)
+    if len(mean_a.shape) != 1:
+        return None
+    shape = [size] if isinstance(size, (int, np.integer)) else ([] if size is None else list(size))
+    final_shape = tuple(shape) + (mean_a.shape[0],)
+    n = int(np.prod(final_shape))
+    if n < _MIN_NORMALS or out.size < n:
+        return None
+    plan = monomial_transform(mean, cov)
+    if plan is None:
+        return None
+    z = legacy_standard_normal(n, out=out)
+    if z is None:   # NumPy's own draw of the same standard normals (multivariate_normal's first call)
+        z = out.reshape(-1)[:n]
+        z[:] = np.random.standard_normal(n)
+    return StdNoise(z.reshape(final_shape), *plan)

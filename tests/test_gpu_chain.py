@@ -410,9 +410,11 @@ def test_chain_c5_spread_weights(paths):
 
 
 def test_chain_lanes_per_sample_agree(paths):
-    """A quad per sample and one lane per sample on the same inputs: S within fp32 rounding of each other (the
-    quad sums the control-cost terms in another order), the same argmin, w_eps within 1e-4; auto picks 4 at
-    the 8-way shard of config 5 (K = 16384) and 1 at the full K."""
+    """A quad per sample and one lane per sample on the same inputs: S within the fp32 bound each keeps against
+    the fp64 oracle (p99 2e-4, test_chain_n7_against_c_oracle: the quad steps in absolute angles and sums the
+    control-cost terms in another order, so its roundings, and the nearest-waypoint ties they tip, are its own),
+    the same argmin, w_eps within 1e-4; auto picks 4 at the 8-way shard of config 5 (K = 16384) and 1 at the
+    full K."""
     K, T, lam = 16384, 64, 100.0
     _, x0, _, ug = _c5()
     win = paths["xydq_circle"][:30]
@@ -430,7 +432,7 @@ def test_chain_lanes_per_sample_agree(paths):
     print(f"lps 4 vs 1: S rel p99 {np.percentile(rel, 99):.2e} max {rel.max():.2e}, "
           f"w_eps {_urel(out[4][1], out[1][1]):.2e}")
     assert int(np.argmin(out[4][0])) == int(np.argmin(out[1][0]))
-    assert float(np.percentile(rel, 99)) < 1e-4
+    assert float(np.percentile(rel, 99)) < 2e-4
     assert _urel(out[4][1], out[1][1]) < U_TOL
     assert _engine(16384, 8).lanes_per_sample == 4 and _engine(131072, 8).lanes_per_sample == 1
 

@@ -137,6 +137,67 @@ def _chain_step(pg, exchange, sampled=True):
     return out
 
 
+LATE_SPINS = "50000"   # MPPI_EXCHANGE_SPINS for the late-rank scenarios: a poll bound of ~50-100 ms
+LATE_TICK, LATE_SLEEP_S = 2, 0.4
+
+
+def _late_rank_ticks(pg, exchange):
+    """Failure semantics of the in-launch exchange: rank 1 starts its tick LATE_TICK LATE_SLEEP_S late, far
+    past the poll bound.  Every rank must see the step fail (ExchangeError inside the call, no update applied
+    anywhere), run it again over the all-gather and return the single-process result; the later ticks run
+    over the all-gather and match too (the state left by the failed launch is consistent)."""
+    import time
+    from mppi_robotarm_amd.controller import MPPIControllerForPathTracking
+    g, paths = load_loop("k64_t20"), load_paths()
+    rank = pg.rank() if pg is not None else 0
+    os.environ["MPPI_EXCHANGE_SPINS"] = LATE_SPINS
+    try:
+        c = MPPIControllerForPathTracking(delta_t=0.006, ref_path=paths["xydq_circle"], horizon_step_T=DEV_T,
+                                          number_of_samples_K=DEV_K, verbose=False, noise="device", seed=DEV_SEED,
+                                          process_group=pg, exchange=exchange, **RUNPY)
+        useq, idx, modes = [], [], []
+        for i in range(DEV_TICKS):
+            if i == LATE_TICK and rank == 1:
+                time.sleep(LATE_SLEEP_S)
+            _, u_seq, _, _ = c.calc_control_input(g["states"][i])
+            useq.append(u_seq.copy())
+            idx.append(c.prev_waypoints_idx)
+            modes.append(str(c._xmode))
+        out = dict(u_seq=np.array(useq), prev=np.array(idx), modes=np.array(modes), xmode=str(c._xmode))
+        c.close()
+    finally:
+        del os.environ["MPPI_EXCHANGE_SPINS"]
+    return out
+
+
+def _late_rank_chain(pg, exchange):
+    """The same for the chain controller's fused step (n = 2, the reference's step fixture, device noise)."""
+    import time
+    from mppi_robotarm_amd.chain import ChainMPPIController, ChainParams
+    g, paths = load_step("runpy_k100_t30"), load_paths()
+    rank = pg.rank() if pg is not None else 0
+    os.environ["MPPI_EXCHANGE_SPINS"] = LATE_SPINS
+    try:
+        c = ChainMPPIController(float(g["delta_t"]), paths[str(g["path"])], int(g["T"]), 4096,
+                                float(g["param_exploration"]), float(g["param_lambda"]), float(g["param_alpha"]),
+                                g["sigma"], g["stage_cost_weight"], g["terminal_cost_weight"],
+                                chain=ChainParams.from_arm2(), u_init=g["u_prev"], noise="device", seed=5,
+                                process_group=pg, exchange=exchange)
+        useq, modes = [], []
+        for i in range(4):
+            c.prev_waypoints_idx = int(g["prev_idx"])
+            if i == LATE_TICK and rank == 1:
+                time.sleep(LATE_SLEEP_S)
+            _, u_seq, _, _ = c.calc_control_input(g["x0"])
+            useq.append(u_seq.copy())
+            modes.append(str(c._xmode))
+        out = dict(u_seq=np.array(useq), modes=np.array(modes), xmode=str(c._xmode))
+        c.close()
+    finally:
+        del os.environ["MPPI_EXCHANGE_SPINS"]
+    return out
+
+
 SCENARIOS = {
     "step_auto": (_step_runpy, "auto"), "step_rccl": (_step_runpy, "rccl"),
     "loop_auto": (_loop, "auto"),
@@ -144,6 +205,8 @@ SCENARIOS = {
     "chain_auto": (_chain_step, "auto"), "chain_rccl": (_chain_step, "rccl"),
     # no sampled re-roll: the chain's fused step (update in the launch, after the in-launch exchange)
     "chainfused_auto": (lambda pg, ex: _chain_step(pg, ex, sampled=False), "auto"),
+    "late_auto": (_late_rank_ticks, "auto"),
+    "latechain_auto": (_late_rank_chain, "auto"),
 }
 
 
@@ -185,10 +248,10 @@ def test_ranks_agree_and_match_single_process(ranks, single, name):
     r0, r1, s = _get(ranks[0], name), _get(ranks[1], name), single[name]
     for k in r0:
         np.testing.assert_array_equal(r0[k], r1[k], err_msg=f"{name}.{k}: ranks differ")
-    want = "rccl" if name.endswith("rccl") else "launch"
+    want = "rccl" if name.endswith("rccl") or name.startswith("late") else "launch"
     assert str(r0["xmode"]) == want, "exchange='auto' must pick the in-launch exchange when its check passes"
     for k, v in s.items():
-        if k in ("xmode", "bound"):
+        if k in ("xmode", "bound", "modes"):
             continue
         if np.asarray(v).dtype.kind == "f":
             np.testing.assert_allclose(r0[k], v, rtol=X_TOL, atol=X_TOL, err_msg=f"{name}.{k}")
@@ -233,3 +296,14 @@ def test_sharded_chain_n2_matches_reference_fixture(ranks, mode):
         assert not np.any(r["samp"])                  # control.py:135 zeros without the re-roll
     else:
         np.testing.assert_allclose(r["samp"], g["sampled_traj"], rtol=1e-4, atol=1e-4)
+
+
+@pytest.mark.parametrize("name", ["late_auto", "latechain_auto"])
+def test_late_rank_falls_back_on_every_rank(ranks, name):
+    """The in-launch exchange on its poll bound: both ranks ran the ticks before the late one in-launch, took
+    the collective fallback in the late tick itself (no exception reached the caller) and stayed on it; the
+    results are the single-process controller's at every tick (test_ranks_agree_and_match_single_process)."""
+    for r in ranks:
+        modes = list(_get(r, name)["modes"])
+        assert modes[:LATE_TICK] == ["launch"] * LATE_TICK, modes
+        assert all(m == "rccl" for m in modes[LATE_TICK:]), modes

@@ -65,3 +65,62 @@ def test_errors_are_numpys():
         hostrng.multivariate_normal(np.zeros(2), np.eye(3), (40000, 2))
     with pytest.warns(RuntimeWarning):
         hostrng.multivariate_normal(np.zeros(2), np.array([[1.0, 2.0], [0.0, 1.0]]), (40000, 2))
+
+
+def _jump_lib():
+    import ctypes as C
+    lib = hostrng._load()
+    lib.mppi_np_jump_config.restype = C.c_int
+    lib.mppi_np_jump_config.argtypes = [C.c_int]
+    return lib
+
+
+def test_jump_ahead_self_test_passes():
+    """The twist in parallel rests on MT19937's jump-ahead: the characteristic polynomial found by
+    Berlekamp-Massey (degree 19937, 135 terms) and two jumps checked against the sequential twist."""
+    assert _jump_lib().mppi_np_jump_config(0) == 1
+
+
+@pytest.mark.parametrize("pre", [0, 5, 1001])
+@pytest.mark.parametrize("n", [1 << 15, 300001, 2_000_000])
+def test_parallel_twist_equals_numpy(n, pre):
+    """The threads' ranges start at jumped blocks (the threshold lowered to 8 blocks so that every size here
+    takes that path): values and the state left behind equal NumPy's."""
+    lib = _jump_lib()
+    lib.mppi_np_jump_config(8)
+    try:
+        np.random.seed(23 + pre)
+        np.random.standard_normal(pre)
+        s0 = np.random.get_state()
+        a = np.random.standard_normal(n)
+        sa = np.random.get_state()
+        np.random.set_state(s0)
+        b = hostrng.legacy_standard_normal(n)
+        assert b is not None and np.array_equal(a, b)
+        assert _state_eq(sa, np.random.get_state())
+    finally:
+        lib.mppi_np_jump_config(4096)
+
+
+@pytest.mark.parametrize("cov", [np.eye(2) * 20.0, np.diag([1.0, 5.0]), np.diag([20.0, 16, 12, 8, 4, 2, 1]),
+                                 np.array([[0.0, 0.0], [0.0, 3.0]])])
+def test_std_noise_equals_numpy(cov):
+    """multivariate_normal_std: the standard normals into the caller's buffer plus a scaled column
+    permutation (a diagonal Sigma, sorted or not) give NumPy's values exactly and leave its state; a Sigma
+    whose transform mixes columns draws nothing."""
+    d = cov.shape[0]
+    size = (9001, 5)
+    np.random.seed(31)
+    a = np.random.multivariate_normal(np.zeros(d), cov, size)
+    sa = np.random.get_state()
+    np.random.seed(31)
+    buf = np.empty(9001 * 5 * d + 3)
+    r = hostrng.multivariate_normal_std(np.zeros(d), cov, size, buf)
+    assert r is not None and np.shares_memory(r.z, buf)
+    x = r.z[..., r.src] * r.scale + r.mean
+    assert np.array_equal(a, x) and _state_eq(sa, np.random.get_state())
+    assert r.eps(3, 4, d - 1) == a[3, 4, d - 1]
+    np.random.seed(31)
+    s0 = np.random.get_state()
+    assert hostrng.multivariate_normal_std(np.zeros(2), np.array([[20.0, 5.0], [5.0, 10.0]]), size, buf) is None
+    assert _state_eq(s0, np.random.get_state())
