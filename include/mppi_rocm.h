@@ -32,7 +32,7 @@ extern "C" {
 #define MPPI_E_SINGULAR -3   /* singular Sigma: the reference raises LinAlgError at   */
                              /* control.py:106 (np.linalg.inv)                          */
 #define MPPI_E_EXCHANGE -5   /* multi-GPU in-launch exchange: a rank's row missed the poll
-                                bound (MPPI_EXCHANGE_SPINS, default ~1 s) on some rank of the
+                                bound (MPPI_EXCHANGE_TIMEOUT_US, default ~1 s) on some rank of the
                                 step; every rank of the step reports it and none applied the
                                 update (the nominal is the one before the step)              */
 #define MPPI_E_PATH_END -4   /* mppi_dropin_tick: the updated waypoint index reached   */

@@ -395,6 +395,7 @@ class ChainMPPIController:
         self._xmode = None
         self._noise_ready = None       # (seed, step) of the device noise already in the buffer
         self._spread = False           # precision="auto": the last step's weights were spread (next step fp64)
+        self._x_failed = False         # an in-launch exchange failed (a late rank): the all-gather from then on
         self.last_precision = None     # the rollout precision of the last step's result
         self.last_eta = None           # and the spread of its weights (eta, mppi_chain_last_eta)
         self._last_sampled = None      # the previous call's sampled_traj_list (_fresh_sampled)
@@ -465,7 +466,7 @@ class ChainMPPIController:
             raise RuntimeError("ranks disagree on the noise stream: every rank must seed np.random identically "
                                "(and pass the same seed / K / T)")
         mode = "rccl"
-        if self.exchange != "rccl":
+        if self.exchange != "rccl" and not self._x_failed:   # after a failed exchange: the all-gather for good
             ok = attach_exchange(eng, pg)
             ok = ok and check_exchange(eng, self._noise_dev, self._partial, self._gathered, pg)
             if not ok and self.exchange == "launch":
@@ -545,7 +546,12 @@ class ChainMPPIController:
         try:
             return self._device_step(prec, x0, window, u, epsilon, step)
         except N.ExchangeError:
+            # a late rank is the ranks' property, not one engine's: every engine takes the all-gather from now on
+            self._x_failed = True
             self._xmode = "rccl"
+            for parked in self._slots.values():
+                if parked.get("_xmode") is not None:
+                    parked["_xmode"] = "rccl"
             self._noise_ready = None   # the fused step queues the next draw into the buffer: draw this one again
             return self._device_step(prec, x0, window, u, epsilon, step)
 

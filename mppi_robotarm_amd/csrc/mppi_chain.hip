@@ -1424,7 +1424,7 @@ struct mppi_chain_ctx {
 
 namespace {
 
-using mppi_host::exchange_spins;
+using mppi_host::exchange_timeout_ticks;
 using mppi_host::fail;
 
 template <int N, bool P, bool F64, int LPS>
@@ -1879,7 +1879,7 @@ int mppi_chain_exchange_attach(mppi_chain_ctx* c, int rank, int world, const voi
     c->xd.epoch = c->d_xepoch;
     c->xd.rank = rank;
     c->xd.world = world;
-    c->xd.spin_max = exchange_spins();
+    c->xd.timeout_ticks = exchange_timeout_ticks();
     return MPPI_OK;
 }
 

@@ -437,14 +437,15 @@ constexpr unsigned kSpinMax = 1u << 20;
 __device__ __forceinline__ void report_timeout(unsigned* tmo) {
     if (tmo) __hip_atomic_store(tmo, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
 }
-#define MPPI_SPIN_OR_GIVE_UP(spins, tmo, lane) MPPI_SPIN_OR_GIVE_UP_L(spins, kSpinMax, tmo, lane, (void)0)
-// with a bound of its own and a statement run when it gives up (the exchange's polls)
-#define MPPI_SPIN_OR_GIVE_UP_L(spins, lim, tmo, lane, on_give_up) \
-    if (spins >= (lim)) {                                         \
-        if ((lane) == 0) report_timeout(tmo);                     \
-        on_give_up;                                               \
-        break;                                                    \
-    }                                                             \
+#define MPPI_SPIN_OR_GIVE_UP(spins, tmo, lane) MPPI_SPIN_OR_GIVE_UP_L(spins, 0ull, tmo, lane, (void)0)
+// with a deadline of its own (s_memrealtime ticks, 100 MHz; 0: the spin bound alone) and a statement run
+// when it gives up (the exchange's polls)
+#define MPPI_SPIN_OR_GIVE_UP_L(spins, deadline, tmo, lane, on_give_up)                                   \
+    if (spins >= kSpinMax || ((deadline) && __builtin_amdgcn_s_memrealtime() > (deadline))) {            \
+        if ((lane) == 0) report_timeout(tmo);                                                            \
+        on_give_up;                                                                                      \
+        break;                                                                                           \
+    }                                                                                                    \
     __builtin_amdgcn_s_sleep(1)
 
 // Order-preserving 64-bit key of a double (unsigned order == numeric order; NaN
@@ -541,9 +542,10 @@ template <int NT, int MAXCH, bool final, bool GRAN, class SM>
 __device__ __forceinline__ void merge_rows_block(__amdgpu_buffer_rsrc_t rows, int row0, int n, const RowGeo& geo,
                                                  double inv_lambda, SM& sm, const __amdgpu_buffer_rsrc_t* out_wt,
                                                  int out_idx, double* out_row, double* w_eps_out, unsigned tag,
-                                                 unsigned* tmo, unsigned spin_max = kSpinMax,
+                                                 unsigned* tmo, unsigned long long deadline = 0ull,
                                                  bool* failed = nullptr) {
-    // spin_max / failed: the polls' bound, and (when given) whether any poll of the workgroup gave up (uniform)
+    // deadline / failed: the polls' deadline (s_memrealtime; 0: the spin bound alone), and (when given) whether
+    // any poll of the workgroup gave up (uniform)
     constexpr bool EAGER = !GRAN && MAXCH == 1;  // one round trip per round of 32 rows
     constexpr int LB = EAGER ? 32 : 16;         // loads per batch per thread
     constexpr int RB = LB / MAXCH;              // rows per load batch
@@ -567,7 +569,7 @@ __device__ __forceinline__ void merge_rows_block(__amdgpu_buffer_rsrc_t rows, in
                 asm volatile("" ::: "memory");
                 gr = ld_gran(rows, lrow);
                 if (__all(lane >= nr || gran_ok(gr, tag))) break;
-                MPPI_SPIN_OR_GIVE_UP_L(spins, spin_max, tmo, lane, gave_up = true);
+                MPPI_SPIN_OR_GIVE_UP_L(spins, deadline, tmo, lane, gave_up = true);
             }
             rho_r = gran_val(gr);
         } else if constexpr (!EAGER) {
@@ -632,7 +634,7 @@ __device__ __forceinline__ void merge_rows_block(__amdgpu_buffer_rsrc_t rows, in
                             ok = ok && (!on || gran_ok(gv[j], tag));
                         }
                         if (__all(ok)) break;
-                        MPPI_SPIN_OR_GIVE_UP_L(spins, spin_max, tmo, lane, gave_up = true);
+                        MPPI_SPIN_OR_GIVE_UP_L(spins, deadline, tmo, lane, gave_up = true);
                     }
                     if (b0 == 0) eta_l = gran_val(ge);
 #pragma unroll
@@ -996,7 +998,8 @@ struct XDesc {
     double* row;                   // this rank's merged row, written by the launch's final merge
     unsigned* epoch;               // this rank's exchange epoch
     int rank, world, bytes;        // bytes: inbox size (2 x world rows of `stride` granules, 2 x world statuses)
-    unsigned spin_max;             // the exchange polls' bound (MPPI_EXCHANGE_SPINS at attach; default kSpinMax)
+    unsigned timeout_ticks;        // the exchange polls' bound in s_memrealtime ticks (10 ns; 0: the ~1 s spin
+                                   // bound), MPPI_EXCHANGE_TIMEOUT_US at attach
 };
 constexpr unsigned kTmoLocal = 1u, kTmoExchange = 2u;   // host timeout word: in-launch hand-off / exchange
 __device__ __forceinline__ void st_gran_sys(__amdgpu_buffer_rsrc_t r, int idx, double v, unsigned tag) {
@@ -1023,7 +1026,9 @@ __device__ __forceinline__ bool exchange_merge(const XDesc& x, const RowGeo& geo
     // the previous exchange launch's final store; kernel boundaries order it
     const unsigned tag = (unsigned)__builtin_amdgcn_readfirstlane((int)*x.epoch) + 1u;
     const int par = (int)(tag & 1u), stride = geo.stride;
-    const unsigned lim = x.spin_max ? x.spin_max : kSpinMax;
+    auto deadline = [&]() {
+        return x.timeout_ticks ? __builtin_amdgcn_s_memrealtime() + x.timeout_ticks : 0ull;
+    };
     for (int idx = threadIdx.x; idx < stride; idx += NT) {
         const double v = x.row[idx];
         for (int p = 0; p < x.world; ++p)
@@ -1031,7 +1036,8 @@ __device__ __forceinline__ bool exchange_merge(const XDesc& x, const RowGeo& geo
     }
     bool late = false;
     merge_rows_block<NT, MAXCH, true, true>(rows_rsrc(x.peer[x.rank], x.bytes), par * x.world, x.world, geo,
-                                            inv_lambda, sm, nullptr, 0, nullptr, w_eps_out, tag, nullptr, lim, &late);
+                                            inv_lambda, sm, nullptr, 0, nullptr, w_eps_out, tag, nullptr, deadline(),
+                                            &late);
     // this rank's own row is invalid if an in-launch hand-off of this launch timed out
     late = __syncthreads_or(late || (threadIdx.x == 0 && tmo &&
                                      __hip_atomic_load(tmo, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) == kTmoLocal));
@@ -1044,11 +1050,12 @@ __device__ __forceinline__ bool exchange_merge(const XDesc& x, const RowGeo& geo
         const __amdgpu_buffer_rsrc_t own = rows_rsrc(x.peer[x.rank], x.bytes);
         u32x4 g;
         bool missing = false;
+        const unsigned long long dl = deadline();
         for (unsigned spins = 0;; ++spins) {
             asm volatile("" ::: "memory");
             g = ld_gran(own, lane < x.world ? sbase + lane : kOffRange);
             if (__all(lane >= x.world || gran_ok(g, tag))) break;
-            MPPI_SPIN_OR_GIVE_UP_L(spins, lim, nullptr, lane, missing = true);
+            MPPI_SPIN_OR_GIVE_UP_L(spins, dl, nullptr, lane, missing = true);
         }
         bad = __any(lane < x.world && !(gran_ok(g, tag) && gran_val(g) > 0.0)) || missing;
     }

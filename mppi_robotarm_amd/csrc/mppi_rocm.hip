@@ -823,15 +823,15 @@ int fail(int code, const std::string& msg) {
     return code;
 }
 const char* last_error() { return g_err.c_str(); }
-unsigned exchange_spins() {
-    const char* e = getenv("MPPI_EXCHANGE_SPINS");
+unsigned exchange_timeout_ticks() {
+    const char* e = getenv("MPPI_EXCHANGE_TIMEOUT_US");
     const long v = e ? strtol(e, nullptr, 10) : 0;
-    return v > 0 ? (unsigned)v : 0u;
+    return v > 0 && v < 40000000 ? (unsigned)(v * 100) : 0u;   // s_memrealtime runs at 100 MHz
 }
 }  // namespace mppi_host
 
 namespace {
-using mppi_host::exchange_spins;
+using mppi_host::exchange_timeout_ticks;
 using mppi_host::fail;
 
 #define HIP_TRY(expr)                                                                 \
@@ -1299,7 +1299,7 @@ int mppi_exchange_attach(mppi_ctx* c, int rank, int world, const void* handles) 
     c->xd.epoch = c->d_xepoch;
     c->xd.rank = rank;
     c->xd.world = world;
-    c->xd.spin_max = exchange_spins();
+    c->xd.timeout_ticks = exchange_timeout_ticks();
     return MPPI_OK;
 }
 

@@ -137,8 +137,8 @@ def _chain_step(pg, exchange, sampled=True):
     return out
 
 
-LATE_SPINS = "50000"   # MPPI_EXCHANGE_SPINS for the late-rank scenarios: a poll bound of ~50-100 ms
-LATE_TICK, LATE_SLEEP_S = 2, 0.4
+LATE_TIMEOUT_US = "30000"   # MPPI_EXCHANGE_TIMEOUT_US of the late-rank scenarios: a 30 ms poll bound
+LATE_TICK, LATE_SLEEP_S = 2, 0.5
 
 
 def _late_rank_ticks(pg, exchange):
@@ -150,7 +150,7 @@ def _late_rank_ticks(pg, exchange):
     from mppi_robotarm_amd.controller import MPPIControllerForPathTracking
     g, paths = load_loop("k64_t20"), load_paths()
     rank = pg.rank() if pg is not None else 0
-    os.environ["MPPI_EXCHANGE_SPINS"] = LATE_SPINS
+    os.environ["MPPI_EXCHANGE_TIMEOUT_US"] = LATE_TIMEOUT_US
     try:
         c = MPPIControllerForPathTracking(delta_t=0.006, ref_path=paths["xydq_circle"], horizon_step_T=DEV_T,
                                           number_of_samples_K=DEV_K, verbose=False, noise="device", seed=DEV_SEED,
@@ -166,7 +166,7 @@ def _late_rank_ticks(pg, exchange):
         out = dict(u_seq=np.array(useq), prev=np.array(idx), modes=np.array(modes), xmode=str(c._xmode))
         c.close()
     finally:
-        del os.environ["MPPI_EXCHANGE_SPINS"]
+        del os.environ["MPPI_EXCHANGE_TIMEOUT_US"]
     return out
 
 
@@ -176,7 +176,7 @@ def _late_rank_chain(pg, exchange):
     from mppi_robotarm_amd.chain import ChainMPPIController, ChainParams
     g, paths = load_step("runpy_k100_t30"), load_paths()
     rank = pg.rank() if pg is not None else 0
-    os.environ["MPPI_EXCHANGE_SPINS"] = LATE_SPINS
+    os.environ["MPPI_EXCHANGE_TIMEOUT_US"] = LATE_TIMEOUT_US
     try:
         c = ChainMPPIController(float(g["delta_t"]), paths[str(g["path"])], int(g["T"]), 4096,
                                 float(g["param_exploration"]), float(g["param_lambda"]), float(g["param_alpha"]),
@@ -194,7 +194,7 @@ def _late_rank_chain(pg, exchange):
         out = dict(u_seq=np.array(useq), modes=np.array(modes), xmode=str(c._xmode))
         c.close()
     finally:
-        del os.environ["MPPI_EXCHANGE_SPINS"]
+        del os.environ["MPPI_EXCHANGE_TIMEOUT_US"]
     return out
 
 
