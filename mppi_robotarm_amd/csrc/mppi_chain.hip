@@ -772,7 +772,8 @@ __device__ __forceinline__ double chain_horizon_lps4(const ChainConst& c, const 
 // come from a 2-deep register ring like the noise rows, and the window row of
 // step t is read from LDS right after its search but consumed only after step
 // t + 1's dynamics (deferred cost; the stage cost goes into S in step order).
-// The stage cost is lane 0's alone (own), so it needs no broadcast.
+// The stage cost's four terms go to two lanes, two apiece (lane 0 has both joint
+// rates of the cost in its own pair), so it needs no broadcast.
 template <int N>
 __device__ __forceinline__ double chain_horizon_q4(const ChainConst& c, const ChainStep* st, const float* dyn,
                                                    const float* noise, int k, float exf, float4* s_ua4,
@@ -789,19 +790,20 @@ __device__ __forceinline__ double chain_horizon_q4(const ChainConst& c, const Ch
     sr.load(st->key, st->ctr, sub);
     const int a0 = 2 * sub, a1 = 2 * sub + 1;   // this lane's links
     const float m1 = sub >= 1 ? 1.f : 0.f, u1 = sub <= 2 ? 1.f : 0.f;
-    const float own = sub == 0 ? 1.f : 0.f;
+    // the stage cost's four terms split over two lanes, two apiece: lane 0 the joint-rate terms (its own
+    // theta_dot pair gives q_dot_1, q_dot_2), lane 1 the position terms; lanes 2, 3 weigh theirs by 0
+    const bool l0 = sub == 0;
     const f32x2 pad = {a0 < N ? 1.f : 0.f, a1 < N ? 1.f : 0.f};
     const f32x2 l2 = {dyn[kOffL + a0], dyn[kOffL + a1]}, nu2 = {dyn[kOffNu + a0], dyn[kOffNu + a1]};
     const f32x2 damp2 = {dyn[kOffDamp + a0], dyn[kOffDamp + a1]}, fk2 = {dyn[kOffFk + a0], dyn[kOffFk + a1]};
     const float dt = dyn[kOffDt], g = dyn[kOffG];
     constexpr float kRev = 0.15915494309189535f;   // 1 / (2 pi)
     const float dtr = dt * kRev;
-    float sw[4], tw[4];
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-        sw[i] = dyn[kOffSw + i];
-        tw[i] = dyn[kOffTw + i];
-    }
+    const f32x2 sw2 = l0 ? f32x2{dyn[kOffSw + 2], dyn[kOffSw + 3]}
+                         : (sub == 1 ? f32x2{dyn[kOffSw], dyn[kOffSw + 1]} : f32x2{0.f, 0.f});
+    const f32x2 tw2 = l0 ? f32x2{dyn[kOffTw + 2], dyn[kOffTw + 3]}
+                         : (sub == 1 ? f32x2{dyn[kOffTw], dyn[kOffTw + 1]} : f32x2{0.f, 0.f});
+    const float2* const s_win2 = reinterpret_cast<const float2*>(s_win) + (l0 ? 1 : 0);   // (rdq1, rdq2) / (rx, ry)
     f32x2 corr[N];   // as chain_horizon_lps4
     {
         const float dc0 = dyn[kOffDd + a0] - l2.x * nu2.x, dc1 = dyn[kOffDd + a1] - l2.y * nu2.y;
@@ -840,12 +842,11 @@ __device__ __forceinline__ double chain_horizon_q4(const ChainConst& c, const Ch
     for (int j = 0; j < kCPF; ++j) uar[j] = s_ua4[j * 4 + sub];
 
     double S = 0.0;
-    float S4 = 0.f;
+    f32x2 S2 = {0.f, 0.f};   // this lane's two stage-cost terms
     f32x2 G2 = {0.f, 0.f};   // this lane's (gamma u^T Sigma^-1) v terms
-    // the pending stage cost (the previous step's): position, lane 0's joint rates 1 and 2, its window row;
+    // the pending stage cost (the previous step's): this lane's two values and their window-row entries;
     // all zero before the first step, so the first "pending" cost is exactly 0
-    float ppx = 0.f, ppy = 0.f, pd1 = 0.f, pd2 = 0.f;
-    float4 prw = make_float4(0.f, 0.f, 0.f, 0.f);
+    f32x2 pAB = {0.f, 0.f}, prw = {0.f, 0.f};
     auto step = [&](int t, auto slot_c) {
         constexpr int slot = decltype(slot_c)::value;
         // the slot's values are taken here (volatile asm keeps its place against the previous step's
@@ -886,7 +887,9 @@ __device__ __forceinline__ double chain_horizon_q4(const ChainConst& c, const Ch
             constexpr int j = decltype(j_c)::value;
             inv[j] = __builtin_amdgcn_rsqf(qbc<j / 2>(elem<j>(col[j])));
             col[j] = col[j] * splat(inv[j]);
-            y[j] = qbc<j / 2>(elem<j>(r) * inv[j]);
+            // inv[j] is the same in every lane (the rsq of one broadcast value), so broadcasting r_j and
+            // scaling after gives the owner's product bit for bit, and the broadcast folds into the multiply
+            y[j] = qbc<j / 2>(elem<j>(r)) * inv[j];
             r = __builtin_elementwise_fma(splat(-y[j]), col[j], r);
             unroll_seq([&](auto k_c) {
                 constexpr int kk = decltype(k_c)::value;
@@ -915,22 +918,25 @@ __device__ __forceinline__ double chain_horizon_q4(const ChainConst& c, const Ch
         // row is taken only now (the asm needs TH, this step's last dynamics result): left free, the
         // scheduler pulls the cost up next to the lookup and waits on the LDS round trip there
         {
-            f32x4 rw = {prw.x, prw.y, prw.z, prw.w};
+            f32x2 rw = prw;
             asm volatile("" : "+v"(rw) : "v"(TH));
-            S4 = fmaf(own, weighted_sq(ppx - rw.x, ppy - rw.y, pd1 - rw.z, pd2 - rw.w, sw), S4);
+            const f32x2 e = pAB - rw;
+            S2 = __builtin_elementwise_fma(sw2, e * e, S2);
         }
         // ---- end effector and nearest waypoint of this step; its row is read now, used next step
         const f32x2 fx = fk2 * C, fy = fk2 * Sn;
-        ppx = q_sum(fx.x + fx.y);
-        ppy = q_sum(fy.x + fy.y);
-        pd1 = THD.x;            // lane 0: q_dot_1 = theta_dot_1
-        pd2 = THD.y - THD.x;    //         q_dot_2 = theta_dot_2 - theta_dot_1
-        const unsigned j = sr.nearest(ppx, ppy);
+        float px = q_sum(fx.x + fx.y), py = q_sum(fy.x + fy.y);
+        asm("" : "+v"(px), "+v"(py));   // opaque: the SLP vectoriser would pair the two sums into v_pk_add
+                                        // with their DPP moves unfolded
+        // lane 0: q_dot_1 = theta_dot_1, q_dot_2 = theta_dot_2 - theta_dot_1; the others: the position
+        pAB = l0 ? f32x2{THD.x, THD.y - THD.x} : f32x2{px, py};
+        const unsigned j = sr.nearest(px, py);
         if (slots && sub == 0) slots[(size_t)k * T + t] = (int)j;   // debug instances only
-        prw = s_win[j];
+        const float2 r2 = s_win2[2 * j];
+        prw = f32x2{r2.x, r2.y};
         if constexpr (slot == kCPF - 1) {
-            S += (double)(S4 + (G2.x + G2.y));
-            S4 = 0.f;
+            S += (double)((S2.x + S2.y) + (G2.x + G2.y));
+            S2 = f32x2{0.f, 0.f};
             G2 = f32x2{0.f, 0.f};
         }
     };
@@ -942,10 +948,11 @@ __device__ __forceinline__ double chain_horizon_q4(const ChainConst& c, const Ch
     }
     if (t < T) step(t, std::integral_constant<int, 0>{});
     // the last step's stage cost and the terminal cost on the same state (control.py:106-109)
-    const float ex = ppx - prw.x, ey = ppy - prw.y, e1 = pd1 - prw.z, e2 = pd2 - prw.w;
-    S4 = fmaf(own, weighted_sq(ex, ey, e1, e2, sw), S4);
-    S += (double)(S4 + (G2.x + G2.y));
-    S += (double)(own * weighted_sq(ex, ey, e1, e2, tw));
+    const f32x2 e = pAB - prw, ee = e * e;
+    S2 = __builtin_elementwise_fma(sw2, ee, S2);
+    S += (double)((S2.x + S2.y) + (G2.x + G2.y));
+    const f32x2 te = tw2 * ee;
+    S += (double)(te.x + te.y);
     return q_sum_f64(S);
 }
 
@@ -1097,6 +1104,14 @@ __global__ __launch_bounds__(kCT) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
     if (S_out && owner) S_out[k] = S;
 
     // ---- workgroup partial: rho_b, eta_b, N_b (control.py:112-118 over this block)
+    // With a quad per sample (one workgroup per CU, every workgroup finishing at once) the running minimum
+    // (below) is read before the block minimum, so its round trip runs under it, and the workgroup's own
+    // atomic goes out after the last barrier, unwaited; with one lane per sample (two workgroups per CU,
+    // finishing spread out) the atomic's fresher return skips more gathers (measured: +1.7 % with the early
+    // read at config 5, -1.7 % at its shard)
+    constexpr bool kEarlyRun = LPS == 4;
+    unsigned long long run0 = ~0ull;
+    if (kEarlyRun && tid == 0) run0 = __hip_atomic_load(runmin, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     const double rho_b = block_min_f64<kCT>(owner ? S : INFINITY, sm);
     // fp64, like the reference's weights; a wave whose samples all lie below the
     // floor (exp(-44.4) = 2^-64: the usual case, S spread >> lambda) skips the exp
@@ -1110,16 +1125,21 @@ __global__ __launch_bounds__(kCT) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
         s_cnt[wave] = __popcll(bal);
         s_redd[wave] = esum;
     }
-    // The running minimum of the workgroups' rho_b so far (one 64-bit atomic min
-    // on an order-preserving key; reset by the final merger).  The final rho is at
-    // most this value, so a workgroup whose rho_b is 2^-64 or more below it in
-    // weight can carry no weight in any merge: it publishes rho_b = +inf and skips
-    // the gather of its weighted samples' noise — each of those is T n scattered
-    // 4-B reads, one cache line apiece (1.14x the algorithmic bytes at config 5).
+    // The running minimum of the workgroups' rho_b (one 64-bit atomic min per
+    // workgroup on an order-preserving key; reset by the final merger).  The final
+    // rho is at most any minimum over published rho_b, so a workgroup whose rho_b
+    // is 2^-64 or more below it in weight can carry no weight in any merge: it
+    // publishes rho_b = +inf and skips the gather of its weighted samples' noise —
+    // each of those is T n scattered 4-B reads, one cache line apiece (1.14x the
+    // algorithmic bytes at config 5).
     if (tid == 0) {
         const unsigned long long key = ord_key(rho_b);
-        const unsigned long long old = __hip_atomic_fetch_min(runmin, key, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        s_run = ord_val(old < key ? old : key);
+        if constexpr (kEarlyRun) {
+            s_run = ord_val(min(run0, key));
+        } else {
+            const unsigned long long old = __hip_atomic_fetch_min(runmin, key, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            s_run = ord_val(old < key ? old : key);
+        }
     }
     __syncthreads();
     const bool skip = exp((s_run - rho_b) * c.inv_lambda) < kMergeFloor;   // uniform
@@ -1137,6 +1157,9 @@ __global__ __launch_bounds__(kCT) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
         s_e[pos] = wgt;
     }
     __syncthreads();
+    // past the barriers (a barrier's fence would wait for the atomic to complete): fire and forget; the
+    // gather's loads, issued after it, return after it anyway
+    if (kEarlyRun && tid == 0) __hip_atomic_fetch_min(runmin, ord_key(rho_b), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     const int nval = T * N;
     const RowGeo geo(nval);
     const int stride = geo.stride;
@@ -1239,10 +1262,13 @@ __global__ __launch_bounds__(kCT) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
     }
     STAMP(11, NOW());
     STAMP(6, (unsigned long long)sm.nrel);
-    const bool xok = (flags & MPPI_FLAG_EXCHANGE)
-                         ? exchange_merge<kCT, kCMaxCh>(xd, geo, c.inv_lambda, sm, w_eps_out, tmo) : true;
+    // with the exchange, the update is computed while the ranks' statuses travel: it lands in the ping-pong
+    // block the host makes current only after a good verdict (on failure the host keeps its block)
+    const unsigned xtag = (flags & MPPI_FLAG_EXCHANGE)
+                              ? exchange_send_merge<kCT, kCMaxCh>(xd, geo, c.inv_lambda, sm, w_eps_out, tmo) : 0u;
     if (tid == 0 && w_eps_out) w_eps_out[nval] = sm.eta;   // the weights' spread (mppi_chain_last_eta)
-    if ((flags & MPPI_FLAG_FUSED_UPDATE) && xok) chain_update_block<N>(nxt, c, sm, u_cur);   // failed: no update
+    if (flags & MPPI_FLAG_FUSED_UPDATE) chain_update_block<N>(nxt, c, sm, u_cur);
+    if (flags & MPPI_FLAG_EXCHANGE) exchange_verdict<kCT>(xd, geo, xtag, tmo);
     STAMP(7, NOW());
 }
 

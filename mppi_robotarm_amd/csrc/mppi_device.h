@@ -1020,37 +1020,48 @@ __device__ __forceinline__ void st_gran_sys(__amdgpu_buffer_rsrc_t r, int idx, d
 // (the host raises MPPI_E_EXCHANGE and keeps the nominal: no update is applied)
 // and the caller runs the step again over the collective fallback.  The epoch
 // advances either way, so the ranks stay in step for the next exchange.
+//
+// Two halves, so the caller can compute the fused update while the statuses
+// travel: exchange_send_merge (rows out, merge, this rank's status out; returns
+// the step's tag) and exchange_verdict (the statuses in).  The update written in
+// between goes only to the ping-pong block the host has not yet made current and
+// to outputs the host reads after the verdict; on failure the host keeps the
+// block it had and ignores them.
 template <int NT, int MAXCH, class SM>
-__device__ __forceinline__ bool exchange_merge(const XDesc& x, const RowGeo& geo, double inv_lambda, SM& sm,
-                                               double* w_eps_out, unsigned* tmo) {
+__device__ __forceinline__ unsigned exchange_send_merge(const XDesc& x, const RowGeo& geo, double inv_lambda, SM& sm,
+                                                        double* w_eps_out, unsigned* tmo) {
     // the previous exchange launch's final store; kernel boundaries order it
     const unsigned tag = (unsigned)__builtin_amdgcn_readfirstlane((int)*x.epoch) + 1u;
     const int par = (int)(tag & 1u), stride = geo.stride;
-    auto deadline = [&]() {
-        return x.timeout_ticks ? __builtin_amdgcn_s_memrealtime() + x.timeout_ticks : 0ull;
-    };
     for (int idx = threadIdx.x; idx < stride; idx += NT) {
         const double v = x.row[idx];
         for (int p = 0; p < x.world; ++p)
             st_gran_sys(rows_rsrc(x.peer[p], x.bytes), (par * x.world + x.rank) * stride + idx, v, tag);
     }
     bool late = false;
+    const unsigned long long dl = x.timeout_ticks ? __builtin_amdgcn_s_memrealtime() + x.timeout_ticks : 0ull;
     merge_rows_block<NT, MAXCH, true, true>(rows_rsrc(x.peer[x.rank], x.bytes), par * x.world, x.world, geo,
-                                            inv_lambda, sm, nullptr, 0, nullptr, w_eps_out, tag, nullptr, deadline(),
-                                            &late);
+                                            inv_lambda, sm, nullptr, 0, nullptr, w_eps_out, tag, nullptr, dl, &late);
     // this rank's own row is invalid if an in-launch hand-off of this launch timed out
     late = __syncthreads_or(late || (threadIdx.x == 0 && tmo &&
                                      __hip_atomic_load(tmo, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) == kTmoLocal));
-    // status round
     const int sbase = 2 * x.world * stride + par * x.world;   // status granules follow the rows: [parity][rank]
+    if ((int)threadIdx.x < x.world)
+        st_gran_sys(rows_rsrc(x.peer[threadIdx.x], x.bytes), sbase + x.rank, late ? -1.0 : 1.0, tag);
+    return tag;
+}
+
+template <int NT>
+__device__ __forceinline__ bool exchange_verdict(const XDesc& x, const RowGeo& geo, unsigned tag, unsigned* tmo) {
+    const int par = (int)(tag & 1u);
+    const int sbase = 2 * x.world * geo.stride + par * x.world;
     const int tid = threadIdx.x, lane = tid & 63;
-    if (tid < x.world) st_gran_sys(rows_rsrc(x.peer[tid], x.bytes), sbase + x.rank, late ? -1.0 : 1.0, tag);
     bool bad = false;
     if (tid < 64) {   // wave 0 polls every rank's status (world <= 64)
         const __amdgpu_buffer_rsrc_t own = rows_rsrc(x.peer[x.rank], x.bytes);
         u32x4 g;
         bool missing = false;
-        const unsigned long long dl = deadline();
+        const unsigned long long dl = x.timeout_ticks ? __builtin_amdgcn_s_memrealtime() + x.timeout_ticks : 0ull;
         for (unsigned spins = 0;; ++spins) {
             asm volatile("" ::: "memory");
             g = ld_gran(own, lane < x.world ? sbase + lane : kOffRange);

@@ -241,7 +241,7 @@ struct HostOut {
 // host outputs are requested).
 template <int NT>
 __device__ void nominal_update_block(DevStep* nxt, const KConst& c, Scratch& sm, double u_src, double u_first,
-                                     float* upd, HostOut ho) {
+                                     float* upd, HostOut ho, bool publish = true) {
     const int tid = threadIdx.x;
     const int T = c.T;
     if (tid < ((2 * T + 63) & ~63)) {   // whole waves: the DPP pairs stay complete
@@ -269,6 +269,7 @@ __device__ void nominal_update_block(DevStep* nxt, const KConst& c, Scratch& sm,
     }
     if (ho.p) {
         __threadfence_system();   // this thread's host stores are out before the barrier
+        if (!publish) return;     // the caller publishes (after the exchange's verdict)
         __syncthreads();
         if (tid == 0) __hip_atomic_store(reinterpret_cast<unsigned*>(ho.p), ho.seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
     }
@@ -607,16 +608,17 @@ __global__ __launch_bounds__(NT) void rollout_kernel(
     }
     STAMP(11, NOW());
     STAMP(6, (unsigned long long)sm.nrel);
-    const bool xok = (flags & MPPI_FLAG_EXCHANGE) ? exchange_merge<NT, 1>(xd, geo, c.inv_lambda, sm, w_eps_out, tmo)
-                                                  : true;
-    if (flags & MPPI_FLAG_FUSED_UPDATE) {
-        if (xok) {
-            nominal_update_block<NT>(nxt, c, sm, u_cur, u_first, upd, ho);
-        } else if (ho.p) {   // the exchange failed: no update; the host's wait ends and reads the timeout word
-            __syncthreads();
-            if (threadIdx.x == 0)
-                __hip_atomic_store(reinterpret_cast<unsigned*>(ho.p), ho.seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
-        }
+    if (flags & MPPI_FLAG_EXCHANGE) {
+        // the update is computed while the ranks' statuses travel (exchange_send_merge / exchange_verdict):
+        // it lands in the ping-pong block and outputs the host takes only after a good verdict; on a failed
+        // exchange the host keeps its block and ignores them (check_timeout), so no rank applies the update
+        const unsigned xtag = exchange_send_merge<NT, 1>(xd, geo, c.inv_lambda, sm, w_eps_out, tmo);
+        if (flags & MPPI_FLAG_FUSED_UPDATE) nominal_update_block<NT>(nxt, c, sm, u_cur, u_first, upd, ho, false);
+        exchange_verdict<NT>(xd, geo, xtag, tmo);   // a barrier: every thread's host stores are out
+        if ((flags & MPPI_FLAG_FUSED_UPDATE) && ho.p && threadIdx.x == 0)   // the host's wait ends, then reads tmo
+            __hip_atomic_store(reinterpret_cast<unsigned*>(ho.p), ho.seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+    } else if (flags & MPPI_FLAG_FUSED_UPDATE) {
+        nominal_update_block<NT>(nxt, c, sm, u_cur, u_first, upd, ho);
     }
     STAMP(7, NOW());
 }

@@ -10,7 +10,9 @@
 //          block from pinned host memory into device memory and releases the
 //          other workgroups through a device word; the call writes the block,
 //          then "go", and spins on the same published word.
-//   armed-all: every workgroup polls the host word itself (256 PCIe pollers).
+//   armed-all: every workgroup polls the host word itself (256 PCIe pollers); a
+//          poller waits for go >= its call, since the host may already have
+//          moved go on for the next call when a slow poller looks.
 //
 // Between two calls the host "works" for GAP us (the caller's plant step).
 //   hipcc --offload-arch=gfx950 -O2 -o tools/_build/armed_launch tools/armed_launch.hip
@@ -43,7 +45,7 @@ static double pct(std::vector<double> v, double q) {
     } while (0)
 
 struct alignas(16) Block { unsigned char b[1024]; };
-constexpr unsigned kSpin = 1u << 22;   // bound on every poll (~seconds): the grid always drains
+constexpr unsigned long long kPollTicks = 200000000ull;   // bound on every poll: 2 s of s_memrealtime (100 MHz)
 
 __device__ __forceinline__ unsigned ld_sys(const unsigned* p) {
     return __hip_atomic_load(p, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM);
@@ -61,9 +63,10 @@ __global__ void k_armed(const unsigned* go, const Block* hblk, Block* dblk, unsi
     __shared__ unsigned ok;
     if (all_poll || blockIdx.x == 0) {
         if (threadIdx.x == 0) {
-            unsigned s = 0;
-            while (ld_sys(go) != seq && ++s < kSpin) __builtin_amdgcn_s_sleep(1);
-            ok = s < kSpin;
+            const unsigned long long end = __builtin_amdgcn_s_memrealtime() + kPollTicks;
+            bool in_time = true;
+            while ((int)(ld_sys(go) - seq) < 0 && (in_time = __builtin_amdgcn_s_memrealtime() < end)) __builtin_amdgcn_s_sleep(1);
+            ok = in_time;
         }
         __syncthreads();
         if (!all_poll) {
@@ -76,15 +79,29 @@ __global__ void k_armed(const unsigned* go, const Block* hblk, Block* dblk, unsi
         }
     } else {
         if (threadIdx.x == 0) {
-            unsigned s = 0;
-            while (__hip_atomic_load(dflag, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT) != seq && ++s < kSpin)
+            const unsigned long long end = __builtin_amdgcn_s_memrealtime() + kPollTicks;
+            bool in_time = true;
+            while (__hip_atomic_load(dflag, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT) != seq &&
+                   (in_time = __builtin_amdgcn_s_memrealtime() < end))
                 __builtin_amdgcn_s_sleep(1);
-            ok = s < kSpin;
+            ok = in_time;
         }
         __syncthreads();
         if (threadIdx.x == 0 && ok && dblk->b[5] == 0xA5) sink[blockIdx.x] = 1;
     }
     if (blockIdx.x == 0 && threadIdx.x == 0) __hip_atomic_store(out, seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
+// bounded host spin on the published word: a grid that never publishes ends the run with a message
+static bool wait_pub(const unsigned* out, unsigned seq, const char* phase, int i) {
+    const auto t0 = clk::now();
+    while (__atomic_load_n(out, __ATOMIC_ACQUIRE) != seq) {
+        if (us(t0, clk::now()) > 2e6) {
+            std::printf("%s: call %d never published (seq %u, word %u)\n", phase, i, seq, *out);
+            return false;
+        }
+    }
+    return true;
 }
 
 static void host_work(double gap_us) {
@@ -94,6 +111,7 @@ static void host_work(double gap_us) {
 }
 
 int main(int argc, char** argv) {
+    std::setvbuf(stdout, nullptr, _IONBF, 0);
     const int iters = argc > 1 ? atoi(argv[1]) : 2000;
     const double gap = argc > 2 ? atof(argv[2]) : 10.0;
     CHECK(hipSetDevice(0));
@@ -122,7 +140,9 @@ int main(int argc, char** argv) {
         blk.b[0] = (unsigned char)seq;
         hipLaunchKernelGGL(k_plain, dim3(256), dim3(256), 0, s, blk, out, seq, sink);
         const auto t1 = clk::now();
-        while (__atomic_load_n(out, __ATOMIC_ACQUIRE) != seq) {
+        if (!wait_pub(out, seq, "plain", i)) {
+            (void)hipStreamSynchronize(s);
+            return 2;
         }
         const auto t2 = clk::now();
         if (i >= 100) {
@@ -143,7 +163,9 @@ int main(int argc, char** argv) {
             const auto t0 = clk::now();
             hblk->b[0] = (unsigned char)seq;     // the step block, then go
             __atomic_store_n(go, seq, __ATOMIC_RELEASE);
-            while (__atomic_load_n(out, __ATOMIC_ACQUIRE) != seq) {
+            if (!wait_pub(out, seq, all ? "armed-all" : "armed", i)) {
+                (void)hipStreamSynchronize(s);   // the grid's polls are bounded: let it drain before exiting
+                return 2;
             }
             const auto t2 = clk::now();
             ++seq;   // arm the next call at the end of this one

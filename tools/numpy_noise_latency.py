@@ -40,6 +40,11 @@ for seed in (0, 1, 2):
     assert same
 print(f"np.random.multivariate_normal      {med(lambda: np.random.multivariate_normal(np.zeros(2), S, (K, T))):8.2f} ms")
 print(f"hostrng.multivariate_normal        {med(lambda: hostrng.multivariate_normal(np.zeros(2), S, (K, T))):8.2f} ms")
+zbuf = torch.empty(K * T * 2, dtype=torch.float64).pin_memory().numpy()
+print(f"hostrng.legacy_standard_normal     {med(lambda: hostrng.legacy_standard_normal(K * T * 2, out=zbuf)):8.2f} ms"
+      "  (the drop-in's draw: standard normals into a page-locked buffer)")
+print(f"hostrng.multivariate_normal_std    {med(lambda: hostrng.multivariate_normal_std(np.zeros(2), S, (K, T), zbuf)):8.2f} ms"
+      "  (+ NumPy's svd / checks of Sigma)")
 torch.cuda.set_device(0)
 path = np.load(os.path.join(ROOT, "tests", "golden", "paths.npz"))["xydq_circle"][:, :4]
 kw = runpy_config()
