@@ -322,6 +322,11 @@ def default_backend(world: int) -> str:
     return "nccl" if torch.cuda.device_count() >= world else "gloo"
 
 
+def progress(msg: str) -> None:
+    """A phase line on stderr (a long profiled run then shows it is alive); stdout keeps only the JSON line."""
+    print(f"bench [rank {os.environ.get('RANK', '0')}]: {msg}", file=sys.stderr, flush=True)
+
+
 def main():
     args = parse()
     if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
@@ -382,6 +387,7 @@ def main():
                             device=local_rank, lanes_per_sample=args.lps)
         x0 = X0_RUNPY.copy()
         u = np.array([[10.0, -2.0]] * T)
+    progress(f"{args.workload} K={K} T={T}: engine ready")
     eng.set_step_inputs(x0, window, u)
     noise = [eng.philox_noise(1234, i) for i in range(args.nbuf)]
     partial = eng.new_partial()
@@ -461,6 +467,7 @@ def main():
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
+    progress(f"settled and warmed up (exchange: {xmode}); timing {steps} steps")
     nev = steps // chunk
     ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(nev)]
     whole = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
@@ -563,11 +570,14 @@ def main():
             "valu_roofline": valu,
         }
         if world == 1 and not c5:
+            progress("device loop timed; drop-in latency legs")
             med, p90, b2b = dropin_latency(K, T, local_rank)
             out["control_step_latency_ms"] = med
             out["control_step_latency_p90_ms"] = p90
             out["control_step_latency_back_to_back_ms"] = b2b
+            progress("sampled-trajectories leg")
             out["control_step_latency_sampled_trajs_ms"] = sampled_latency(K, T, local_rank)
+            progress("NumPy-noise leg")
             out["control_step_latency_numpy_noise_ms"] = numpy_noise_latency(K, T, local_rank)
             out["control_step_latency_def"] = (
                 "median wall time of MPPIControllerForPathTracking.calc_control_input (drop-in, noise='device') "
@@ -592,6 +602,7 @@ def main():
                 "the launch (each call then also waits for the previous draw). 40 calls after 10 uncounted. "
                 "ms_per_step is the device-resident loop")
         if world == 1 and args.cpu_seconds > 0:
+            progress("CPU baseline")
             out["cpu_baseline"] = (cpu_baseline_c5(args, window, x0, u, K, T) if c5
                                    else cpu_baseline(args, window, x0, u))
         print(json.dumps(out))
