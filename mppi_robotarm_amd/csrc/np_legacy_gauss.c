@@ -30,6 +30,8 @@
 // NumPy's own calls.
 #include <math.h>
 #include <pthread.h>
+#include <stdio.h>
+#include <time.h>
 #include <stdint.h>
 #include <stdlib.h>
 #include <string.h>
@@ -475,7 +477,7 @@ static inline void attempt(const uint32_t* blocks, int64_t base, int64_t i, doub
     *r2 = *x1 * *x1 + *x2 * *x2;
 }
 
-static void* count_pass(void* p) {
+MT_CLONES static void* count_pass(void* p) {
     Work* w = (Work*)p;
     int64_t n = 0;
     for (int64_t i = w->a0; i < w->a1; ++i) {
@@ -510,8 +512,17 @@ static void* write_pass(void* p) {
 // key[624] / *pos: the MT19937 state (NumPy's get_state()[1:3]); *has_gauss / *gauss: the cached Gaussian
 // (get_state()[3:5]).  Writes n standard normals exactly as n calls of legacy_gauss would, and leaves the
 // state those calls would leave.  Returns 0, or -1 on bad arguments / allocation failure (state untouched).
+static double now_ms(void) {
+    struct timespec ts;
+    clock_gettime(CLOCK_MONOTONIC, &ts);
+    return ts.tv_sec * 1e3 + ts.tv_nsec * 1e-6;
+}
+
 static int legacy_gauss_locked(uint32_t* key, int* pos, int* has_gauss, double* gauss, double* out, int64_t n,
                                int nthreads) {
+    static int timing = -1;   // MPPI_NP_TIMING=1: the phases' wall times on stderr (diagnostics)
+    if (timing < 0) timing = getenv("MPPI_NP_TIMING") != NULL;
+    const double t_start = timing ? now_ms() : 0.0;
     if (!key || !pos || !has_gauss || !gauss || (n > 0 && !out) || n < 0 || *pos < 0 || *pos > MT_N) return -1;
     if (nthreads < 1) nthreads = 1;
     if (nthreads > 64) nthreads = 64;
@@ -538,7 +549,9 @@ static int legacy_gauss_locked(uint32_t* key, int* pos, int* has_gauss, double* 
         }
         uint32_t* blocks = g_blocks;
         memcpy(blocks, key, MT_N * sizeof(uint32_t));
+        const double t_tw = timing ? now_ms() : 0.0;
         twist_blocks(blocks, nblk, nthreads);
+        const double t_cnt = timing ? now_ms() : 0.0;
         Work wk[64];
         const int nt = (int)(A < nthreads * 4096 ? 1 : nthreads);
         for (int t = 0; t < nt; ++t) {
@@ -562,7 +575,11 @@ static int legacy_gauss_locked(uint32_t* key, int* pos, int* has_gauss, double* 
             A = A + A / 2;
             continue;
         }
+        const double t_wr = timing ? now_ms() : 0.0;
         pool_run(write_pass, wk, sizeof(Work), nt);
+        if (timing)
+            fprintf(stderr, "np_legacy_gauss n=%lld threads=%d: setup %.3f twist %.3f count %.3f write %.3f ms\n",
+                    (long long)n, nt, t_tw - t_start, t_cnt - t_tw, t_wr - t_cnt, now_ms() - t_wr);
         int64_t last = -1;
         double fx1 = 0.0;
         for (int t = 0; t < nt; ++t)
