@@ -777,7 +777,7 @@ __device__ __forceinline__ double chain_horizon_lps4(const ChainConst& c, const 
 template <int N>
 __device__ __forceinline__ double chain_horizon_q4(const ChainConst& c, const ChainStep* st, const float* dyn,
                                                    const float* noise, int k, float exf, float4* s_ua4,
-                                                   float4* s_win, int* slots) {
+                                                   float4* s_win, float4* s_lcs, int* slots) {
     static_assert(N <= 8, "four link pairs");
     const int tid = threadIdx.x, sub = tid & 3, K = c.K_local, T = c.T;
     if (tid < kSlots) s_win[tid] = st->win[tid];
@@ -790,6 +790,11 @@ __device__ __forceinline__ double chain_horizon_q4(const ChainConst& c, const Ch
     sr.load(st->key, st->ctr, sub);
     const int a0 = 2 * sub, a1 = 2 * sub + 1;   // this lane's links
     const float m1 = sub >= 1 ? 1.f : 0.f, u1 = sub <= 2 ? 1.f : 0.f;
+#ifdef MPPI_Q4_MASKSEL
+    float oh[4];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) oh[q] = sub == q ? 1.f : 0.f;
+#endif
     // the stage cost's four terms split over two lanes, two apiece: lane 0 the joint-rate terms (its own
     // theta_dot pair gives q_dot_1, q_dot_2), lane 1 the position terms; lanes 2, 3 weigh theirs by 0
     const bool l0 = sub == 0;
@@ -829,10 +834,22 @@ __device__ __forceinline__ double chain_horizon_q4(const ChainConst& c, const Ch
     };
     angles();
     const unsigned o0 = (unsigned)(min(a0, N - 1) * K + k) * 4u, o1 = (unsigned)(min(a1, N - 1) * K + k) * 4u;
+#ifdef MPPI_Q4_NOISEBUF
+    // the row's byte offset in the buffer instruction's scalar soffset (one s_min and one s_mul per row), the
+    // lane's offset in its VGPR: no 64-bit address arithmetic per step (the host keeps T N K 4 below 2^31)
+    const __amdgpu_buffer_rsrc_t nrs = rows_rsrc(noise, T * N * K * 4);
+    const int rowb = N * K * 4;
+    auto nrow = [&](int t) {
+        const int so = min(t, T - 1) * rowb;
+        return f32x2{__builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(nrs, (int)o0, so, 0)),
+                     __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(nrs, (int)o1, so, 0))};
+    };
+#else
     auto nrow = [&](int t) {
         const char* row = (const char*)(noise + (size_t)min(t, T - 1) * N * K);
         return f32x2{*(const float*)(row + o0), *(const float*)(row + o1)};
     };
+#endif
     f32x2 ring[kCPF];
 #pragma unroll
     for (int j = 0; j < kCPF; ++j) ring[j] = nrow(j);
@@ -847,8 +864,29 @@ __device__ __forceinline__ double chain_horizon_q4(const ChainConst& c, const Ch
     // the pending stage cost (the previous step's): this lane's two values and their window-row entries;
     // all zero before the first step, so the first "pending" cost is exactly 0
     f32x2 pAB = {0.f, 0.f}, prw = {0.f, 0.f};
-    auto step = [&](int t, auto slot_c) {
+#ifdef MPPI_Q4_LATESEARCH
+    // the current state's end effector, window search and row read placed inside the step's factorization
+    // (after column MPPI_Q4_LATESEARCH), where the pivot chain leaves issue slots idle; the cost is taken at
+    // the end of the same step.  Step 0's state carries no cost (control.py:95-109): step 0 has no search,
+    // and the last state's search runs after the loop.
+    // The state's cost is taken one step after its search (the row read has a whole step to arrive):
+    // (nAB, nrw) are this step's, (pAB, prw) the pending previous ones.
+    constexpr int kLateAt = MPPI_Q4_LATESEARCH;
+    f32x2 nAB = {0.f, 0.f}, nrw = {0.f, 0.f};
+    auto search_state = [&](int t, float anchor) {
+        const f32x2 fx = fk2 * C, fy = fk2 * Sn;
+        float px = q_sum(fx.x + fx.y), py = q_sum(fy.x + fy.y);
+        asm volatile("" : "+v"(px), "+v"(py) : "v"(anchor));
+        nAB = l0 ? f32x2{THD.x, THD.y - THD.x} : f32x2{px, py};
+        const unsigned j = sr.nearest(px, py);
+        if (slots && sub == 0) slots[(size_t)k * T + t - 1] = (int)j;   // debug instances only
+        const float2 r2 = s_win2[2 * j];
+        nrw = f32x2{r2.x, r2.y};
+    };
+#endif
+    auto step = [&](int t, auto slot_c, auto srch_c) {
         constexpr int slot = decltype(slot_c)::value;
+        constexpr bool srch = decltype(srch_c)::value;
         // the slot's values are taken here (volatile asm keeps its place against the previous step's
         // PIN_LOADS): left free, the scheduler hoists their uses into the previous step, where waiting for
         // them means waiting for every load in flight (as rollout_kernel's dstep)
@@ -863,6 +901,15 @@ __device__ __forceinline__ double chain_horizon_q4(const ChainConst& c, const Ch
         // ---- dynamics in absolute angles: bias, D' rows (a0, a1), Cholesky with the forward solve
         const f32x2 w = THD * THD;   // thdot^2
         const f32x2 lc = l2 * C, ls = l2 * Sn, vc = nu2 * C, vs = nu2 * Sn;
+#ifdef MPPI_Q4_LDSCOL
+        // (l c, l s) of every link of the quad through LDS: one write, four broadcast reads of the quad's
+        // rows (in order behind the write: LDS is in order within a wave) instead of 14 DPP moves
+        s_lcs[tid] = make_float4(lc.x, lc.y, ls.x, ls.y);
+        __builtin_amdgcn_wave_barrier();
+        float4 lcs[4];
+#pragma unroll
+        for (int i = 0; i < 4; ++i) lcs[i] = s_lcs[(tid & ~3) + i];
+#endif
         const f32x2 wvc = w * vc, wvs = w * vs, wlc = w * lc, wls = w * ls;
         const float sC = q_excl_suffix(wvc.x + wvc.y, u1), sS = q_excl_suffix(wvs.x + wvs.y, u1);
         const float pC = q_excl_prefix(wlc.x + wlc.y, m1), pS = q_excl_prefix(wls.x + wls.y, m1);
@@ -879,7 +926,11 @@ __device__ __forceinline__ double chain_horizon_q4(const ChainConst& c, const Ch
         f32x2 col[N];
         unroll_seq([&](auto a_c) {
             constexpr int a = decltype(a_c)::value;
+#ifdef MPPI_Q4_LDSCOL
+            const float la = (a & 1) ? lcs[a / 2].y : lcs[a / 2].x, sa = (a & 1) ? lcs[a / 2].w : lcs[a / 2].z;
+#else
             const float la = qbc<a / 2>(elem<a>(lc)), sa = qbc<a / 2>(elem<a>(ls));
+#endif
             col[a] = __builtin_elementwise_fma(splat(la), vc, __builtin_elementwise_fma(splat(sa), vs, corr[a]));
         }, std::make_integer_sequence<int, N>{});
         float inv[N], L[N][N], y[N];
@@ -898,6 +949,9 @@ __device__ __forceinline__ double chain_horizon_q4(const ChainConst& c, const Ch
                     col[kk] = __builtin_elementwise_fma(splat(-L[kk][j]), col[j], col[kk]);
                 }
             }, std::make_integer_sequence<int, N>{});
+#ifdef MPPI_Q4_LATESEARCH
+            if constexpr (srch && j == (kLateAt < N ? kLateAt : N - 1)) search_state(t, inv[j]);
+#endif
         }, std::make_integer_sequence<int, N>{});
         float x[N];   // L^T x = y: theta_ddot, redundantly in every lane
 #pragma unroll
@@ -908,11 +962,32 @@ __device__ __forceinline__ double chain_horizon_q4(const ChainConst& c, const Ch
             x[i] = e * inv[i];
         }
         auto xs = [&](int i) { return i < N ? x[i] : 0.f; };
+#ifdef MPPI_Q4_MASKSEL
+        // this lane's pair by one-hot weights (exact: one product by 1, the others by 0 added as +0)
+        f32x2 xab = f32x2{xs(0), xs(1)} * splat(oh[0]);
+#pragma unroll
+        for (int q = 1; q < 4; ++q) xab = __builtin_elementwise_fma(f32x2{xs(2 * q), xs(2 * q + 1)}, splat(oh[q]), xab);
+        const float xa = xab.x, xb = xab.y;
+#else
         const bool b0 = sub & 1, b1 = sub & 2;
         const float xa = b1 ? (b0 ? xs(6) : xs(4)) : (b0 ? xs(2) : xs(0));
         const float xb = b1 ? (b0 ? xs(7) : xs(5)) : (b0 ? xs(3) : xs(1));
+#endif
         THD = __builtin_elementwise_fma(f32x2{xa, xb}, splat(dt), THD);  // semi-implicit Euler (chain_oracle.py)
         TH = __builtin_elementwise_fma(THD, splat(dtr), TH);
+#ifdef MPPI_Q4_LATESEARCH
+        angles();
+        {   // the pending cost (the previous step's state; exactly 0 until the first search)
+            f32x2 rw = prw;
+            asm volatile("" : "+v"(rw) : "v"(TH));
+            const f32x2 e = pAB - rw;
+            S2 = __builtin_elementwise_fma(sw2, e * e, S2);
+        }
+        if constexpr (srch) {
+            pAB = nAB;
+            prw = nrw;
+        }
+#else
         angles();
         // ---- the previous step's stage cost: its window row has long arrived (control.py:174-185); the
         // row is taken only now (the asm needs TH, this step's last dynamics result): left free, the
@@ -923,6 +998,8 @@ __device__ __forceinline__ double chain_horizon_q4(const ChainConst& c, const Ch
             const f32x2 e = pAB - rw;
             S2 = __builtin_elementwise_fma(sw2, e * e, S2);
         }
+#endif
+#ifndef MPPI_Q4_LATESEARCH
         // ---- end effector and nearest waypoint of this step; its row is read now, used next step
         const f32x2 fx = fk2 * C, fy = fk2 * Sn;
         float px = q_sum(fx.x + fx.y), py = q_sum(fy.x + fy.y);
@@ -934,6 +1011,7 @@ __device__ __forceinline__ double chain_horizon_q4(const ChainConst& c, const Ch
         if (slots && sub == 0) slots[(size_t)k * T + t] = (int)j;   // debug instances only
         const float2 r2 = s_win2[2 * j];
         prw = f32x2{r2.x, r2.y};
+#endif
         if constexpr (slot == kCPF - 1) {
             S += (double)((S2.x + S2.y) + (G2.x + G2.y));
             S2 = f32x2{0.f, 0.f};
@@ -941,12 +1019,34 @@ __device__ __forceinline__ double chain_horizon_q4(const ChainConst& c, const Ch
         }
     };
     static_assert(kCPF == 2, "unrolled for a 2-deep ring");
+    using I0 = std::integral_constant<int, 0>;
+    using I1 = std::integral_constant<int, 1>;
+#ifdef MPPI_Q4_LATESEARCH
+    using B0 = std::false_type;
+    using B1 = std::true_type;
+    step(0, I0{}, B0{});
+    int t = 1;
+    for (; t + 2 <= T; t += 2) {
+        step(t, I1{}, B1{});
+        step(t + 1, I0{}, B1{});
+    }
+    if (t < T) step(t, I1{}, B1{});
+    {   // state T - 1's pending cost, then the last state's search (its cost below, with the terminal cost)
+        const f32x2 e = pAB - prw;
+        S2 = __builtin_elementwise_fma(sw2, e * e, S2);
+    }
+    search_state(T, TH.x);
+    pAB = nAB;
+    prw = nrw;
+#else
+    using B1 = std::true_type;
     int t = 0;
     for (; t + 2 <= T; t += 2) {
-        step(t, std::integral_constant<int, 0>{});
-        step(t + 1, std::integral_constant<int, 1>{});
+        step(t, I0{}, B1{});
+        step(t + 1, I1{}, B1{});
     }
-    if (t < T) step(t, std::integral_constant<int, 0>{});
+    if (t < T) step(t, I0{}, B1{});
+#endif
     // the last step's stage cost and the terminal cost on the same state (control.py:106-109)
     const f32x2 e = pAB - prw, ee = e * e;
     S2 = __builtin_elementwise_fma(sw2, ee, S2);
@@ -971,6 +1071,7 @@ __global__ __launch_bounds__(kCT) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
     __shared__ KeyPair s_keys[kKeyPairs];
     __shared__ WinRowD s_wind[F64 ? kSlots : 1];
     __shared__ float4 s_ua4[LPS == 4 ? (kMaxT + kCPF) * 4 : 1];
+    __shared__ float4 s_lcs[LPS == 4 ? kCT : 1];
     __shared__ double s_redd[kCT / 64];
     __shared__ int s_cnt[kCT / 64];
     __shared__ int s_k[kCT];
@@ -1010,7 +1111,7 @@ __global__ __launch_bounds__(kCT) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
 #ifdef MPPI_CHAIN_Q_OLD
         S = chain_horizon_lps4<N>(c, st, dyn, noise, k, exf, s_ua4, s_win, slots);
 #else
-        S = chain_horizon_q4<N>(c, st, dyn, noise, k, exf, s_ua4, s_win, slots);
+        S = chain_horizon_q4<N>(c, st, dyn, noise, k, exf, s_ua4, s_win, s_lcs, slots);
 #endif
     } else {
     if (tid < kSlots) s_win[tid] = st->win[tid];

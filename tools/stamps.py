@@ -30,7 +30,7 @@ if os.environ.get("WORKLOAD") == "c5":   # the 7-link chain engine (config 5)
     eng = ChainEngine(K, T, 0.006, lam, 0.98, CHAIN7_SIGMA, [0.5, 0.5, 5, 5], [5, 5, 50, 50], 0.0, device=0)
     eng.set_step_inputs(CHAIN7_X0, path[:30], np.tile(gravity_torque(CHAIN7_X0[:7]), (T, 1)))
     set_dbg = eng._lib.mppi_chain_debug_set_buffer
-    eng.lanes_per_sample = 1
+    eng.lanes_per_sample = int(os.environ.get("LPS", "1"))
 else:
     eng = RolloutEngine(K, T, 0.006, lam, 0.98, np.eye(2) * 20.0, [0.5, 0.5, 5, 5], [5, 5, 50, 50], 0.0, ArmParams(),
                         device=0, lanes_per_sample=int(os.environ.get("LPS", "0")))
