@@ -551,11 +551,11 @@ __device__ __forceinline__ double chain_horizon_f64(const ChainConst& c, const C
 // ChainState's representation — and the quad exchanges values with DPP
 // quad_perm (one instruction per broadcast or scan step).  Per lane and step:
 // one pair's sincos, prefix / suffix sums as 4-lane scans, the rows (2p, 2p+1)
-// of D' and of the right-looking Cholesky (each pivot and each L[kk][j]
-// broadcast from the lane that owns it, so every lane ends with all of L), the
-// forward solve on the pairs with each y_j broadcast, the backward solve
+// of D' and of its right-looking L D L^T factorization (each pivot and each
+// L[kk][j] broadcast from the lane that owns it, so every lane ends with all of
+// L), the forward solve on the pairs with each y_j broadcast, the backward solve
 // redundantly from those broadcast values, and 8 of the 30 window slots.
-// ~0.55x the instructions per lane of one lane per sample, on 4x the lanes.
+// ~0.52x the instructions per lane of one lane per sample, on 4x the lanes.
 
 // v from lane Q of each quad
 template <int Q>
@@ -591,194 +591,31 @@ __device__ __forceinline__ float elem(f32x2 v) {
     return (J & 1) ? v.y : v.x;
 }
 
-// The horizon loop of sample k on the 4 lanes of its quad (control.py:95-109 with
-// the chain model).  Returns S, the same value in all 4 lanes.  s_ua4 holds
-// (T + kCPF) x 4 rows: (u_2p, u_2p+1, a_2p, a_2p+1) of step t for lane p.
-template <int N>
-__device__ __forceinline__ double chain_horizon_lps4(const ChainConst& c, const ChainStep* st, const float* dyn,
-                                                     const float* noise, int k, float exf, float4* s_ua4,
-                                                     float4* s_win, int* slots) {
-    static_assert(N <= 8, "four link pairs");
-    const int tid = threadIdx.x, sub = tid & 3, K = c.K_local, T = c.T;
-    if (tid < kSlots) s_win[tid] = st->win[tid];
-    for (int i = tid; i < (T + kCPF) * 4; i += kCT) {
-        const int t = min(i >> 2, T - 1), p = i & 3;
-        const float* r = st->ua[t];
-        s_ua4[i] = make_float4(r[2 * p], r[2 * p + 1], r[kCMax + 2 * p], r[kCMax + 2 * p + 1]);
-    }
-    Search<4, true> sr;
-    sr.load(st->key, st->ctr, sub);
-    const int a0 = 2 * sub, a1 = 2 * sub + 1;   // this lane's links
-    const float m1 = sub >= 1 ? 1.f : 0.f, u1 = sub <= 2 ? 1.f : 0.f;
-    const float own = sub == 0 ? 1.f : 0.f;
-    const f32x2 pad = {a0 < N ? 1.f : 0.f, a1 < N ? 1.f : 0.f};
-    const f32x2 l2 = {dyn[kOffL + a0], dyn[kOffL + a1]}, nu2 = {dyn[kOffNu + a0], dyn[kOffNu + a1]};
-    const f32x2 damp2 = {dyn[kOffDamp + a0], dyn[kOffDamp + a1]}, fk2 = {dyn[kOffFk + a0], dyn[kOffFk + a1]};
-    const float dt = dyn[kOffDt], g = dyn[kOffG];
-    float sw[4], tw[4];
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-        sw[i] = dyn[kOffSw + i];
-        tw[i] = dyn[kOffTw + i];
-    }
-    // column a of D' on rows (a0, a1): l_a nu_i cos(th_a - th_i) from the broadcast (l c, l s) of link a, plus
-    // corr[a]: Dd_a - l_a nu_a on the diagonal (the product gives l_a nu_a there) and -J_{a+1} below it
-    f32x2 corr[N];
-    {
-        const float dc0 = dyn[kOffDd + a0] - l2.x * nu2.x, dc1 = dyn[kOffDd + a1] - l2.y * nu2.y;
-        const float j0 = a0 >= 1 ? dyn[kOffJ + 2 * (a0 - 1) + (a0 & 1)] : 0.f;   // -J_{a0} at (a0, a0 - 1)
-        const float j1 = dyn[kOffJ + 2 * (a1 - 1) + (a1 & 1)];                    // -J_{a1} at (a1, a1 - 1)
-#pragma unroll
-        for (int a = 0; a < N; ++a)
-            corr[a] = f32x2{a0 == a ? dc0 : (a0 == a + 1 ? j0 : 0.f), a1 == a ? dc1 : (a1 == a + 1 ? j1 : 0.f)};
-    }
-    // state of this lane's pair
-    f32x2 Q = {a0 < N ? st->x0[a0] : 0.f, a1 < N ? st->x0[a1] : 0.f};
-    f32x2 DQ = {a0 < N ? st->x0[N + a0] : 0.f, a1 < N ? st->x0[N + a1] : 0.f};
-    f32x2 C, Sn;
-    auto angles = [&]() {
-        const float t = Q.x + Q.y;
-        const float e = q_excl_prefix(t, m1);
-        float s0, c0, s1, c1;
-        sincos_f32(e + Q.x, &s0, &c0);
-        sincos_f32(e + t, &s1, &c1);
-        Sn = f32x2{s0, s1};
-        C = f32x2{c0, c1};
-    };
-    angles();
-    // noise of links (a0, a1) at step t: rows (t N + d) K + k; pad links read link N - 1 (masked below).
-    // A uniform row base plus a 32-bit lane byte offset (the saddr form of global_load).
-    const unsigned o0 = (unsigned)(min(a0, N - 1) * K + k) * 4u, o1 = (unsigned)(min(a1, N - 1) * K + k) * 4u;
-    auto nrow = [&](int t) {
-        const char* row = (const char*)(noise + (size_t)min(t, T - 1) * N * K);
-        return f32x2{*(const float*)(row + o0), *(const float*)(row + o1)};
-    };
-    f32x2 ring[kCPF];
-#pragma unroll
-    for (int j = 0; j < kCPF; ++j) ring[j] = nrow(j);
-    __syncthreads();
-
-    double S = 0.0;
-    float S4 = 0.f;
-    f32x2 G2 = {0.f, 0.f};   // this lane's (gamma u^T Sigma^-1) v terms
-    float ex = 0.f, ey = 0.f, e1 = 0.f, e2 = 0.f;
-    auto step = [&](int t, auto slot_c) {
-        constexpr int slot = decltype(slot_c)::value;
-        const float4 ua = s_ua4[t * 4 + sub];
-        const f32x2 v = __builtin_elementwise_fma(splat(exf), f32x2{ua.x, ua.y}, ring[slot]) * pad;  // control.py:99-101
-        G2 = __builtin_elementwise_fma(f32x2{ua.z, ua.w}, v, G2);                                  // control.py:106
-        ring[slot] = nrow(t + kCPF);
-        PIN_LOADS();
-        // ---- dynamics (ChainState::step on the quad)
-        f32x2 w;
-        {
-            const float t2 = DQ.x + DQ.y;
-            const float e = q_excl_prefix(t2, m1);
-            w = f32x2{e + DQ.x, e + t2};
-            w = w * w;   // thdot^2
-        }
-        const f32x2 lc = l2 * C, ls = l2 * Sn, vc = nu2 * C, vs = nu2 * Sn;
-        const f32x2 wvc = w * vc, wvs = w * vs, wlc = w * lc, wls = w * ls;
-        const float sC = q_excl_suffix(wvc.x + wvc.y, u1), sS = q_excl_suffix(wvs.x + wvs.y, u1);
-        const float pC = q_excl_prefix(wlc.x + wlc.y, m1), pS = q_excl_prefix(wls.x + wls.y, m1);
-        const f32x2 Cs = {wvc.y + sC, sC}, Ss = {wvs.y + sS, sS};
-        const f32x2 Cp = {pC, wlc.x + pC}, Sp = {pS, wls.x + pS};
-        const f32x2 X = __builtin_elementwise_fma(l2, Cs, nu2 * Cp);
-        const f32x2 Y = __builtin_elementwise_fma(l2, Ss, nu2 * Sp);
-        const f32x2 ve = __builtin_elementwise_fma(-damp2, DQ, v);
-        const float ve_next = dpp_f32<0xF9>(ve.x) * u1;   // link a1 + 1 (0 past the quad)
-        f32x2 r = {ve.x - ve.y, ve.y - ve_next};            // tau
-        r = __builtin_elementwise_fma(C, Y, __builtin_elementwise_fma(-Sn, X, __builtin_elementwise_fma(splat(-g), vc, r)));
-        // D' rows (a0, a1), Cholesky: every lane keeps the broadcast L[kk][j] and 1 / L[j][j]
-        f32x2 col[N];
-        unroll_seq([&](auto a_c) {
-            constexpr int a = decltype(a_c)::value;
-            const float la = qbc<a / 2>(elem<a>(lc)), sa = qbc<a / 2>(elem<a>(ls));
-            col[a] = __builtin_elementwise_fma(splat(la), vc, __builtin_elementwise_fma(splat(sa), vs, corr[a]));
-        }, std::make_integer_sequence<int, N>{});
-        // with L y = r folded in as the factorization's extra column: y_j leaves as soon as column j is
-        // scaled (rows <= j of r go stale once their y is out), so the solve's chain runs beside the
-        // factorization's instead of after it; every lane keeps every y_j
-        float inv[N], L[N][N], y[N];
-        unroll_seq([&](auto j_c) {
-            constexpr int j = decltype(j_c)::value;
-            inv[j] = __builtin_amdgcn_rsqf(qbc<j / 2>(elem<j>(col[j])));
-            col[j] = col[j] * splat(inv[j]);
-            y[j] = qbc<j / 2>(elem<j>(r) * inv[j]);
-            r = __builtin_elementwise_fma(splat(-y[j]), col[j], r);
-            unroll_seq([&](auto k_c) {
-                constexpr int kk = decltype(k_c)::value;
-                if constexpr (kk > j) {
-                    L[kk][j] = qbc<kk / 2>(elem<kk>(col[j]));
-                    col[kk] = __builtin_elementwise_fma(splat(-L[kk][j]), col[j], col[kk]);
-                }
-            }, std::make_integer_sequence<int, N>{});
-        }, std::make_integer_sequence<int, N>{});
-        // L^T x = y, redundantly in every lane from the broadcast values; the oldest x first, so each
-        // x_i waits on x_{i+1} through one fma and one multiply
-        float x[N];
-#pragma unroll
-        for (int i = N - 1; i >= 0; --i) {
-            float e = y[i];
-#pragma unroll
-            for (int kk = N - 1; kk > i; --kk) e = fmaf(-L[kk][i], x[kk], e);
-            x[i] = e * inv[i];
-        }
-        auto xs = [&](int i) { return i >= 0 && i < N ? x[i] : 0.f; };   // i compile-time below
-        const bool b0 = sub & 1, b1 = sub & 2;
-        const float xa = b1 ? (b0 ? xs(6) : xs(4)) : (b0 ? xs(2) : xs(0));
-        const float xb = b1 ? (b0 ? xs(7) : xs(5)) : (b0 ? xs(3) : xs(1));
-        const float xp = b1 ? (b0 ? xs(5) : xs(3)) : (b0 ? xs(1) : 0.f);   // link a0 - 1
-        const f32x2 qdd = f32x2{xa - xp, xb - xa} * pad;                     // q_ddot = diff(theta_ddot)
-        DQ = __builtin_elementwise_fma(qdd, splat(dt), DQ);
-        Q = __builtin_elementwise_fma(DQ, splat(dt), Q);
-        angles();
-        // ---- end effector, nearest waypoint, stage cost (control.py:174-198)
-        const f32x2 fx = fk2 * C, fy = fk2 * Sn;
-        const float px = q_sum(fx.x + fx.y), py = q_sum(fy.x + fy.y);
-        const unsigned j = sr.nearest(px, py);
-        if (slots && sub == 0) slots[(size_t)k * T + t] = (int)j;   // debug instances only
-        const float4 rw = s_win[j];
-        ex = px - rw.x;
-        ey = py - rw.y;
-        e1 = qbc<0>(DQ.x) - rw.z;
-        e2 = qbc<0>(DQ.y) - rw.w;
-        S4 = fmaf(own, weighted_sq(ex, ey, e1, e2, sw), S4);
-        if constexpr (slot == kCPF - 1) {
-            S += (double)(S4 + (G2.x + G2.y));
-            S4 = 0.f;
-            G2 = f32x2{0.f, 0.f};
-        }
-    };
-    static_assert(kCPF == 2, "unrolled for a 2-deep ring");
-    int t = 0;
-    for (; t + 2 <= T; t += 2) {
-        step(t, std::integral_constant<int, 0>{});
-        step(t + 1, std::integral_constant<int, 1>{});
-    }
-    if (t < T) step(t, std::integral_constant<int, 0>{});
-    S += (double)(S4 + (G2.x + G2.y));
-    S += (double)(own * weighted_sq(ex, ey, e1, e2, tw));   // terminal cost, control.py:109
-    return q_sum_f64(S);
-}
-
-// The same quad, stepped in absolute angles (theta_a = q_1 + ... + q_a, kept in
+// The quad stepped in absolute angles (theta_a = q_1 + ... + q_a, kept in
 // revolutions, the unit of v_sin_f32 / v_cos_f32) and their rates: the solve
-// gives theta_ddot directly, so the per-step prefix sums of q and q_dot (two
-// 4-lane scans on the serial path before the sincos), the difference of the
-// solution and its pad mask drop out; the joint rates the damping needs are one
-// difference (theta_dot of link a0 - 1 from the lane below).  Software-pipelined
-// at one wave per SIMD, where every latency is exposed: the per-step constants
-// come from a 2-deep register ring like the noise rows, and the window row of
-// step t is read from LDS right after its search but consumed only after step
-// t + 1's dynamics (deferred cost; the stage cost goes into S in step order).
+// gives theta_ddot directly; the joint rates the damping needs are one
+// difference (theta_dot of link a0 - 1 from the lane below).  Scheduled for one
+// wave per SIMD, where every latency is exposed:
+// - D' = L D L^T (unit lower L) instead of Cholesky: 1 / d_j is the rcp of the
+//   broadcast pivot, each L entry and each y_j one multiply with its broadcast
+//   folded in, and the back solve has no scaling (no square roots, no column
+//   scalings, 7 fewer multiplies per step);
+// - the state's end effector, window search and LDS row read sit inside the
+//   factorization (after column kSearchAt), whose pivot chain leaves issue
+//   slots idle; the state's stage cost is taken one step later, when its row
+//   has long arrived.  State 0 carries no cost (control.py:95-109), so step 0
+//   has no search, and the last state's search follows the loop;
+// - noise rows through a buffer resource (the row offset in soffset, the
+//   lane's in its VGPR: no 64-bit address arithmetic per step), prefetched two
+//   steps ahead; the per-step constants from a 2-deep register ring.
 // The stage cost's four terms go to two lanes, two apiece (lane 0 has both joint
 // rates of the cost in its own pair), so it needs no broadcast.
 template <int N>
 __device__ __forceinline__ double chain_horizon_q4(const ChainConst& c, const ChainStep* st, const float* dyn,
                                                    const float* noise, int k, float exf, float4* s_ua4,
-                                                   float4* s_win, float4* s_lcs, int* slots) {
+                                                   float4* s_win, int* slots) {
     static_assert(N <= 8, "four link pairs");
+    constexpr int kSearchAt = N > 4 ? 4 : N - 1;   // the column after which the search is placed
     const int tid = threadIdx.x, sub = tid & 3, K = c.K_local, T = c.T;
     if (tid < kSlots) s_win[tid] = st->win[tid];
     for (int i = tid; i < (T + kCPF) * 4; i += kCT) {
@@ -790,11 +627,6 @@ __device__ __forceinline__ double chain_horizon_q4(const ChainConst& c, const Ch
     sr.load(st->key, st->ctr, sub);
     const int a0 = 2 * sub, a1 = 2 * sub + 1;   // this lane's links
     const float m1 = sub >= 1 ? 1.f : 0.f, u1 = sub <= 2 ? 1.f : 0.f;
-#ifdef MPPI_Q4_MASKSEL
-    float oh[4];
-#pragma unroll
-    for (int q = 0; q < 4; ++q) oh[q] = sub == q ? 1.f : 0.f;
-#endif
     // the stage cost's four terms split over two lanes, two apiece: lane 0 the joint-rate terms (its own
     // theta_dot pair gives q_dot_1, q_dot_2), lane 1 the position terms; lanes 2, 3 weigh theirs by 0
     const bool l0 = sub == 0;
@@ -809,11 +641,13 @@ __device__ __forceinline__ double chain_horizon_q4(const ChainConst& c, const Ch
     const f32x2 tw2 = l0 ? f32x2{dyn[kOffTw + 2], dyn[kOffTw + 3]}
                          : (sub == 1 ? f32x2{dyn[kOffTw], dyn[kOffTw + 1]} : f32x2{0.f, 0.f});
     const float2* const s_win2 = reinterpret_cast<const float2*>(s_win) + (l0 ? 1 : 0);   // (rdq1, rdq2) / (rx, ry)
-    f32x2 corr[N];   // as chain_horizon_lps4
+    // column a of D' on rows (a0, a1): l_a nu_i cos(th_a - th_i) from the broadcast (l c, l s) of link a, plus
+    // corr[a]: Dd_a - l_a nu_a on the diagonal (the product gives l_a nu_a there) and -J_{a+1} below it
+    f32x2 corr[N];
     {
         const float dc0 = dyn[kOffDd + a0] - l2.x * nu2.x, dc1 = dyn[kOffDd + a1] - l2.y * nu2.y;
-        const float j0 = a0 >= 1 ? dyn[kOffJ + 2 * (a0 - 1) + (a0 & 1)] : 0.f;
-        const float j1 = dyn[kOffJ + 2 * (a1 - 1) + (a1 & 1)];
+        const float j0 = a0 >= 1 ? dyn[kOffJ + 2 * (a0 - 1) + (a0 & 1)] : 0.f;   // -J_{a0} at (a0, a0 - 1)
+        const float j1 = dyn[kOffJ + 2 * (a1 - 1) + (a1 & 1)];                    // -J_{a1} at (a1, a1 - 1)
 #pragma unroll
         for (int a = 0; a < N; ++a)
             corr[a] = f32x2{a0 == a ? dc0 : (a0 == a + 1 ? j0 : 0.f), a1 == a ? dc1 : (a1 == a + 1 ? j1 : 0.f)};
@@ -833,10 +667,9 @@ __device__ __forceinline__ double chain_horizon_q4(const ChainConst& c, const Ch
         Sn = f32x2{__builtin_amdgcn_sinf(TH.x), __builtin_amdgcn_sinf(TH.y)};
     };
     angles();
+    // noise of links (a0, a1) at step t: rows (t N + d) K + k; pad links read link N - 1 (masked below);
+    // the host keeps T N K 4 below 2^31 for this kernel (mppi_chain_ctx_create)
     const unsigned o0 = (unsigned)(min(a0, N - 1) * K + k) * 4u, o1 = (unsigned)(min(a1, N - 1) * K + k) * 4u;
-#ifdef MPPI_Q4_NOISEBUF
-    // the row's byte offset in the buffer instruction's scalar soffset (one s_min and one s_mul per row), the
-    // lane's offset in its VGPR: no 64-bit address arithmetic per step (the host keeps T N K 4 below 2^31)
     const __amdgpu_buffer_rsrc_t nrs = rows_rsrc(noise, T * N * K * 4);
     const int rowb = N * K * 4;
     auto nrow = [&](int t) {
@@ -844,12 +677,6 @@ __device__ __forceinline__ double chain_horizon_q4(const ChainConst& c, const Ch
         return f32x2{__builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(nrs, (int)o0, so, 0)),
                      __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(nrs, (int)o1, so, 0))};
     };
-#else
-    auto nrow = [&](int t) {
-        const char* row = (const char*)(noise + (size_t)min(t, T - 1) * N * K);
-        return f32x2{*(const float*)(row + o0), *(const float*)(row + o1)};
-    };
-#endif
     f32x2 ring[kCPF];
 #pragma unroll
     for (int j = 0; j < kCPF; ++j) ring[j] = nrow(j);
@@ -861,29 +688,21 @@ __device__ __forceinline__ double chain_horizon_q4(const ChainConst& c, const Ch
     double S = 0.0;
     f32x2 S2 = {0.f, 0.f};   // this lane's two stage-cost terms
     f32x2 G2 = {0.f, 0.f};   // this lane's (gamma u^T Sigma^-1) v terms
-    // the pending stage cost (the previous step's): this lane's two values and their window-row entries;
-    // all zero before the first step, so the first "pending" cost is exactly 0
-    f32x2 pAB = {0.f, 0.f}, prw = {0.f, 0.f};
-#ifdef MPPI_Q4_LATESEARCH
-    // the current state's end effector, window search and row read placed inside the step's factorization
-    // (after column MPPI_Q4_LATESEARCH), where the pivot chain leaves issue slots idle; the cost is taken at
-    // the end of the same step.  Step 0's state carries no cost (control.py:95-109): step 0 has no search,
-    // and the last state's search runs after the loop.
-    // The state's cost is taken one step after its search (the row read has a whole step to arrive):
-    // (nAB, nrw) are this step's, (pAB, prw) the pending previous ones.
-    constexpr int kLateAt = MPPI_Q4_LATESEARCH;
-    f32x2 nAB = {0.f, 0.f}, nrw = {0.f, 0.f};
-    auto search_state = [&](int t, float anchor) {
+    // the pending stage cost (the previous step's state): this lane's two values and their window-row entries,
+    // all zero until the first search, so the cost taken in steps 0 and 1 is exactly 0; (nAB, nrw) this step's
+    f32x2 pAB = {0.f, 0.f}, prw = {0.f, 0.f}, nAB = {0.f, 0.f}, nrw = {0.f, 0.f};
+    auto search_state = [&](int t, float anchor) {   // the current state (t): end effector, nearest slot, row
         const f32x2 fx = fk2 * C, fy = fk2 * Sn;
         float px = q_sum(fx.x + fx.y), py = q_sum(fy.x + fy.y);
-        asm volatile("" : "+v"(px), "+v"(py) : "v"(anchor));
+        asm volatile("" : "+v"(px), "+v"(py) : "v"(anchor));   // no earlier than the anchor (and opaque: the
+                                                                 // SLP vectoriser would pair the two sums)
+        // lane 0: q_dot_1 = theta_dot_1, q_dot_2 = theta_dot_2 - theta_dot_1; the others: the position
         nAB = l0 ? f32x2{THD.x, THD.y - THD.x} : f32x2{px, py};
         const unsigned j = sr.nearest(px, py);
         if (slots && sub == 0) slots[(size_t)k * T + t - 1] = (int)j;   // debug instances only
         const float2 r2 = s_win2[2 * j];
         nrw = f32x2{r2.x, r2.y};
     };
-#endif
     auto step = [&](int t, auto slot_c, auto srch_c) {
         constexpr int slot = decltype(slot_c)::value;
         constexpr bool srch = decltype(srch_c)::value;
@@ -898,18 +717,9 @@ __device__ __forceinline__ double chain_horizon_q4(const ChainConst& c, const Ch
         ring[slot] = nrow(t + kCPF);
         uar[slot] = s_ua4[(t + kCPF) * 4 + sub];
         PIN_LOADS();
-        // ---- dynamics in absolute angles: bias, D' rows (a0, a1), Cholesky with the forward solve
+        // ---- dynamics in absolute angles: bias, D' rows (a0, a1), L D L^T with the forward solve
         const f32x2 w = THD * THD;   // thdot^2
         const f32x2 lc = l2 * C, ls = l2 * Sn, vc = nu2 * C, vs = nu2 * Sn;
-#ifdef MPPI_Q4_LDSCOL
-        // (l c, l s) of every link of the quad through LDS: one write, four broadcast reads of the quad's
-        // rows (in order behind the write: LDS is in order within a wave) instead of 14 DPP moves
-        s_lcs[tid] = make_float4(lc.x, lc.y, ls.x, ls.y);
-        __builtin_amdgcn_wave_barrier();
-        float4 lcs[4];
-#pragma unroll
-        for (int i = 0; i < 4; ++i) lcs[i] = s_lcs[(tid & ~3) + i];
-#endif
         const f32x2 wvc = w * vc, wvs = w * vs, wlc = w * lc, wls = w * ls;
         const float sC = q_excl_suffix(wvc.x + wvc.y, u1), sS = q_excl_suffix(wvs.x + wvs.y, u1);
         const float pC = q_excl_prefix(wlc.x + wlc.y, m1), pS = q_excl_prefix(wls.x + wls.y, m1);
@@ -926,58 +736,46 @@ __device__ __forceinline__ double chain_horizon_q4(const ChainConst& c, const Ch
         f32x2 col[N];
         unroll_seq([&](auto a_c) {
             constexpr int a = decltype(a_c)::value;
-#ifdef MPPI_Q4_LDSCOL
-            const float la = (a & 1) ? lcs[a / 2].y : lcs[a / 2].x, sa = (a & 1) ? lcs[a / 2].w : lcs[a / 2].z;
-#else
             const float la = qbc<a / 2>(elem<a>(lc)), sa = qbc<a / 2>(elem<a>(ls));
-#endif
             col[a] = __builtin_elementwise_fma(splat(la), vc, __builtin_elementwise_fma(splat(sa), vs, corr[a]));
         }, std::make_integer_sequence<int, N>{});
-        float inv[N], L[N][N], y[N];
+        // right-looking on the raw columns, every factor kept negated: -1 / d_j is the rcp of the negated
+        // broadcast pivot (a source modifier of the DPP form), -L[kk][j] and -y_j are the broadcast entries
+        // times it, so no product needs a negation that would take it out of the VOP2 encoding the broadcast
+        // folds into; every lane keeps every -L[kk][j] and -y_j (y = D^-1 L^-1 r: the back solve needs no
+        // scaling)
+        float Ln[N][N], yn[N];
         unroll_seq([&](auto j_c) {
             constexpr int j = decltype(j_c)::value;
-            inv[j] = __builtin_amdgcn_rsqf(qbc<j / 2>(elem<j>(col[j])));
-            col[j] = col[j] * splat(inv[j]);
-            // inv[j] is the same in every lane (the rsq of one broadcast value), so broadcasting r_j and
-            // scaling after gives the owner's product bit for bit, and the broadcast folds into the multiply
-            y[j] = qbc<j / 2>(elem<j>(r)) * inv[j];
-            r = __builtin_elementwise_fma(splat(-y[j]), col[j], r);
+            const float nrd = __builtin_amdgcn_rcpf(-qbc<j / 2>(elem<j>(col[j])));
+            yn[j] = qbc<j / 2>(elem<j>(r)) * nrd;
+            r = __builtin_elementwise_fma(splat(yn[j]), col[j], r);
             unroll_seq([&](auto k_c) {
                 constexpr int kk = decltype(k_c)::value;
                 if constexpr (kk > j) {
-                    L[kk][j] = qbc<kk / 2>(elem<kk>(col[j]));
-                    col[kk] = __builtin_elementwise_fma(splat(-L[kk][j]), col[j], col[kk]);
+                    Ln[kk][j] = qbc<kk / 2>(elem<kk>(col[j])) * nrd;
+                    col[kk] = __builtin_elementwise_fma(splat(Ln[kk][j]), col[j], col[kk]);
                 }
             }, std::make_integer_sequence<int, N>{});
-#ifdef MPPI_Q4_LATESEARCH
-            if constexpr (srch && j == (kLateAt < N ? kLateAt : N - 1)) search_state(t, inv[j]);
-#endif
+            if constexpr (srch && j == kSearchAt) search_state(t, nrd);
         }, std::make_integer_sequence<int, N>{});
-        float x[N];   // L^T x = y: theta_ddot, redundantly in every lane
+        float x[N];   // L^T x = y: theta_ddot, redundantly in every lane; the oldest x first
 #pragma unroll
         for (int i = N - 1; i >= 0; --i) {
-            float e = y[i];
+            float e = -yn[i];
 #pragma unroll
-            for (int kk = N - 1; kk > i; --kk) e = fmaf(-L[kk][i], x[kk], e);
-            x[i] = e * inv[i];
+            for (int kk = N - 1; kk > i; --kk) e = fmaf(Ln[kk][i], x[kk], e);
+            x[i] = e;
         }
         auto xs = [&](int i) { return i < N ? x[i] : 0.f; };
-#ifdef MPPI_Q4_MASKSEL
-        // this lane's pair by one-hot weights (exact: one product by 1, the others by 0 added as +0)
-        f32x2 xab = f32x2{xs(0), xs(1)} * splat(oh[0]);
-#pragma unroll
-        for (int q = 1; q < 4; ++q) xab = __builtin_elementwise_fma(f32x2{xs(2 * q), xs(2 * q + 1)}, splat(oh[q]), xab);
-        const float xa = xab.x, xb = xab.y;
-#else
         const bool b0 = sub & 1, b1 = sub & 2;
         const float xa = b1 ? (b0 ? xs(6) : xs(4)) : (b0 ? xs(2) : xs(0));
         const float xb = b1 ? (b0 ? xs(7) : xs(5)) : (b0 ? xs(3) : xs(1));
-#endif
         THD = __builtin_elementwise_fma(f32x2{xa, xb}, splat(dt), THD);  // semi-implicit Euler (chain_oracle.py)
         TH = __builtin_elementwise_fma(THD, splat(dtr), TH);
-#ifdef MPPI_Q4_LATESEARCH
         angles();
-        {   // the pending cost (the previous step's state; exactly 0 until the first search)
+        {   // the pending (previous state's) stage cost, control.py:174-185; the row is taken only now (the
+            // asm needs TH, this step's last dynamics result)
             f32x2 rw = prw;
             asm volatile("" : "+v"(rw) : "v"(TH));
             const f32x2 e = pAB - rw;
@@ -987,31 +785,6 @@ __device__ __forceinline__ double chain_horizon_q4(const ChainConst& c, const Ch
             pAB = nAB;
             prw = nrw;
         }
-#else
-        angles();
-        // ---- the previous step's stage cost: its window row has long arrived (control.py:174-185); the
-        // row is taken only now (the asm needs TH, this step's last dynamics result): left free, the
-        // scheduler pulls the cost up next to the lookup and waits on the LDS round trip there
-        {
-            f32x2 rw = prw;
-            asm volatile("" : "+v"(rw) : "v"(TH));
-            const f32x2 e = pAB - rw;
-            S2 = __builtin_elementwise_fma(sw2, e * e, S2);
-        }
-#endif
-#ifndef MPPI_Q4_LATESEARCH
-        // ---- end effector and nearest waypoint of this step; its row is read now, used next step
-        const f32x2 fx = fk2 * C, fy = fk2 * Sn;
-        float px = q_sum(fx.x + fx.y), py = q_sum(fy.x + fy.y);
-        asm("" : "+v"(px), "+v"(py));   // opaque: the SLP vectoriser would pair the two sums into v_pk_add
-                                        // with their DPP moves unfolded
-        // lane 0: q_dot_1 = theta_dot_1, q_dot_2 = theta_dot_2 - theta_dot_1; the others: the position
-        pAB = l0 ? f32x2{THD.x, THD.y - THD.x} : f32x2{px, py};
-        const unsigned j = sr.nearest(px, py);
-        if (slots && sub == 0) slots[(size_t)k * T + t] = (int)j;   // debug instances only
-        const float2 r2 = s_win2[2 * j];
-        prw = f32x2{r2.x, r2.y};
-#endif
         if constexpr (slot == kCPF - 1) {
             S += (double)((S2.x + S2.y) + (G2.x + G2.y));
             S2 = f32x2{0.f, 0.f};
@@ -1021,34 +794,20 @@ __device__ __forceinline__ double chain_horizon_q4(const ChainConst& c, const Ch
     static_assert(kCPF == 2, "unrolled for a 2-deep ring");
     using I0 = std::integral_constant<int, 0>;
     using I1 = std::integral_constant<int, 1>;
-#ifdef MPPI_Q4_LATESEARCH
-    using B0 = std::false_type;
-    using B1 = std::true_type;
-    step(0, I0{}, B0{});
+    step(0, I0{}, std::false_type{});
     int t = 1;
     for (; t + 2 <= T; t += 2) {
-        step(t, I1{}, B1{});
-        step(t + 1, I0{}, B1{});
+        step(t, I1{}, std::true_type{});
+        step(t + 1, I0{}, std::true_type{});
     }
-    if (t < T) step(t, I1{}, B1{});
-    {   // state T - 1's pending cost, then the last state's search (its cost below, with the terminal cost)
+    if (t < T) step(t, I1{}, std::true_type{});
+    {   // state T - 1's pending cost, then the last state's search: its stage and terminal cost
+        // (control.py:106-109) on the same state
         const f32x2 e = pAB - prw;
         S2 = __builtin_elementwise_fma(sw2, e * e, S2);
     }
     search_state(T, TH.x);
-    pAB = nAB;
-    prw = nrw;
-#else
-    using B1 = std::true_type;
-    int t = 0;
-    for (; t + 2 <= T; t += 2) {
-        step(t, I0{}, B1{});
-        step(t + 1, I1{}, B1{});
-    }
-    if (t < T) step(t, I0{}, B1{});
-#endif
-    // the last step's stage cost and the terminal cost on the same state (control.py:106-109)
-    const f32x2 e = pAB - prw, ee = e * e;
+    const f32x2 e = nAB - nrw, ee = e * e;
     S2 = __builtin_elementwise_fma(sw2, ee, S2);
     S += (double)((S2.x + S2.y) + (G2.x + G2.y));
     const f32x2 te = tw2 * ee;
@@ -1071,7 +830,6 @@ __global__ __launch_bounds__(kCT) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
     __shared__ KeyPair s_keys[kKeyPairs];
     __shared__ WinRowD s_wind[F64 ? kSlots : 1];
     __shared__ float4 s_ua4[LPS == 4 ? (kMaxT + kCPF) * 4 : 1];
-    __shared__ float4 s_lcs[LPS == 4 ? kCT : 1];
     __shared__ double s_redd[kCT / 64];
     __shared__ int s_cnt[kCT / 64];
     __shared__ int s_k[kCT];
@@ -1108,11 +866,7 @@ __global__ __launch_bounds__(kCT) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
     if constexpr (F64) {
         S = chain_horizon_f64<N>(c, st, (cdouble*)(dyn + kDynF64Off), noise, k, exf, s_wind, slots);
     } else if constexpr (LPS == 4) {
-#ifdef MPPI_CHAIN_Q_OLD
-        S = chain_horizon_lps4<N>(c, st, dyn, noise, k, exf, s_ua4, s_win, slots);
-#else
-        S = chain_horizon_q4<N>(c, st, dyn, noise, k, exf, s_ua4, s_win, s_lcs, slots);
-#endif
+        S = chain_horizon_q4<N>(c, st, dyn, noise, k, exf, s_ua4, s_win, slots);
     } else {
     if (tid < kSlots) s_win[tid] = st->win[tid];
     // window keys in LDS (broadcast reads): the 90 key registers would cost the
@@ -1667,6 +1421,13 @@ int mppi_chain_ctx_create(const mppi_chain_config* cfg, int device, void* stream
     if (c->lps == 4 && c->f64) {
         delete c;
         return fail(MPPI_E_ARG, "lanes_per_sample 4 is for the fp32 rollout");
+    }
+    if (c->lps == 4 && (long long)cfg->K_local * cfg->T * n * 4 >= (1LL << 31)) {   // its noise buffer offsets
+        if (cfg->lanes_per_sample > 0) {
+            delete c;
+            return fail(MPPI_E_ARG, "lanes_per_sample 4 needs K_local * T * n * 4 below 2^31 bytes of noise");
+        }
+        c->lps = 1;
     }
     c->nblocks = (int)(((long long)cfg->K_local * c->lps + kCT - 1) / kCT);
     ChainConst& k = c->kc;
