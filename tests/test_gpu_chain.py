@@ -260,12 +260,19 @@ def test_chain_trajectories_match_oracle(paths):
 
 
 def test_chain_errors():
-    from mppi_robotarm_amd.chain import ChainEngine, ChainParams
+    from mppi_robotarm_amd.chain import CHAIN7_SIGMA, ChainEngine, ChainParams
     with pytest.raises(np.linalg.LinAlgError):
         ChainEngine(256, 8, 0.006, 100.0, 0.98, -np.eye(7), W, TW, device=0)
     with pytest.raises(ValueError):
         ChainEngine(256, 8, 0.006, 100.0, 0.98, np.eye(8), W, TW, chain=ChainParams(*(tuple([1.0] * 8),) * 7),
                     device=0)
+    # a quad per sample addresses its noise with 32-bit buffer offsets: K T n 4 bytes must stay below 2^31
+    big = 600000   # 600000 * 128 * 7 * 4 B = 2.15 GB
+    with pytest.raises(ValueError, match="lanes_per_sample 4"):
+        ChainEngine(big, 128, 0.006, 100.0, 0.98, CHAIN7_SIGMA, W, TW, device=0, lanes_per_sample=4)
+    e = ChainEngine(32768, 128, 0.006, 100.0, 0.98, CHAIN7_SIGMA, W, TW, device=0, lanes_per_sample=4)
+    assert e.lanes_per_sample == 4   # 117 MB of noise: allowed
+    e.close()
 
 
 def _uniform_chain(mod, n):
