@@ -5,7 +5,10 @@ first pass's loop-carried results) and reports the cycles of the second pass.  A
 previous one has left the issue slot and its register sources are ready:
   issue cost: VALU 4 (transcendentals 8, s_nop n: 4(n+1)), SALU / waitcnt / memory 4;
   result ready after: VALU LAT (default 8), transcendental TLAT (12), SALU 4; loads are assumed in time.
-Usage: issue_sim.py file.s [kernel-substring] [LAT] [TLAT]"""
+Usage: issue_sim.py file.s [kernel-substring] [LAT] [TLAT] [--ubench]
+--ubench: the issue costs measured by tools/ubench_issue.hip on gfx950 (profiles/r13/ubench_issue.txt, s_memtime
+cycles of one wave alone): v_add 6, other VALU 7, packed 7.76, transcendental 9.8, s_nop n 6(n + 1), scalar and
+memory 6; dependent-use latency LAT 9.5."""
 import re
 import sys
 
@@ -65,14 +68,18 @@ for p in range(2):
             srcs += dst
         if op == 's_cmp_le_i32' or op.startswith('s_cmp'):
             dst = ['scc']
-        cost = 4.0
-        lat = 4.0
+        UB = '--ubench' in sys.argv
+        base = 6.0 if UB else 4.0
+        cost = base
+        lat = base
         if op == 's_nop':
-            cost = 4.0 * (int(parts[0] or 0) + 1) if parts and parts[0] else 4.0
+            cost = base * (int(parts[0] or 0) + 1) if parts and parts[0] else base
         elif op.startswith(TRANS):
-            cost, lat = 8.0, TLAT
+            cost, lat = (9.8 if UB else 8.0), TLAT
         elif op.startswith('v_'):
             lat = LAT
+            if UB:
+                cost = 7.76 if op.startswith('v_pk_') else (6.0 if op.startswith(('v_add_f32', 'v_sub')) else 7.0)
         elif op.startswith(('global_load', 'buffer_load', 'ds_read')):
             lat = 0.0
         r = max([ready.get(s, 0.0) for s in srcs] + [t])
