@@ -46,6 +46,10 @@ constexpr int kCMaxVals = kMaxT * kCMax;    // T N values per row, at most
 #define MPPI_CHAIN_CPU 2
 #endif
 constexpr int kCPF = MPPI_CHAIN_CPF;        // noise steps in flight per lane (N rows each)
+#ifndef MPPI_Q4_PF
+#define MPPI_Q4_PF 2
+#endif
+constexpr int kQPF = MPPI_Q4_PF;            // the same for a quad per sample (its steps are ~4x shorter)
 constexpr int kCPU = MPPI_CHAIN_CPU;        // per-step constant rows in flight
 
 // Device-resident per-step parameter block (ping-pong pair in the context).
@@ -618,7 +622,7 @@ __device__ __forceinline__ double chain_horizon_q4(const ChainConst& c, const Ch
     constexpr int kSearchAt = N > 4 ? 4 : N - 1;   // the column after which the search is placed
     const int tid = threadIdx.x, sub = tid & 3, K = c.K_local, T = c.T;
     if (tid < kSlots) s_win[tid] = st->win[tid];
-    for (int i = tid; i < (T + kCPF) * 4; i += kCT) {
+    for (int i = tid; i < (T + kQPF) * 4; i += kCT) {
         const int t = min(i >> 2, T - 1), p = i & 3;
         const float* r = st->ua[t];
         s_ua4[i] = make_float4(r[2 * p], r[2 * p + 1], r[kCMax + 2 * p], r[kCMax + 2 * p + 1]);
@@ -677,13 +681,13 @@ __device__ __forceinline__ double chain_horizon_q4(const ChainConst& c, const Ch
         return f32x2{__builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(nrs, (int)o0, so, 0)),
                      __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(nrs, (int)o1, so, 0))};
     };
-    f32x2 ring[kCPF];
+    f32x2 ring[kQPF];
 #pragma unroll
-    for (int j = 0; j < kCPF; ++j) ring[j] = nrow(j);
+    for (int j = 0; j < kQPF; ++j) ring[j] = nrow(j);
     __syncthreads();
-    float4 uar[kCPF];
+    float4 uar[kQPF];
 #pragma unroll
-    for (int j = 0; j < kCPF; ++j) uar[j] = s_ua4[j * 4 + sub];
+    for (int j = 0; j < kQPF; ++j) uar[j] = s_ua4[j * 4 + sub];
 
     double S = 0.0;
     f32x2 S2 = {0.f, 0.f};   // this lane's two stage-cost terms
@@ -714,8 +718,8 @@ __device__ __forceinline__ double chain_horizon_q4(const ChainConst& c, const Ch
         asm volatile("" : "+v"(nz), "+v"(ua));
         const f32x2 v = __builtin_elementwise_fma(splat(exf), f32x2{ua.x, ua.y}, nz) * pad;  // control.py:99-101
         G2 = __builtin_elementwise_fma(f32x2{ua.z, ua.w}, v, G2);                          // control.py:106
-        ring[slot] = nrow(t + kCPF);
-        uar[slot] = s_ua4[(t + kCPF) * 4 + sub];
+        ring[slot] = nrow(t + kQPF);
+        uar[slot] = s_ua4[(t + kQPF) * 4 + sub];
         PIN_LOADS();
         // ---- dynamics in absolute angles: bias, D' rows (a0, a1), L D L^T with the forward solve
         const f32x2 w = THD * THD;   // thdot^2
@@ -785,22 +789,37 @@ __device__ __forceinline__ double chain_horizon_q4(const ChainConst& c, const Ch
             pAB = nAB;
             prw = nrw;
         }
-        if constexpr (slot == kCPF - 1) {
+        if constexpr (slot == kQPF - 1) {
             S += (double)((S2.x + S2.y) + (G2.x + G2.y));
             S2 = f32x2{0.f, 0.f};
             G2 = f32x2{0.f, 0.f};
         }
     };
-    static_assert(kCPF == 2, "unrolled for a 2-deep ring");
     using I0 = std::integral_constant<int, 0>;
     using I1 = std::integral_constant<int, 1>;
+    using I2 = std::integral_constant<int, 2>;
+    using I3 = std::integral_constant<int, 3>;
+    using Y = std::true_type;
     step(0, I0{}, std::false_type{});
     int t = 1;
-    for (; t + 2 <= T; t += 2) {
-        step(t, I1{}, std::true_type{});
-        step(t + 1, I0{}, std::true_type{});
+    if constexpr (kQPF == 2) {
+        for (; t + 2 <= T; t += 2) {
+            step(t, I1{}, Y{});
+            step(t + 1, I0{}, Y{});
+        }
+        if (t < T) step(t, I1{}, Y{});
+    } else {
+        static_assert(kQPF == 4, "a 2- or 4-deep ring");
+        for (; t + 4 <= T; t += 4) {   // slots 1, 2, 3, 0
+            step(t, I1{}, Y{});
+            step(t + 1, I2{}, Y{});
+            step(t + 2, I3{}, Y{});
+            step(t + 3, I0{}, Y{});
+        }
+        if (t < T) step(t, I1{}, Y{});   // remainder: slots 1, 2, 3 in order
+        if (t + 1 < T) step(t + 1, I2{}, Y{});
+        if (t + 2 < T) step(t + 2, I3{}, Y{});
     }
-    if (t < T) step(t, I1{}, std::true_type{});
     {   // state T - 1's pending cost, then the last state's search: its stage and terminal cost
         // (control.py:106-109) on the same state
         const f32x2 e = pAB - prw;
@@ -829,7 +848,7 @@ __global__ __launch_bounds__(kCT) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
     __shared__ float4 s_win[kSlots];
     __shared__ KeyPair s_keys[kKeyPairs];
     __shared__ WinRowD s_wind[F64 ? kSlots : 1];
-    __shared__ float4 s_ua4[LPS == 4 ? (kMaxT + kCPF) * 4 : 1];
+    __shared__ float4 s_ua4[LPS == 4 ? (kMaxT + kQPF) * 4 : 1];
     __shared__ double s_redd[kCT / 64];
     __shared__ int s_cnt[kCT / 64];
     __shared__ int s_k[kCT];

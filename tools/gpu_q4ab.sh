@@ -12,5 +12,7 @@ for l in "$@"; do
     --timeout 300 --timeout-method thread -k "n7 or every_link_count_against or short or lanes_per or fused" > $O/t_$l.log 2>&1
   rc=$?; echo "$l tests rc=$rc $(tail -1 $O/t_$l.log)"; [ $rc -eq 0 ] || { grep -E "^FAILED|^E " $O/t_$l.log | head -20; exit $rc; }
 done
-WORKLOAD=c5 timeout -k 10 400 python -u tools/ab.py $libs 16384 128 12 20 > $O/ab_c5k16384.txt 2>&1 || { tail -20 $O/ab_c5k16384.txt; exit 1; }
-cat $O/ab_c5k16384.txt
+for K in ${AB_K:-16384}; do
+  WORKLOAD=c5 timeout -k 10 400 python -u tools/ab.py $libs $K 128 12 20 > $O/ab_c5k$K.txt 2>&1 || { tail -20 $O/ab_c5k$K.txt; exit 1; }
+  cat $O/ab_c5k$K.txt
+done
