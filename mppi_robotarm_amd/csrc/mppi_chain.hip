@@ -47,7 +47,7 @@ constexpr int kCMaxVals = kMaxT * kCMax;    // T N values per row, at most
 #endif
 constexpr int kCPF = MPPI_CHAIN_CPF;        // noise steps in flight per lane (N rows each)
 #ifndef MPPI_Q4_PF
-#define MPPI_Q4_PF 2
+#define MPPI_Q4_PF 4   // 2 and 4 measured: equal at K = 16384, 4 -2.1 % at K = 32768 (profiles/r13/chain_quad_ring_depth_ab.txt)
 #endif
 constexpr int kQPF = MPPI_Q4_PF;            // the same for a quad per sample (its steps are ~4x shorter)
 constexpr int kCPU = MPPI_CHAIN_CPU;        // per-step constant rows in flight
@@ -617,7 +617,7 @@ __device__ __forceinline__ float elem(f32x2 v) {
 template <int N>
 __device__ __forceinline__ double chain_horizon_q4(const ChainConst& c, const ChainStep* st, const float* dyn,
                                                    const float* noise, int k, float exf, float4* s_ua4,
-                                                   float4* s_win, int* slots) {
+                                                   float4* s_win, int* slots, unsigned long long* dbg) {
     static_assert(N <= 8, "four link pairs");
     constexpr int kSearchAt = N > 4 ? 4 : N - 1;   // the column after which the search is placed
     const int tid = threadIdx.x, sub = tid & 3, K = c.K_local, T = c.T;
@@ -800,6 +800,7 @@ __device__ __forceinline__ double chain_horizon_q4(const ChainConst& c, const Ch
     using I2 = std::integral_constant<int, 2>;
     using I3 = std::integral_constant<int, 3>;
     using Y = std::true_type;
+    STAMP(12, NOW());   // stamp builds: the prologue's end, then the first steps and the horizon's middle
     step(0, I0{}, std::false_type{});
     int t = 1;
     if constexpr (kQPF == 2) {
@@ -815,6 +816,10 @@ __device__ __forceinline__ double chain_horizon_q4(const ChainConst& c, const Ch
             step(t + 1, I2{}, Y{});
             step(t + 2, I3{}, Y{});
             step(t + 3, I0{}, Y{});
+#ifdef MPPI_STAMPS
+            if (t == 1) STAMP(13, NOW());
+            if (t + 4 == T / 2 + 1) STAMP(14, NOW());
+#endif
         }
         if (t < T) step(t, I1{}, Y{});   // remainder: slots 1, 2, 3 in order
         if (t + 1 < T) step(t + 1, I2{}, Y{});
@@ -885,7 +890,7 @@ __global__ __launch_bounds__(kCT) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
     if constexpr (F64) {
         S = chain_horizon_f64<N>(c, st, (cdouble*)(dyn + kDynF64Off), noise, k, exf, s_wind, slots);
     } else if constexpr (LPS == 4) {
-        S = chain_horizon_q4<N>(c, st, dyn, noise, k, exf, s_ua4, s_win, slots);
+        S = chain_horizon_q4<N>(c, st, dyn, noise, k, exf, s_ua4, s_win, slots, dbg);
     } else {
     if (tid < kSlots) s_win[tid] = st->win[tid];
     // window keys in LDS (broadcast reads): the 90 key registers would cost the
