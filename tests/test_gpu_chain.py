@@ -94,6 +94,7 @@ def test_chain_at_n2_reproduces_reference_steps(name, paths):
 @pytest.mark.parametrize("K,T,lam,s99,lps", [(4096, 32, 100.0, 2e-4, 1), (4096, 32, 100.0, 2e-4, 4),
                                             (4096, 32, 1.0e9, 1e-7, 1), (4096, 32, 1.0e9, 1e-7, 4),
                                             (131072, 128, 100.0, 2e-4, 1), (16384, 128, 100.0, 2e-4, 4),
+                                            (32768, 128, 100.0, 2e-4, 4),   # the quad at auto's upper bound
                                             (3000, 7, 100.0, 1e-5, 1), (3000, 7, 100.0, 1e-5, 4)])
 def test_chain_n7_against_c_oracle(K, T, lam, s99, lps, paths):
     """Config 5 (K=131072 T=128), its 8-way shard (K=16384, a quad per sample) and smaller shapes: S and the
@@ -444,11 +445,12 @@ def test_chain_lanes_per_sample_agree(paths):
     assert _engine(16384, 8).lanes_per_sample == 4 and _engine(131072, 8).lanes_per_sample == 1
 
 
-@pytest.mark.parametrize("T", [1, 2, 3])
+@pytest.mark.parametrize("T", [1, 2, 3, 5, 6])
 @pytest.mark.parametrize("precision,lps", [("f32", 1), ("f32", 4), ("f64", 1)])
 def test_chain_short_horizons(T, precision, lps, paths):
-    """Horizons shorter than the prefetch rings and the 2- / 4-step unrolls (the remainder steps alone), ragged K,
-    against the C fp64 chain oracle."""
+    """Horizons shorter than the prefetch rings and the 2- / 4-step unrolls (the remainder steps alone; with a
+    quad per sample, step 0 is peeled and T = 5 is exactly one 4-step iteration, T = 6 one plus a remainder),
+    ragged K, against the C fp64 chain oracle."""
     K, lam = 999, 100.0
     _, x0, sig, ug = _c5()
     win = paths["xydq_circle"][:30]
