@@ -619,7 +619,12 @@ __device__ __forceinline__ double chain_horizon_q4(const ChainConst& c, const Ch
                                                    const float* noise, int k, float exf, float4* s_ua4,
                                                    float4* s_win, int* slots, unsigned long long* dbg) {
     static_assert(N <= 8, "four link pairs");
-    constexpr int kSearchAt = N > 4 ? 4 : N - 1;   // the column after which the search is placed
+    // the column after which the search is placed: after 2 / 3 / 4 / 5 / 6 measured 77.0 / 76.6 / 77.6 / 75.3 /
+    // 77.3 us at K = 16384 (one process, profiles/r13/chain_quad_search_at_ab.txt); MPPI_Q4_SEARCH_AT for A/B builds
+#ifndef MPPI_Q4_SEARCH_AT
+#define MPPI_Q4_SEARCH_AT 5
+#endif
+    constexpr int kSearchAt = N > MPPI_Q4_SEARCH_AT ? MPPI_Q4_SEARCH_AT : N - 1;
     const int tid = threadIdx.x, sub = tid & 3, K = c.K_local, T = c.T;
     if (tid < kSlots) s_win[tid] = st->win[tid];
     for (int i = tid; i < (T + kQPF) * 4; i += kCT) {
