@@ -763,6 +763,11 @@ __device__ __forceinline__ double chain_horizon_q4(const ChainConst& c, const Ch
                 constexpr int kk = decltype(k_c)::value;
                 if constexpr (kk > j) {
                     Ln[kk][j] = qbc<kk / 2>(elem<kk>(col[j])) * nrd;
+#ifndef MPPI_Q4_NO_LAST_ROW_PIN
+                    // the last row's products, left free, are paired by the SLP vectoriser into a v_pk_mul_f32,
+                    // which has no DPP form: their broadcasts come back as separate moves (7 per step)
+                    if constexpr (kk == N - 1) asm volatile("" : "+v"(Ln[kk][j]));
+#endif
                     col[kk] = __builtin_elementwise_fma(splat(Ln[kk][j]), col[j], col[kk]);
                 }
             }, std::make_integer_sequence<int, N>{});
