@@ -451,37 +451,90 @@ struct ChainStateD {
     }
 };
 
+// The fused update's median filter runs over windows of kMedRun consecutive steps per thread: thread
+// (q, d) = (tid / N, tid % N) takes the windows of t = kMedRun q .. kMedRun q + 3 of column d.
+constexpr int kMedRun = 4;
+static_assert(kCMax * ((kMaxT + kMedRun - 1) / kMedRun) <= kCT && 2 * kMaxT <= kCT, "one pass of the workgroup");
+
+// This thread's values of the current nominal (cur->u) for chain_update_block, read at kernel entry so their
+// latency is hidden
+template <int N>
+__device__ __forceinline__ void chain_nominal_prefetch(const ChainStep* s, int T, bool on, double (&u4)[kMedRun]) {
+    const int q = threadIdx.x / N, d = threadIdx.x - q * N;
+#pragma unroll
+    for (int j = 0; j < kMedRun; ++j) {
+        const int t = kMedRun * q + j;
+        u4[j] = (on && t < T) ? s->u[t][d] : 0.0;
+    }
+}
+
 // Median filter (control.py:319-327) of the T x N weighted noise, u += w_eps
 // (control.py:126), shift (control.py:148-149) and the next launch's fp32
-// per-step constants.  u_cur[ch]: this thread's cur->u value idx = tid + ch kCT,
-// read at kernel entry.
+// per-step constants.  u4: chain_nominal_prefetch's values.
+//
+// The four windows of a thread (t - 5 .. t + 4 for t = t0 .. t0 + 3) share the 7 values t0 - 2 .. t0 + 4:
+// those are sorted once (16 comparators), and each window's median — scipy's median of 10, the upper one
+// (rank 5, as median10) — is the 6th smallest of that sorted A and the window's 3 other values sorted as B:
+// min(A5, max(A4, B0), max(A3, B1), max(A2, B2)) (the k-th smallest of two sorted lists is the least
+// max(A_i, B_j) over i + j = k).  80 min / max for the four windows against 4 x 58 with median10, and one
+// pass of the workgroup instead of four; the same element is selected, so the same bits.
 template <int N>
-__device__ void chain_update_block(ChainStep* nxt, const ChainConst& c, CScratch& sm, const double (&u_cur)[kCMaxCh]) {
+__device__ void chain_update_block(ChainStep* nxt, const ChainConst& c, CScratch& sm, const double (&u4)[kMedRun]) {
     const int tid = threadIdx.x, T = c.T;
+    const int q = tid / N, d = tid - q * N, t0 = kMedRun * q;
+    if (t0 < T) {
+        double e[13];   // t0 - 5 .. t0 + 7, reflected at both ends (T >= 5: one reflection)
 #pragma unroll
-    for (int ch = 0; ch < kCMaxCh; ++ch) {
-        const int idx = tid + ch * kCT;
-        if (idx < T * N) sm.unew[idx] = u_cur[ch] + median_at(sm, idx / N, idx % N, T, N);
+        for (int i = 0; i < 13; ++i) {
+            int m = t0 - 5 + i;
+            m = m < 0 ? -m - 1 : m;
+            m = m >= T ? 2 * T - 1 - m : m;
+            m = min(max(m, 0), T - 1);   // only windows past T (never written) read a clamped value
+            e[i] = sm.weps[m * N + d];
+        }
+#define CX(v, i, j) { const double lo = min_raw_f64(v[i], v[j]), hi = max_raw_f64(v[i], v[j]); v[i] = lo; v[j] = hi; }
+        double A[7] = {e[3], e[4], e[5], e[6], e[7], e[8], e[9]};
+        CX(A, 0, 6) CX(A, 2, 3) CX(A, 4, 5) CX(A, 0, 2) CX(A, 1, 4) CX(A, 3, 6) CX(A, 0, 1) CX(A, 2, 5)
+        CX(A, 3, 4) CX(A, 1, 2) CX(A, 4, 6) CX(A, 2, 3) CX(A, 4, 5) CX(A, 1, 2) CX(A, 3, 4) CX(A, 5, 6)
+#pragma unroll
+        for (int j = 0; j < kMedRun; ++j) {
+            // window t0 + j: e[j .. j + 9]; besides A, e[j .. 2] and e[10 .. 9 + j]
+            double B[3];
+#pragma unroll
+            for (int k = 0; k < 3; ++k) B[k] = e[j + k < 3 ? j + k : j + k + 7];
+            CX(B, 0, 1) CX(B, 1, 2) CX(B, 0, 1)
+            const double med = min_raw_f64(min_raw_f64(A[5], max_raw_f64(A[4], B[0])),
+                                           min_raw_f64(max_raw_f64(A[3], B[1]), max_raw_f64(A[2], B[2])));
+            if (t0 + j < T) sm.unew[(t0 + j) * N + d] = u4[j] + med;
+        }
+#undef CX
     }
     __syncthreads();
     if (tid < N) nxt->u_first[tid] = sm.unew[tid];
     if (tid == 0) nxt->eta = sm.eta;
-    if (tid < T) {
-        const int src = tid + 1 < T ? tid + 1 : T - 1;
+    // row t of the shifted nominal and its a_t = (gamma u_t)^T Sigma^-1: two threads a row, in different waves
+    // (h wave-uniform), the first taking d < 4
+    const int t = tid % kMaxT;
+    if (t < T) {
+        const int src = t + 1 < T ? t + 1 : T - 1;
         double u[N];
 #pragma unroll
-        for (int d = 0; d < N; ++d) {
-            u[d] = sm.unew[src * N + d];
-            nxt->u[tid][d] = u[d];
-            nxt->ua[tid][d] = (float)u[d];
-        }
-#pragma unroll
-        for (int d = 0; d < N; ++d) {
+        for (int dd = 0; dd < N; ++dd) u[dd] = sm.unew[src * N + dd];
+        auto put = [&](int dd) {   // dd a compile-time constant at every call (sig_inv stays in SGPRs)
+            nxt->u[t][dd] = u[dd];
+            nxt->ua[t][dd] = (float)u[dd];
             double a = 0.0;
 #pragma unroll
-            for (int e = 0; e < N; ++e) a += (c.gamma * u[e]) * c.sig_inv[e * N + d];
-            nxt->ua[tid][kCMax + d] = (float)a;
-            nxt->a[tid][d] = a;
+            for (int e = 0; e < N; ++e) a += (c.gamma * u[e]) * c.sig_inv[e * N + dd];
+            nxt->ua[t][kCMax + dd] = (float)a;
+            nxt->a[t][dd] = a;
+        };
+        if (__builtin_amdgcn_readfirstlane(tid) < kMaxT) {
+#pragma unroll
+            for (int dd = 0; dd < (N < 4 ? N : 4); ++dd) put(dd);
+        } else {
+#pragma unroll
+            for (int dd = 4; dd < N; ++dd) put(dd);
         }
     }
 }
@@ -890,12 +943,8 @@ __global__ __launch_bounds__(kCT) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
     STAMP(9, (unsigned long long)__builtin_amdgcn_s_getreg(0xF814));   // XCC_ID
 #endif
     const unsigned tag_v = POLL ? __hip_atomic_load(epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) + 1u : 0u;
-    double u_cur[kCMaxCh];
-#pragma unroll
-    for (int ch = 0; ch < kCMaxCh; ++ch) {
-        const int idx = tid + ch * kCT;
-        u_cur[ch] = ((flags & MPPI_FLAG_FUSED_UPDATE) && idx < T * N) ? st->u[idx / N][idx % N] : 0.0;
-    }
+    double u_cur[kMedRun];
+    chain_nominal_prefetch<N>(st, T, flags & MPPI_FLAG_FUSED_UPDATE, u_cur);
     double S = 0.0;
     if constexpr (F64) {
         S = chain_horizon_f64<N>(c, st, (cdouble*)(dyn + kDynF64Off), noise, k, exf, s_wind, slots);
@@ -1167,12 +1216,8 @@ __global__ __launch_bounds__(kCT) void chain_merge_kernel(const ChainConst c, co
                                                           int n, double* w_eps_out, ChainStep* nxt, unsigned flags) {
     __shared__ CScratch sm;
     const int tid = threadIdx.x, T = c.T;
-    double u_cur[kCMaxCh];
-#pragma unroll
-    for (int ch = 0; ch < kCMaxCh; ++ch) {
-        const int idx = tid + ch * kCT;
-        u_cur[ch] = ((flags & MPPI_FLAG_FUSED_UPDATE) && idx < T * N) ? cur->u[idx / N][idx % N] : 0.0;
-    }
+    double u_cur[kMedRun];
+    chain_nominal_prefetch<N>(cur, T, flags & MPPI_FLAG_FUSED_UPDATE, u_cur);
     const RowGeo geo(T * N);
     const __amdgpu_buffer_rsrc_t r = rows_rsrc(parts, n * geo.stride * 8);
     merge_rows_block<kCT, kCMaxCh, true, false>(r, 0, n, geo, c.inv_lambda, sm, nullptr, 0, nullptr, w_eps_out, 0u,

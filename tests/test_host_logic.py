@@ -267,3 +267,37 @@ def test_sampled_readback_buffers_are_never_shared_with_a_live_array():
     assert np.all(a3 == 3.25) and np.all(a4 == 4.25) and np.all(v == 2.25)
     a6 = rb(torch.zeros((3, 5, 4)))                # K changed: new buffers, held arrays intact
     assert a6.shape == (3, 5, 4) and np.all(a3 == 3.25) and np.all(v == 2.25)
+
+
+# the chain's fused update (mppi_chain.hip chain_update_block): four consecutive windows of scipy's median of 10
+# from one sorted 7-value core; restated here against scipy.ndimage.median_filter (control.py:319-327)
+_SORT7 = [(0, 6), (2, 3), (4, 5), (0, 2), (1, 4), (3, 6), (0, 1), (2, 5), (3, 4), (1, 2), (4, 6), (2, 3), (4, 5),
+          (1, 2), (3, 4), (5, 6)]
+
+
+def _sliding_median10(col):
+    T = len(col)
+    out = np.empty(T)
+    for t0 in range(0, T, 4):
+        idx = np.arange(t0 - 5, t0 + 8)
+        idx = np.where(idx < 0, -idx - 1, idx)
+        idx = np.where(idx >= T, 2 * T - 1 - idx, idx)
+        e = col[np.clip(idx, 0, T - 1)]
+        A = list(e[3:10])
+        for i, j in _SORT7:
+            A[i], A[j] = min(A[i], A[j]), max(A[i], A[j])
+        for j in range(4):
+            if t0 + j < T:
+                B = sorted(e[[k if k < 3 else k + 7 for k in range(j, j + 3)]])
+                out[t0 + j] = min(A[5], max(A[4], B[0]), max(A[3], B[1]), max(A[2], B[2]))
+    return out
+
+
+@pytest.mark.parametrize("T", [5, 6, 7, 9, 32, 127, 128])
+def test_chain_sliding_median_equals_scipy(T):
+    from scipy.ndimage import median_filter
+    rng = np.random.default_rng(T)
+    for x in (rng.standard_normal((T, 7)), rng.integers(-3, 4, (T, 7)).astype(float)):   # ties included
+        ref = median_filter(x, size=(10, 1), mode="reflect")
+        got = np.stack([_sliding_median10(x[:, d]) for d in range(7)], axis=1)
+        assert np.array_equal(got, ref)
