@@ -301,3 +301,17 @@ def test_chain_sliding_median_equals_scipy(T):
         ref = median_filter(x, size=(10, 1), mode="reflect")
         got = np.stack([_sliding_median10(x[:, d]) for d in range(7)], axis=1)
         assert np.array_equal(got, ref)
+
+
+# the rank-5 selection network measured for median10 (the full 10-sort minus 5 comparators)
+_SEL10 = [(4, 9), (3, 8), (2, 7), (1, 6), (0, 5), (1, 4), (6, 9), (0, 3), (5, 8), (0, 2), (3, 6), (2, 4), (5, 7), (8, 9),
+          (1, 2), (4, 6), (7, 8), (3, 5), (2, 5), (6, 8), (4, 7), (6, 7), (5, 6), (4, 5)]
+
+
+def test_median10_selection_network_is_rank5():
+    import itertools
+    for bits in itertools.product([0, 1], repeat=10):   # 0-1 principle
+        v = list(bits)
+        for i, j in _SEL10:
+            v[i], v[j] = min(v[i], v[j]), max(v[i], v[j])
+        assert v[5] == sorted(bits)[5]
