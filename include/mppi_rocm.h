@@ -80,6 +80,13 @@ typedef struct {
 
 typedef struct mppi_ctx mppi_ctx;
 
+/* Fill *cfg with the defaults a C caller should start from before setting its
+ * fields: every field zero except param_gamma = NaN (gamma = lambda (1 - alpha),
+ * control.py:45) and arm = sys_params.py:1-13 with the cost's kinematics lengths
+ * self.l1 = self.l2 = 1 (control.py:55-56).  A config zeroed with memset or
+ * `= {0}` instead has gamma = 0 (no control-cost term).  No device call. */
+void mppi_config_init(mppi_config *cfg);
+
 /* Context: device scratch (workgroup partial slabs, arrival counter, step
  * parameter block) is allocated here; no call below allocates.  Fails with
  * MPPI_E_SINGULAR for a singular Sigma. */
@@ -325,6 +332,11 @@ typedef struct {
 } mppi_chain_config;
 
 typedef struct mppi_chain_ctx mppi_chain_ctx;
+
+/* As mppi_config_init for the chain: every field zero except param_gamma = NaN
+ * (lambda (1 - alpha)) and chain.g = 9.81 (sys_params.py:13); the caller sets n,
+ * the link parameters, Sigma and the rest.  No device call. */
+void mppi_chain_config_init(mppi_chain_config *cfg);
 
 /* control.py:21-65 with the chain model; MPPI_E_SINGULAR if Sigma is not SPD. */
 int mppi_chain_ctx_create(const mppi_chain_config *cfg, int device, void *stream, mppi_chain_ctx **out);

@@ -44,6 +44,7 @@ EXPORTS = (
     "mppi_chain_get_weighted_noise", "mppi_chain_get_nominal", "mppi_chain_rollout_traj",
     "mppi_chain_noise_philox", "mppi_chain_sync", "mppi_chain_debug_set_buffer", "mppi_chain_debug_slots",
     "mppi_chain_wait_outputs", "mppi_chain_optimal_traj_host", "mppi_chain_last_eta",
+    "mppi_config_init", "mppi_chain_config_init",
 )
 
 
@@ -166,6 +167,8 @@ def open_library(path: str):
         "mppi_chain_wait_outputs": ([vp, dp, dp, dp], C.c_int),
         "mppi_chain_optimal_traj_host": ([vp, dp, dp, dp], C.c_int),
         "mppi_chain_last_eta": ([vp, dp], C.c_int),
+        "mppi_config_init": ([C.POINTER(ConfigC)], None),
+        "mppi_chain_config_init": ([C.POINTER(ChainConfigC)], None),
     }
     for name, (args, res) in sig.items():
         if not hasattr(L, name):   # an older diagnostic build (tools/ab.py); load() checks the product's exports

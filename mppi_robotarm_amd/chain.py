@@ -546,6 +546,11 @@ class ChainMPPIController:
         try:
             return self._device_step(prec, x0, window, u, epsilon, step)
         except N.ExchangeError:
+            # every rank re-runs the same step (a rank whose verdict differed would pair its retry with the
+            # others' next step)
+            if not same_on_all_ranks(("exchange retry", step), self.process_group):
+                raise RuntimeError("multi-GPU exchange: the ranks disagree on the failed step; "
+                                   "their nominals can no longer be kept in step") from None
             # a late rank is the ranks' property, not one engine's: every engine takes the all-gather from now on
             self._x_failed = True
             self._xmode = "rccl"

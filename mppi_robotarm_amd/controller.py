@@ -209,6 +209,7 @@ class MPPIControllerForPathTracking:
             raise ValueError("exchange must be 'auto', 'launch' or 'rccl'")
         self.exchange = exchange
         self._xmode = None             # multi-GPU exchange in use: "launch" / "rccl" (decided at the first step)
+        self._x_failed = False         # an in-launch exchange failed (a late rank): the all-gather for good
         self._lanes_per_sample = lanes_per_sample
         self._device = device
         self._engine = None
@@ -288,7 +289,7 @@ class MPPIControllerForPathTracking:
             raise RuntimeError("ranks disagree on the noise stream: every rank must seed np.random identically "
                                "(and pass the same seed / K / T)")
         mode = "rccl"
-        if self.exchange != "rccl":
+        if self.exchange != "rccl" and not self._x_failed:   # after a failed exchange: the all-gather for good
             ok = attach_exchange(eng, pg)
             ok = ok and check_exchange(eng, self._noise_dev, self._partial, self._gathered, pg)
             if not ok and self.exchange == "launch":
@@ -311,16 +312,23 @@ class MPPIControllerForPathTracking:
     # ------------------------------------------------------------ API
     def calc_control_input(self, observed_x: np.ndarray) -> Tuple[float, np.ndarray]:
         """calculate optimal control input (control.py:67-152)"""
-        if self.process_group is not None and self._xmode == "launch":
+        if self.process_group is not None and (self._xmode == "launch" or (
+                self._xmode is None and self.exchange != "rccl" and not self._x_failed)):
             # the in-launch exchange can fail on a late rank (ExchangeError on every rank of the step, no update
             # applied anywhere): every rank then restores what the call changed and runs it again over the
-            # all-gather, which waits for the late rank, and stays on it
+            # all-gather, which waits for the late rank, and stays on it.  The first call is covered too (it
+            # picks the exchange and then runs its step in-launch).
             saved = (self.prev_waypoints_idx, self._step_count,
                      np.random.get_state() if self.noise_source == "numpy" else None)
             try:
                 return self._calc_control_input(observed_x)
             except _native.ExchangeError:
                 self.prev_waypoints_idx, self._step_count, rng = saved
+                # the ranks re-run the same step: a rank whose verdict differed (it saw the step fail while the
+                # others applied it) would pair its retry's all-gather with their next step
+                if not same_on_all_ranks(("exchange retry", self._step_count), self.process_group):
+                    raise RuntimeError("multi-GPU exchange: the ranks disagree on the failed step; "
+                                       "their nominals can no longer be kept in step") from None
                 if rng is not None:
                     np.random.set_state(rng)
                 self._exchange_failed()
@@ -335,6 +343,7 @@ class MPPIControllerForPathTracking:
         """After an ExchangeError (every rank): the collective exchange from now on, no native tick, and the
         device noise drawn again for the step (the tick queues the next step's draw into the same buffer)."""
         self._xmode = "rccl"
+        self._x_failed = True
         self._fast = None
         self._bound = None
         self._noise_ready = None

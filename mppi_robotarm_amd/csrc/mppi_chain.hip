@@ -1423,9 +1423,11 @@ int chain_auto_lps(int K_local, bool f64) {
 }
 
 int check_tmo(mppi_chain_ctx* c) {
-    const unsigned v = c->h_tmo ? __atomic_load_n(c->h_tmo, __ATOMIC_ACQUIRE) : 0u;
+    // tmo[0]: a local hand-off gave up (kTmoLocal); tmo[1]: the exchange's verdict bits (mppi_device.h)
+    const unsigned v = c->h_tmo ? __atomic_load_n(c->h_tmo, __ATOMIC_ACQUIRE) | __atomic_load_n(c->h_tmo + 1, __ATOMIC_ACQUIRE)
+                                : 0u;
     if (!v) return MPPI_OK;
-    *c->h_tmo = 0;
+    c->h_tmo[0] = c->h_tmo[1] = 0;
     if (v == kTmoExchange) {   // as the 2-link engine's check_timeout: the nominal before the launch
         if (c->x_flipped) c->cur ^= 1;
         c->x_flipped = false;
@@ -1436,13 +1438,23 @@ int check_tmo(mppi_chain_ctx* c) {
                                      "rank of this step; no rank applied the update (run the step again)");
     }
     // an aborted merge left the running minimum set: clear it for the next launch
-    (void)hipMemsetAsync(c->d_runmin, 0xFF, sizeof(unsigned long long), c->stream);
+    if (v & kTmoLocal) (void)hipMemsetAsync(c->d_runmin, 0xFF, sizeof(unsigned long long), c->stream);
+    if (v & kTmoSplit)
+        return fail(MPPI_E_HIP, "multi-GPU exchange: this rank had every row but not every rank's verdict within "
+                                "the bound; other ranks may have applied the step, so it cannot be re-run");
     return fail(MPPI_E_HIP, "in-launch hand-off timed out (workgroups not co-resident?); results invalid");
 }
 
 }  // namespace
 
 extern "C" {
+
+void mppi_chain_config_init(mppi_chain_config* cfg) {
+    if (!cfg) return;
+    memset(cfg, 0, sizeof(*cfg));
+    cfg->param_gamma = NAN;   // lambda (1 - alpha), control.py:45
+    cfg->chain.g = 9.81;      // sys_params.py:13
+}
 
 int mppi_chain_ctx_create(const mppi_chain_config* cfg, int device, void* stream, mppi_chain_ctx** out) {
     if (!cfg || !out) return fail(MPPI_E_ARG, "null argument");
@@ -1629,7 +1641,7 @@ int mppi_chain_ctx_create(const mppi_chain_config* cfg, int device, void* stream
         (e = hipDeviceSynchronize()) != hipSuccess)
         return cleanup_fail(fail(MPPI_E_HIP, std::string("allocation: ") + hipGetErrorString(e)));
     memset(c->h_step, 0, sizeof(ChainStep));
-    *c->h_tmo = 0;
+    c->h_tmo[0] = c->h_tmo[1] = 0;
     c->d_epoch = c->d_counter + ngroups + 1;
     *out = c;
     return MPPI_OK;

@@ -434,6 +434,9 @@ __device__ __forceinline__ double gran_val(u32x4 x) {
 // Bounded spins: ~1 s of polling, then the hand-off reports a timeout (host
 // error word) instead of hanging the GPU; results of that launch are invalid.
 constexpr unsigned kSpinMax = 1u << 20;
+// The host-mapped timeout words: tmo[0] = kTmoLocal (a hand-off of this launch gave up), tmo[1] = the
+// exchange's verdict bits (kTmoExchange, kTmoSplit below).  Separate words, plain stores (no read-modify-write
+// over the host link), so the exchange's verdict never overwrites a local cause; the host ORs them.
 __device__ __forceinline__ void report_timeout(unsigned* tmo) {
     if (tmo) __hip_atomic_store(tmo, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
 }
@@ -1001,7 +1004,10 @@ struct XDesc {
     unsigned timeout_ticks;        // the exchange polls' bound in s_memrealtime ticks (10 ns; 0: the ~1 s spin
                                    // bound), MPPI_EXCHANGE_TIMEOUT_US at attach
 };
-constexpr unsigned kTmoLocal = 1u, kTmoExchange = 2u;   // host timeout word: in-launch hand-off / exchange
+// host timeout word, cause bits: an in-launch hand-off of this launch timed out (its results are invalid; not
+// retryable) / the step's exchange failed on every rank (retryable over the all-gather) / this rank had every
+// row but not every rank's status in time, so the other ranks may have applied the step (not retryable)
+constexpr unsigned kTmoLocal = 1u, kTmoExchange = 2u, kTmoSplit = 4u;
 __device__ __forceinline__ void st_gran_sys(__amdgpu_buffer_rsrc_t r, int idx, double v, unsigned tag) {
     const unsigned long long b = (unsigned long long)__double_as_longlong(v);
     const u32x4 x = {(unsigned)b, tag, (unsigned)(b >> 32), tag};
@@ -1044,7 +1050,7 @@ __device__ __forceinline__ unsigned exchange_send_merge(const XDesc& x, const Ro
                                             inv_lambda, sm, nullptr, 0, nullptr, w_eps_out, tag, nullptr, dl, &late);
     // this rank's own row is invalid if an in-launch hand-off of this launch timed out
     late = __syncthreads_or(late || (threadIdx.x == 0 && tmo &&
-                                     __hip_atomic_load(tmo, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) == kTmoLocal));
+                                     __hip_atomic_load(tmo, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) != 0u));
     const int sbase = 2 * x.world * stride + par * x.world;   // status granules follow the rows: [parity][rank]
     if ((int)threadIdx.x < x.world)
         st_gran_sys(rows_rsrc(x.peer[threadIdx.x], x.bytes), sbase + x.rank, late ? -1.0 : 1.0, tag);
@@ -1056,7 +1062,7 @@ __device__ __forceinline__ bool exchange_verdict(const XDesc& x, const RowGeo& g
     const int par = (int)(tag & 1u);
     const int sbase = 2 * x.world * geo.stride + par * x.world;
     const int tid = threadIdx.x, lane = tid & 63;
-    bool bad = false;
+    bool bad = false, split = false;
     if (tid < 64) {   // wave 0 polls every rank's status (world <= 64)
         const __amdgpu_buffer_rsrc_t own = rows_rsrc(x.peer[x.rank], x.bytes);
         u32x4 g;
@@ -1069,10 +1075,17 @@ __device__ __forceinline__ bool exchange_verdict(const XDesc& x, const RowGeo& g
             MPPI_SPIN_OR_GIVE_UP_L(spins, dl, nullptr, lane, missing = true);
         }
         bad = __any(lane < x.world && !(gran_ok(g, tag) && gran_val(g) > 0.0)) || missing;
+        // A status that never came while this rank's own is not a -1: the ranks whose statuses all arrived may
+        // have applied the step, so re-running it here would pair this rank's retry with their next step.
+        // Only a rank that reported -1 itself knows every rank fails (each waits for, or times out on, its -1).
+        split = missing && !__any(lane == x.rank && gran_ok(g, tag) && gran_val(g) < 0.0);
     }
     bad = __syncthreads_or(bad);
+    split = __syncthreads_or(split);
     if (tid == 0) {
-        if (bad) __hip_atomic_store(tmo, kTmoExchange, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        if (bad)
+            __hip_atomic_store(tmo + 1, split ? kTmoExchange | kTmoSplit : kTmoExchange, __ATOMIC_RELAXED,
+                               __HIP_MEMORY_SCOPE_SYSTEM);
         *x.epoch = tag;
     }
     return !bad;

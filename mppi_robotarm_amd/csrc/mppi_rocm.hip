@@ -855,9 +855,11 @@ int occupancy(int* per_cu) {
 }
 
 int check_timeout(mppi_ctx* c) {
-    const unsigned v = c->h_tmo ? __atomic_load_n(c->h_tmo, __ATOMIC_ACQUIRE) : 0u;
+    // tmo[0]: a local hand-off gave up (kTmoLocal); tmo[1]: the exchange's verdict bits (mppi_device.h)
+    const unsigned v = c->h_tmo ? __atomic_load_n(c->h_tmo, __ATOMIC_ACQUIRE) | __atomic_load_n(c->h_tmo + 1, __ATOMIC_ACQUIRE)
+                                : 0u;
     if (!v) return MPPI_OK;
-    *c->h_tmo = 0;
+    c->h_tmo[0] = c->h_tmo[1] = 0;
     if (v == kTmoExchange) {
         // every rank of the step reports it and none applied the update: back to the nominal before the launch
         if (c->x_flipped) c->cur ^= 1;
@@ -867,6 +869,9 @@ int check_timeout(mppi_ctx* c) {
         return fail(MPPI_E_EXCHANGE, "multi-GPU exchange: a rank's row did not arrive within the bound on every "
                                      "rank of this step; no rank applied the update (run the step again)");
     }
+    if (v & kTmoSplit)
+        return fail(MPPI_E_HIP, "multi-GPU exchange: this rank had every row but not every rank's verdict within "
+                                "the bound; other ranks may have applied the step, so it cannot be re-run");
     return fail(MPPI_E_HIP, "in-launch hand-off timed out (workgroups not co-resident?); results invalid");
 }
 
@@ -893,6 +898,13 @@ int auto_lps(int K_local) {
 }  // namespace
 
 extern "C" {
+
+void mppi_config_init(mppi_config* cfg) {
+    if (!cfg) return;
+    memset(cfg, 0, sizeof(*cfg));
+    cfg->param_gamma = NAN;   // lambda (1 - alpha), control.py:45
+    cfg->arm = mppi_arm_params{1.0, 1.0, 1.0, 1.0, 0.5, 0.5, 9.81, 1.0, 1.0};   // sys_params.py:1-13, control.py:55-56
+}
 
 const char* mppi_last_error(void) { return mppi_host::last_error(); }
 
@@ -1026,7 +1038,7 @@ int mppi_ctx_create(const mppi_config* cfg, int device, void* stream, mppi_ctx**
         return cleanup_fail(fail(MPPI_E_HIP, std::string("allocation: ") + hipGetErrorString(e)));
     memset(c->h_step, 0, sizeof(DevStep));
     memset(c->h_dout, 0, (4 + 2 * kMaxT) * sizeof(double));
-    *c->h_tmo = 0;
+    c->h_tmo[0] = c->h_tmo[1] = 0;
     c->d_epoch = c->d_counter + ngroups + 1;
     *out = c;
     return MPPI_OK;

@@ -41,7 +41,7 @@ def _upload_std(eng, noise, z: torch.Tensor, out: torch.Tensor, perm) -> torch.E
         stage = eng._noise_stage = torch.empty((kl, T, du), dtype=torch.float64, device=eng.device)
     stage.copy_(zz, non_blocking=True)
     ev = torch.cuda.Event()
-    ev.record()
+    ev.record(eng.stream)   # the engine's stream (its device need not be the current one)
     key = (noise.src.tobytes(), noise.scale.tobytes(), noise.mean.tobytes())
     if getattr(eng, "_std_key", None) != key:
         eng._std_key = key

@@ -110,6 +110,28 @@ def test_constants_match_header():
     assert re.search(r"#define MPPI_FLAG_FUSED_UPDATE\s+1u", text) and N.MPPI_FLAG_FUSED_UPDATE == 1
 
 
+def test_config_init_defaults():
+    """mppi_config_init / mppi_chain_config_init (host-only calls): a C caller that starts from them gets
+    gamma = lambda (1 - alpha) (the NaN sentinel, control.py:45) and sys_params.py's arm, not the gamma = 0 of
+    a memset / `= {0}` config."""
+    import math
+    from mppi_robotarm_amd import _native as N
+    from mppi_robotarm_amd.params import ArmParams
+    lib = N.load()
+    cfg = N.ConfigC(param_gamma=1.0)
+    cfg.K_local, cfg.delta_t, cfg.sigma[3] = 7, 0.5, 2.0
+    lib.mppi_config_init(C.byref(cfg))
+    assert math.isnan(cfg.param_gamma)
+    assert [getattr(cfg.arm, f) for f, _ in N.ArmParamsC._fields_] == [
+        getattr(ArmParams(), f) for f, _ in N.ArmParamsC._fields_]
+    assert (cfg.K_local, cfg.T, cfg.delta_t, cfg.lanes_per_sample, list(cfg.sigma)) == (0, 0, 0.0, 0, [0.0] * 4)
+    ch = N.ChainConfigC(param_gamma=1.0)
+    ch.precision, ch.chain.n = 1, 7
+    lib.mppi_chain_config_init(C.byref(ch))
+    assert math.isnan(ch.param_gamma) and ch.chain.g == 9.81
+    assert (ch.precision, ch.chain.n, ch.lanes_per_sample, ch.chain.m[0]) == (0, 0, 0, 0.0)
+
+
 def test_missing_library_fails_loudly(monkeypatch, tmp_path):
     """No silent fallback: a missing .so raises at load time."""
     from mppi_robotarm_amd import _native as N
