@@ -49,33 +49,49 @@ from mppi_robotarm_amd.params import ArmParams, X0_RUNPY  # noqa: E402
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md, chip-level parameters)
 BYTES_PER_STATE_STEP = 8  # fp32 eps[t][k][0:2] read once
 C5_BYTES_PER_STATE_STEP = 28  # fp32 eps[t][0:7][k] read once ("C5 (du=7): 28 B/state-step")
-# VALU issue roofline (SURVEY §8d asks for it beside the HBM one).  MI355X_MICROARCH.md: 256 CUs x 4 SIMD-32,
-# 2.4 GHz max clock; a SIMD issues one wave64 VALU instruction per 2 cycles, one wave alone one per 4 cycles
-# (row 'vector-instruction ISSUE cost'; transcendentals 8).
+# VALU issue roofline (SURVEY §8d asks for it beside the HBM one), priced against this chip's measured issue
+# rates: tools/ubench_issue.hip (profiles/ubench_issue.json) times independent instruction streams of the c3
+# horizon loop's mix with 1, 2 and 4 waves on every SIMD of the chip (the clock the chip picks under that load),
+# in nanoseconds per wave-instruction.  One wave alone on its SIMD (the c3 launch: 1024 waves on 1024 SIMDs)
+# issues the mix at one instruction per ~2.9 ns (~7 cycles at the 2.39 GHz s_memtime rate the same run reports);
+# the SIMD saturates near one per ~1.8 ns with four.  The guide's 2- and 4-cycle figures are single-class
+# streams; the mix (packed FMAs, transcendentals) is what the loop issues.
 SIMDS = 1024
-CLOCK_HZ = 2.4e9
-SIMD_ISSUE_CYC = 2.0
-LONE_WAVE_ISSUE_CYC = 4.0
+UBENCH_JSON = os.path.join(ROOT, "profiles", "ubench_issue.json")
+
+
+def issue_ceilings(path=UBENCH_JSON):
+    """(lone-wave, SIMD-saturated) ns per instruction per SIMD for the c3 mix, from the committed ubench run."""
+    try:
+        rows = json.load(open(path))["rows"]
+        mix = {r["waves_per_simd"]: r["event_ns_per_inst_wave"] for r in rows if r["op"] == "c3_mix"}
+        return mix[1], min(ns / w for w, ns in mix.items())
+    except Exception:
+        return None
 
 
 def valu_roofline(tj, kern_ms):
-    """VALU issue roofline of the rollout launch from the PMC count in the traffic json (SQ_INSTS_VALU, whole
-    device, per launch; tools/traffic_summary.py) and this run's kernel time."""
+    """VALU issue roofline of the rollout launch: the PMC count in the traffic json (SQ_INSTS_VALU, whole device,
+    per launch; tools/traffic_summary.py) over this run's kernel time, per SIMD, against the measured issue rates
+    of issue_ceilings() (profiles/ubench_issue.json)."""
     n = tj.get("valu_insts_per_launch") if tj else None
     waves = tj.get("waves_per_launch") if tj else None
-    if not n or not waves:
+    ceil = issue_ceilings()
+    if not n or not waves or ceil is None:
         return None
-    cycles = kern_ms * 1e-3 * CLOCK_HZ
-    per_simd = n / SIMDS   # wave-instructions each SIMD issues (waves are spread evenly, <= 1 workgroup per CU)
-    waves_per_simd = waves / SIMDS
-    achieved = per_simd / cycles   # wave-instructions per SIMD-cycle
-    out = {"bound": "valu-issue", "achieved": achieved, "peak": 1.0 / SIMD_ISSUE_CYC,
-           "unit": "wave-instr/SIMD/cycle", "frac": achieved * SIMD_ISSUE_CYC,
-           "waves_per_simd": waves_per_simd, "valu_insts_per_launch": n,
-           "source": "SQ_INSTS_VALU (" + str(tj.get("source", "")).split("; ")[-1] + "), live kernel time, 2.4 GHz"}
-    if waves_per_simd <= 1.0:
-        # a lone wave cannot use the SIMD's full rate: its own ceiling is one instruction per 4 cycles
-        out["frac_one_wave_ceiling"] = achieved * LONE_WAVE_ISSUE_CYC
+    lone_ns, simd_ns = ceil
+    # wave-instructions each busy SIMD issues (waves are spread evenly, <= 1 workgroup per CU; c2's 512 waves
+    # leave half the SIMDs empty)
+    per_simd = n / min(waves, SIMDS)
+    achieved = per_simd / (kern_ms * 1e6)   # wave-instructions per SIMD per ns
+    out = {"bound": "valu-issue", "achieved": achieved, "peak": 1.0 / simd_ns, "unit": "wave-instr/SIMD/ns",
+           "frac": achieved * simd_ns, "waves_per_simd": waves / SIMDS, "busy_simds": min(waves, SIMDS), "valu_insts_per_launch": n,
+           "source": "SQ_INSTS_VALU (" + str(tj.get("source", "")).split("; ")[-1] + "), live kernel time; peak and "
+                     "lone-wave ceiling: the c3 mix in profiles/ubench_issue.json (tools/ubench_issue.hip)"}
+    if waves / SIMDS <= 1.0:
+        # one wave per SIMD cannot reach the SIMD's rate: its own measured ceiling
+        out["lone_wave_ceiling"] = 1.0 / lone_ns
+        out["frac_one_wave_ceiling"] = achieved * lone_ns
     for key in ("valu_active_frac_of_wave_time", "cycles_per_valu_inst"):
         if tj.get(key) is not None:
             out[key] = tj[key]   # SQ_ACTIVE_INST_VALU of the committed PMC pass (how busy the VALU is)
