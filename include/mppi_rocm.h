@@ -35,6 +35,9 @@ extern "C" {
                                 bound (MPPI_EXCHANGE_TIMEOUT_US, default ~1 s) on some rank of the
                                 step; every rank of the step reports it and none applied the
                                 update (the nominal is the one before the step)              */
+#define MPPI_E_RETRY -6      /* mppi_np_draw_result: the draw generated fewer accepted   */
+                             /* polar attempts than it needed; nothing was written and   */
+                             /* the state is the caller's (draw on the host instead)     */
 #define MPPI_E_PATH_END -4   /* mppi_dropin_tick: the updated waypoint index reached   */
                              /* the end of the path (control.py:76-78: the reference   */
                              /* prints "[ERROR] ..." and raises IndexError)           */
@@ -389,6 +392,69 @@ int mppi_chain_debug_set_buffer(mppi_chain_ctx *ctx, void *dbg_dev);
  * slots_dev int32 [K_local][T].  7-link contexts only.  The parity tests use it
  * to recompute a sample's fp64 cost with the device's own picks. */
 int mppi_chain_debug_slots(mppi_chain_ctx *ctx, const float *noise_dev, double *S_dev, int *slots_dev);
+
+/* ------------------------------------------------------------------------
+ * The reference's own noise on the device: NumPy's legacy global-RNG stream of
+ * np.random.multivariate_normal(mu, Sigma, (K, T)) (control.py:154-164), the
+ * drop-in's default noise="numpy", generated bit for bit — the same values
+ * and the same RNG state left behind as NumPy's draw — when Sigma's transform
+ * is a scaled column permutation (run.py's 20 I, the chain's diagonal Sigma;
+ * mppi_robotarm_amd/hostrng.py monomial_transform).  Replaces the host draw
+ * (hostrng / np_legacy_gauss.c) and the upload of its 67 MB at config 3.
+ *
+ * Host inputs the device cannot make: the MT19937 jump polynomials x^J mod P
+ * (np_legacy_gauss.c mppi_np_jump_poly) and glibc's log constants, read from
+ * the process's libm and checked against its log() (mppi_np_log_params).
+ * ------------------------------------------------------------------------ */
+#define MPPI_NP_POLY_WORDS 312          /* 64-bit words of a jump polynomial (degree < 19937) */
+#define MPPI_NP_LOG_DATA 274            /* doubles of the log constants (np_glibc_log.h)       */
+#define MPPI_NP_MAX_DU 8                /* components per step                                 */
+#define MPPI_NP_MAX_STREAMS 1024        /* generator streams of one draw                       */
+#define MPPI_NP_MAX_NORMALS 2147483647LL
+
+/* NumPy's RandomState.get_state()[1:5]: the MT19937 key array, its position,
+ * and the cached Gaussian of legacy_gauss. */
+typedef struct {
+    unsigned key[624];
+    int pos;
+    int has_gauss;
+    double gauss;
+} mppi_np_state;
+
+/* Where the draw goes: the standard normals z of shape (K, T, du) (C order,
+ * n = K T du of them) become out(t, k, d) = (float)(z[k][t][src[d]] * scale[d]
+ * + mean[d]) (fp64 multiply and add, each rounded, as NumPy's np.dot with one
+ * nonzero per column and `x += mean`; then the fp32 rounding of the upload),
+ * stored at out_dev[t * stride_t + (k - k_offset) * stride_k + d * stride_d]
+ * for the samples k_offset <= k < k_offset + K_local of this rank (every rank
+ * draws the whole stream, as every rank of the reference's loop would). */
+typedef struct {
+    void *out_dev;
+    long long K, T;
+    int du;
+    long long k_offset, K_local;
+    long long stride_t, stride_k, stride_d;
+    int src[MPPI_NP_MAX_DU];
+    double scale[MPPI_NP_MAX_DU];
+    double mean[MPPI_NP_MAX_DU];
+} mppi_np_target;
+
+typedef struct mppi_np_ctx mppi_np_ctx;
+
+/* log_params: MPPI_NP_LOG_DATA doubles (mppi_np_log_params). */
+int mppi_np_ctx_create(int device, const double *log_params, mppi_np_ctx **out);
+void mppi_np_ctx_destroy(mppi_np_ctx *ctx);
+/* The generator partition of a draw of n normals from a state at position
+ * pos: *streams streams of *block_stride key arrays; stream s >= 1 starts from
+ * the jump polynomial x^(624 (block_stride s - 1)) mod P. */
+int mppi_np_plan(const mppi_np_ctx *ctx, long long n, int pos, int has_gauss, int *block_stride, int *streams);
+/* Upload the polynomials of streams 1 .. streams - 1 (words = MPPI_NP_POLY_WORDS each, row-major). */
+int mppi_np_set_jumps(mppi_np_ctx *ctx, int block_stride, int streams, const unsigned long long *polys, int words);
+/* Queue the draw of n normals from state *st on `stream` (a hipStream_t) into tgt;
+ * asynchronous: mppi_np_draw_result waits for it and returns the state the
+ * draw leaves (MPPI_E_RETRY: nothing written, the state untouched). */
+int mppi_np_draw(mppi_np_ctx *ctx, void *stream, const mppi_np_state *st, long long n, const mppi_np_target *tgt);
+int mppi_np_draw_result(mppi_np_ctx *ctx, mppi_np_state *st_out);
 
 #ifdef __cplusplus
 }

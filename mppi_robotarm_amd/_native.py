@@ -20,6 +20,7 @@ MPPI_E_HIP = -2
 MPPI_E_SINGULAR = -3
 MPPI_E_PATH_END = -4
 MPPI_E_EXCHANGE = -5
+MPPI_E_RETRY = -6
 MPPI_FLAG_FUSED_UPDATE = 1
 MPPI_FLAG_EXCHANGE = 2
 MPPI_FLAG_HOST_OUT = 4
@@ -45,6 +46,8 @@ EXPORTS = (
     "mppi_chain_noise_philox", "mppi_chain_sync", "mppi_chain_debug_set_buffer", "mppi_chain_debug_slots",
     "mppi_chain_wait_outputs", "mppi_chain_optimal_traj_host", "mppi_chain_last_eta",
     "mppi_config_init", "mppi_chain_config_init",
+    "mppi_np_ctx_create", "mppi_np_ctx_destroy", "mppi_np_plan", "mppi_np_set_jumps", "mppi_np_draw",
+    "mppi_np_draw_result",
 )
 
 
@@ -53,6 +56,23 @@ class DropinBindingC(C.Structure):
                 ("fk_l2", C.c_double), ("x0", C.c_void_p), ("idx", C.c_void_p), ("u", C.c_void_p),
                 ("traj", C.c_void_p), ("noise_dev", C.c_void_p), ("next_noise_dev", C.c_void_p),
                 ("S_dev", C.c_void_p), ("seed", C.c_ulonglong)]
+
+
+NP_MAX_DU = 8
+NP_LOG_DATA = 274
+NP_POLY_WORDS = 312
+
+
+class NpStateC(C.Structure):
+    """mppi_np_state: NumPy's RandomState.get_state()[1:5]."""
+    _fields_ = [("key", C.c_uint * 624), ("pos", C.c_int), ("has_gauss", C.c_int), ("gauss", C.c_double)]
+
+
+class NpTargetC(C.Structure):
+    _fields_ = [("out_dev", C.c_void_p), ("K", C.c_longlong), ("T", C.c_longlong), ("du", C.c_int),
+                ("k_offset", C.c_longlong), ("K_local", C.c_longlong), ("stride_t", C.c_longlong),
+                ("stride_k", C.c_longlong), ("stride_d", C.c_longlong), ("src", C.c_int * NP_MAX_DU),
+                ("scale", C.c_double * NP_MAX_DU), ("mean", C.c_double * NP_MAX_DU)]
 
 
 class ArmParamsC(C.Structure):
@@ -168,6 +188,12 @@ def open_library(path: str):
         "mppi_chain_optimal_traj_host": ([vp, dp, dp, dp], C.c_int),
         "mppi_chain_last_eta": ([vp, dp], C.c_int),
         "mppi_config_init": ([C.POINTER(ConfigC)], None),
+        "mppi_np_ctx_create": ([C.c_int, vp, C.POINTER(vp)], C.c_int),
+        "mppi_np_ctx_destroy": ([vp], None),
+        "mppi_np_plan": ([vp, C.c_longlong, C.c_int, C.c_int, ip, ip], C.c_int),
+        "mppi_np_set_jumps": ([vp, C.c_int, C.c_int, vp, C.c_int], C.c_int),
+        "mppi_np_draw": ([vp, vp, C.POINTER(NpStateC), C.c_longlong, C.POINTER(NpTargetC)], C.c_int),
+        "mppi_np_draw_result": ([vp, C.POINTER(NpStateC)], C.c_int),
         "mppi_chain_config_init": ([C.POINTER(ChainConfigC)], None),
     }
     for name, (args, res) in sig.items():

@@ -84,11 +84,21 @@ def _pinned_zbuf(buf, ev, n: int):
     return buf, None
 
 
+class DeviceDrawn:
+    """The reference's draw (control.py:84) made on the device straight into the engine's noise buffer
+    (engine.NpDeviceStream); `check` is the value the ranks compare (from the RNG state the draw left)."""
+
+    def __init__(self, check: float):
+        self.check = check
+
+
 def _noise_check(epsilon, K: int, T: int, du: int):
     """The value the ranks compare to agree on the noise stream: eps[0, 0, 0] + eps[-1, -1, -1] of the draw
-    (an array, a hostrng.StdNoise, or None for device noise)."""
+    (an array, a hostrng.StdNoise, or None for device noise), or the device draw's state check."""
     if epsilon is None:
         return None
+    if isinstance(epsilon, DeviceDrawn):
+        return epsilon.check
     if isinstance(epsilon, hostrng.StdNoise):
         return epsilon.eps(0, 0, 0) + epsilon.eps(K - 1, T - 1, du - 1)
     return float(epsilon[0, 0, 0] + epsilon[-1, -1, -1])
@@ -175,6 +185,7 @@ class MPPIControllerForPathTracking:
             process_group=None,
             exchange: str = "auto",
             host_update: bool = False,
+            numpy_noise_on_device: bool = True,
     ) -> None:
         self.dim_x = 4
         self.dim_u = 2
@@ -223,6 +234,8 @@ class MPPIControllerForPathTracking:
         self._last_sampled = None      # the previous call's sampled_traj_list (_fresh_sampled)
         self._sampled_pool = PinnedReadback()   # sampled_traj_list's read-back buffers (_sampled_host)
         self._fast = None              # what the last bound tick checked (calc_control_input's fast test)
+        self.numpy_noise_on_device = numpy_noise_on_device   # noise="numpy": the same stream drawn on the device
+        self._npdev = None             # its engine.NpDeviceStream (False: unavailable here)
 
     @property
     def host_update(self) -> bool:
@@ -370,7 +383,9 @@ class MPPIControllerForPathTracking:
             raise ValueError("zero-size array to reduction operation minimum which has no identity")
 
         if self.noise_source == "numpy":
-            epsilon = self._reference_noise()
+            epsilon = self._device_reference_noise()
+            if epsilon is None:
+                epsilon = self._reference_noise()
         else:
             epsilon = None
             self._check_sigma(self.Sigma, self.dim_u)
@@ -378,7 +393,9 @@ class MPPIControllerForPathTracking:
         if key != self._engine_built_for:
             np.linalg.inv(self.Sigma)                      # LinAlgError exactly as control.py:106
         eng = self._get_engine(key)
-        if isinstance(epsilon, hostrng.StdNoise):
+        if isinstance(epsilon, DeviceDrawn):
+            pass                                           # already in self._noise_dev
+        elif isinstance(epsilon, hostrng.StdNoise):
             self._zbuf_ev = eng.upload_std_noise(epsilon, self._zbuf, self._noise_dev)
         elif epsilon is not None:
             lo = eng.k_offset
@@ -599,6 +616,56 @@ class MPPIControllerForPathTracking:
                                               self._zbuf_numpy(self.K * self.T * self.dim_u))
         return std if std is not None else self._calc_epsilon(self.Sigma, self.K, self.T, self.dim_u)
 
+    def _device_reference_noise(self):
+        """control.py:84 on the device: the reference's own stream (np.random.multivariate_normal on the legacy
+        global RNG, NumPy's values and the state it leaves) drawn straight into the engine's noise buffer
+        (engine.NpDeviceStream, include/mppi_rocm.h mppi_np_*), when _calc_epsilon is the reference's and Sigma's
+        transform is a scaled column permutation (run.py's 20 I).  None: not applicable here (the host path
+        draws then; nothing was drawn).  A singular Sigma takes the host path too, which draws before
+        np.linalg.inv raises, as control.py:84,106 do."""
+        if not self.numpy_noise_on_device or self._npdev is False:
+            return None
+        cls = MPPIControllerForPathTracking
+        if "_calc_epsilon" in self.__dict__ or type(self)._calc_epsilon is not cls._calc_epsilon:
+            return None
+        sig = self.Sigma
+        if not (isinstance(sig, np.ndarray) and sig.shape == (self.dim_u, self.dim_u)):
+            return None                                    # the host path prints and raises as the reference
+        n = int(self.K) * int(self.T) * self.dim_u
+        if n < hostrng._MIN_NORMALS or n >= 2 ** 31:
+            return None
+        state = np.random.get_state()
+        if state[0] != "MT19937":
+            return None
+        plan = hostrng.monomial_plan(np.full((self.dim_u), 0.0), sig)
+        if plan is None:
+            return None
+        key = self._engine_key()
+        if key != self._engine_built_for:
+            try:
+                np.linalg.inv(sig)
+            except np.linalg.LinAlgError:
+                return None
+        eng = self._get_engine(key)
+        if self._npdev is None:
+            try:
+                from .engine import NpDeviceStream
+                self._npdev = NpDeviceStream(eng.device)
+            except (RuntimeError, OSError):
+                self._npdev = False
+                return None
+        if not plan[3]:
+            import warnings
+            warnings.warn("covariance is not symmetric positive-semidefinite.", RuntimeWarning)   # NumPy's
+        eng._sync_stream()
+        self._npdev.draw(state, (int(self.K), int(self.T), self.dim_u), plan, self._noise_dev, eng.stream.cuda_stream,
+                         eng.k_offset, eng.K_local, (eng.K_local * self.dim_u, self.dim_u, 1))
+        new = self._npdev.result()
+        if new is None:
+            return None
+        np.random.set_state(new)
+        return DeviceDrawn(float(np.sum(new[1][:16], dtype=np.float64)) + new[2])
+
     def _zbuf_numpy(self, n: int) -> np.ndarray:
         """The page-locked buffer of the standard normals (>= n values), free to be rewritten: the DMA of the
         previous draw out of it has completed."""
@@ -651,6 +718,9 @@ class MPPIControllerForPathTracking:
         if self._engine is not None:
             self._engine.close()
             self._engine = None
+        if self._npdev:
+            self._npdev.close()
+        self._npdev = None
         self._noise_ready = None       # the next engine's noise buffer is fresh: draw again
         self._engine_built_for = None
         self._bound = None

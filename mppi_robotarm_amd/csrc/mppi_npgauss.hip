@@ -1,0 +1,590 @@
+// mppi_npgauss.hip — the reference's noise draw, NumPy's legacy global-RNG Gaussian stream, generated on the
+// MI355X bit for bit (values and the RNG state left behind).
+//
+// control.py:163 draws eps with np.random.multivariate_normal(mu, Sigma, (K, T)) on the legacy RandomState:
+// MT19937 words -> NumPy's legacy doubles (two words each) -> the polar method with rejection (legacy_gauss:
+// one attempt = four words, accepted when 0 < r2 < 1, then a pair f x2, f x1 with f = sqrt(-2 log r2 / r2))
+// -> the Sigma transform.  Sequential in NumPy; here every phase is parallel:
+//
+//   np_seq_kernel    the first 34 key arrays (blocks) after the state's: the word windows the jumps read.
+//   np_jump_kernel   the state of every generator stream's start: MT19937 is linear over GF(2), so the block
+//                    J words on is sum_d phi_d F^d(key) with phi = x^J mod P (P: the characteristic
+//                    polynomial, found and powered on the host, np_legacy_gauss.c) and F^d(key) the window
+//                    [d, d + 624) of the word sequence: each output word is the XOR of ~10k sequence words at
+//                    phi's set bits (Haramoto et al. 2008, the window form).  The sequence sits in LDS.
+//   np_gen_kernel    one workgroup per stream twists its range of blocks; a block's 624 words are each a
+//                    function of the previous block alone (the twist's in-block dependencies unrolled: up to
+//                    three tempering-free mix terms per word), so one barrier per block.
+//   np_count_kernel  accepted attempts per workgroup (2048 consecutive attempts each).
+//   np_scan_kernel   their exclusive prefix: the index of each workgroup's first pair.
+//   np_write_kernel  the accepted attempts again, each pair's place from the prefix; f with glibc's log
+//                    reproduced (np_glibc_log.h), IEEE division and square root; the transform of the drop-in
+//                    (a scaled column permutation, hostrng.monomial_transform) and the rounding to fp32, into
+//                    the engine's noise layout for this rank's samples.
+//   np_state_kernel  the state NumPy leaves: the key array holding the last consumed word, its position, and
+//                    the cached Gaussian of an odd count.
+//
+// No contraction anywhere in this file: NumPy's r2 = x1 x1 + x2 x2, the transform's multiply and add are
+// separately rounded; the log's fused multiply-adds are explicit.
+//
+// C ABI: include/mppi_rocm.h (mppi_np_*).  Reference: control.py:154-164.
+#include <hip/hip_runtime.h>
+
+#include <stdint.h>
+#include <string.h>
+
+#include <string>
+#include <vector>
+
+#include "mppi_host.h"
+#include "mppi_rocm.h"
+#include "np_glibc_log.h"
+
+#pragma clang fp contract(off)
+
+namespace {
+
+using mppi_host::fail;
+
+constexpr int kN = 624, kM = 397;
+constexpr uint32_t kMatA = 0x9908b0dfu, kUp = 0x80000000u, kLo = 0x7fffffffu;
+constexpr int kDeg = 19937;
+constexpr int kPolyWords = MPPI_NP_POLY_WORDS;        // 312 x 64 bits: a polynomial of degree < 19937
+constexpr int kSeqBlocks = (kDeg + kN) / kN + 1;      // 34: the windows d + j < 19937 + 624 of the jumps
+constexpr int kNT = 256;                              // threads of the twist / attempt kernels
+constexpr int kJT = 320;                              // threads of a jump workgroup (2 per stream: 640 >= 624)
+constexpr int kJBatch = 16;                           // set bits of a jump polynomial read per batch
+constexpr int kSeqPad = kSeqBlocks * kN;              // list padding: s_seq[kSeqPad + j] = 0 for j < 624
+constexpr int kJListStride = ((kDeg + 1 + kJBatch - 1) / kJBatch) * kJBatch;   // uint16 per stream's list
+constexpr int kAttPerThread = 8;
+constexpr int kAttPerWG = kNT * kAttPerThread;
+constexpr int kScanT = 1024;
+
+__device__ __forceinline__ uint32_t mt_mix(uint32_t a, uint32_t b) {
+    const uint32_t y = (a & kUp) | (b & kLo);
+    return (y >> 1) ^ ((0u - (y & 1u)) & kMatA);
+}
+
+// The key array after o (LDS) into k (LDS).  NumPy's twist (in place, word order) is k[i] = o[i + 397] ^
+// mix(o[i], o[i + 1]) for i < 227, k[i] = k[i - 227] ^ mix(o[i], o[i + 1]) up to 622, and k[623] =
+// k[396] ^ mix(o[623], k[0]); substituting the earlier k's, every word depends on o only.
+__device__ __forceinline__ void twist_block(const uint32_t* o, uint32_t* k) {
+    for (int i = threadIdx.x; i < kN; i += blockDim.x) {
+        uint32_t v;
+        if (i < kN - kM) {
+            v = o[i + kM] ^ mt_mix(o[i], o[i + 1]);
+        } else if (i < 2 * (kN - kM)) {
+            v = o[i + 170] ^ mt_mix(o[i - 227], o[i - 226]) ^ mt_mix(o[i], o[i + 1]);
+        } else if (i < kN - 1) {
+            v = o[i - 57] ^ mt_mix(o[i - 454], o[i - 453]) ^ mt_mix(o[i - 227], o[i - 226]) ^ mt_mix(o[i], o[i + 1]);
+        } else {
+            const uint32_t k0 = o[kM] ^ mt_mix(o[0], o[1]);
+            const uint32_t k396 = o[566] ^ mt_mix(o[169], o[170]) ^ mt_mix(o[396], o[397]);
+            v = k396 ^ mt_mix(o[623], k0);
+        }
+        k[i] = v;
+    }
+}
+
+__device__ __forceinline__ uint32_t temper(uint32_t y) {
+    y ^= (y >> 11);
+    y ^= (y << 7) & 0x9d2c5680u;
+    y ^= (y << 15) & 0xefc60000u;
+    y ^= (y >> 18);
+    return y;
+}
+
+__device__ __forceinline__ double legacy_double(uint32_t a, uint32_t b) {
+    return ((double)(a >> 5) * 67108864.0 + (double)(b >> 6)) / 9007199254740992.0;
+}
+
+// attempt a: words [base + 4a, base + 4a + 4) of the untempered block sequence
+__device__ __forceinline__ void attempt(const uint32_t* __restrict__ words, long long base, long long a, double& x1,
+                                       double& x2, double& r2) {
+    const uint32_t* w = words + base + 4 * a;
+    const uint32_t w0 = temper(w[0]), w1 = temper(w[1]), w2 = temper(w[2]), w3 = temper(w[3]);
+    x1 = 2.0 * legacy_double(w0, w1) - 1.0;
+    x2 = 2.0 * legacy_double(w2, w3) - 1.0;
+    r2 = x1 * x1 + x2 * x2;
+}
+
+__device__ __forceinline__ bool accepted(double r2) { return r2 < 1.0 && r2 != 0.0; }
+
+struct NpResult {
+    long long last_attempt;   // the attempt of the last wanted pair
+    double last_fx1;          // its f x1 (cached by an odd count)
+    long long total;          // accepted attempts among the generated ones
+    int status;               // 1: fewer than the pairs wanted (not written; the host draws again)
+    int pad;
+};
+
+struct NpShape {
+    float* out;
+    unsigned per_k, du;         // T du normals per sample, du per step
+    unsigned k_offset, K_local;
+    long long st, sk, sd;       // out element (t, k - k_offset, d)
+    int src[MPPI_NP_MAX_DU];
+    double scale[MPPI_NP_MAX_DU], mean[MPPI_NP_MAX_DU];
+};
+
+// ------------------------------------------------------------------ generation
+__global__ __launch_bounds__(kNT) void np_seq_kernel(const uint32_t* __restrict__ key, uint32_t* __restrict__ seq) {
+    __shared__ uint32_t buf[2][kN];
+    for (int i = threadIdx.x; i < kN; i += kNT) {
+        buf[0][i] = key[i];
+        seq[i] = key[i];
+    }
+    __syncthreads();
+    for (int b = 1; b < kSeqBlocks; ++b) {
+        twist_block(buf[(b - 1) & 1], buf[b & 1]);
+        __syncthreads();   // the next twist writes the buffer this one read; the stores below read the other
+        for (int i = threadIdx.x; i < kN; i += kNT) seq[(size_t)b * kN + i] = buf[b & 1][i];
+    }
+}
+
+// stream s = blockIdx.y + 1 starts at block P s: its jump polynomial is x^(624 (P s - 1)) mod P, giving block
+// P s - 1 up to the 31 low bits of its word 0 (outside the 19937-bit state); np_gen_kernel twists once more.
+// The polynomial comes as the list of its set bits (mppi_np_set_jumps), padded to a multiple of kJBatch with
+// kSeqPad (a window of zero words past the sequence), so each batch's LDS reads are issued together.
+__global__ __launch_bounds__(kJT) void np_jump_kernel(const uint32_t* __restrict__ seq, const uint16_t* __restrict__ bits,
+                                                      const int* __restrict__ nbits, uint32_t* __restrict__ jumped) {
+    extern __shared__ uint32_t s_seq[];   // kSeqBlocks x 624 words, then 624 zero words: 87 KB
+    const uint4* src = reinterpret_cast<const uint4*>(seq);
+    for (int i = threadIdx.x; i < kSeqBlocks * kN / 4; i += kJT) reinterpret_cast<uint4*>(s_seq)[i] = src[i];
+    for (int i = kSeqBlocks * kN + threadIdx.x; i < kSeqPad + kN; i += kJT) s_seq[i] = 0u;
+    __syncthreads();
+    const int j = blockIdx.x * kJT + threadIdx.x;
+    const int jj = j < kN ? j : kN - 1;   // the idle lanes read in bounds and store nothing
+    const int nb = nbits[blockIdx.y];     // a multiple of kJBatch
+    const uint4* lst = reinterpret_cast<const uint4*>(bits + (size_t)blockIdx.y * kJListStride);
+    uint32_t acc0 = 0, acc1 = 0;
+    for (int b = 0; b < nb; b += kJBatch) {
+        // kJBatch positions (the same for every lane: scalar loads), then their reads, then the XORs
+        uint32_t d[kJBatch / 2];
+#pragma unroll
+        for (int q = 0; q < kJBatch / 8; ++q) {
+            const uint4 v = lst[b / 8 + q];
+            d[4 * q + 0] = __builtin_amdgcn_readfirstlane(v.x);
+            d[4 * q + 1] = __builtin_amdgcn_readfirstlane(v.y);
+            d[4 * q + 2] = __builtin_amdgcn_readfirstlane(v.z);
+            d[4 * q + 3] = __builtin_amdgcn_readfirstlane(v.w);
+        }
+        uint32_t r[kJBatch];
+#pragma unroll
+        for (int q = 0; q < kJBatch / 2; ++q) {
+            r[2 * q] = s_seq[(d[q] & 0xFFFFu) + jj];
+            r[2 * q + 1] = s_seq[(d[q] >> 16) + jj];
+        }
+#pragma unroll
+        for (int q = 0; q < kJBatch; q += 2) {
+            acc0 ^= r[q];
+            acc1 ^= r[q + 1];
+        }
+    }
+    if (j < kN) jumped[(size_t)blockIdx.y * kN + j] = acc0 ^ acc1;
+}
+
+// stream s: blocks [1 + P s, min(1 + P (s + 1), nblk)); stream 0 also writes block 0 (the state's key array)
+__global__ __launch_bounds__(kNT) void np_gen_kernel(const uint32_t* __restrict__ key, const uint32_t* __restrict__ jumped,
+                                                     uint32_t* __restrict__ words, int P, int nblk) {
+    __shared__ uint32_t buf[2][kN];
+    const int s = blockIdx.x;
+    const int b0 = 1 + P * s, b1 = min(1 + P * (s + 1), nblk);
+    if (s == 0) {
+        for (int i = threadIdx.x; i < kN; i += kNT) {
+            buf[0][i] = key[i];
+            words[i] = key[i];
+        }
+        __syncthreads();
+    } else {
+        for (int i = threadIdx.x; i < kN; i += kNT) buf[1][i] = jumped[(size_t)(s - 1) * kN + i];
+        __syncthreads();
+        twist_block(buf[1], buf[0]);   // block P s, exactly
+        __syncthreads();
+    }
+    int cur = 0;
+    for (int b = b0; b < b1; ++b) {
+        twist_block(buf[cur], buf[cur ^ 1]);
+        __syncthreads();
+        cur ^= 1;
+        uint32_t* dst = words + (size_t)b * kN;
+        for (int i = threadIdx.x; i < kN; i += kNT) dst[i] = buf[cur][i];
+    }
+}
+
+// ------------------------------------------------------------------ the polar method
+__device__ __forceinline__ int block_sum(int v, int* s_tmp) {
+    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    if (lane == 0) s_tmp[wave] = v;
+    __syncthreads();
+    int t = 0;
+    for (int w = 0; w < (int)(blockDim.x >> 6); ++w) t += s_tmp[w];
+    return t;
+}
+
+__global__ __launch_bounds__(kNT) void np_count_kernel(const uint32_t* __restrict__ words, long long base,
+                                                       long long A, int* __restrict__ counts) {
+    __shared__ int s_tmp[kNT / 64];
+    const long long a0 = (long long)blockIdx.x * kAttPerWG + (long long)threadIdx.x * kAttPerThread;
+    int c = 0;
+    for (int q = 0; q < kAttPerThread; ++q) {
+        if (a0 + q >= A) break;
+        double x1, x2, r2;
+        attempt(words, base, a0 + q, x1, x2, r2);
+        c += accepted(r2);
+    }
+    c = block_sum(c, s_tmp);
+    if (threadIdx.x == 0) counts[blockIdx.x] = c;
+}
+
+// exclusive prefix of the workgroup counts (one workgroup); the total and the sufficiency check
+__global__ __launch_bounds__(kScanT) void np_scan_kernel(const int* __restrict__ counts, long long* __restrict__ offsets,
+                                                         int nwg, long long pairs, NpResult* res) {
+    __shared__ long long s_part[kScanT];
+    const int per = (nwg + kScanT - 1) / kScanT;
+    const int i0 = threadIdx.x * per, i1 = min(i0 + per, nwg);
+    long long sum = 0;
+    for (int i = i0; i < i1; ++i) sum += counts[i];
+    s_part[threadIdx.x] = sum;
+    __syncthreads();
+    for (int o = 1; o < kScanT; o <<= 1) {   // inclusive scan of the per-thread sums
+        const long long v = threadIdx.x >= (unsigned)o ? s_part[threadIdx.x - o] : 0;
+        __syncthreads();
+        s_part[threadIdx.x] += v;
+        __syncthreads();
+    }
+    long long run = s_part[threadIdx.x] - sum;
+    for (int i = i0; i < i1; ++i) {
+        offsets[i] = run;
+        run += counts[i];
+    }
+    if (threadIdx.x == kScanT - 1) {
+        res->total = s_part[kScanT - 1];
+        res->status = s_part[kScanT - 1] < pairs ? 1 : 0;
+        res->last_attempt = -1;
+    }
+}
+
+// z[m] (standard normal m of the draw) through the transform into the engine's layout, if sample k is this rank's
+__device__ __forceinline__ void emit(const NpShape& sh, unsigned m, double z) {
+    const unsigned k = m / sh.per_k, r = m - k * sh.per_k;
+    const unsigned t = r / sh.du, dd = r - t * sh.du;
+    if (k - sh.k_offset >= sh.K_local) return;   // unsigned: also k < k_offset
+    const long long at = (long long)t * sh.st + (long long)(k - sh.k_offset) * sh.sk;
+    for (unsigned d = 0; d < sh.du; ++d)
+        if ((unsigned)sh.src[d] == dd) sh.out[at + (long long)d * sh.sd] = (float)(z * sh.scale[d] + sh.mean[d]);
+}
+
+__global__ __launch_bounds__(kNT) void np_write_kernel(const uint32_t* __restrict__ words, long long base, long long A,
+                                                       const long long* __restrict__ offsets,
+                                                       const double* __restrict__ logd, NpShape sh, long long pairs,
+                                                       long long n, int o, double cached, NpResult* res) {
+    __shared__ double s_log[NPLOG_NDATA];
+    __shared__ int s_tmp[kNT / 64];
+    for (int i = threadIdx.x; i < NPLOG_NDATA; i += kNT) s_log[i] = logd[i];
+    if (res->status) return;   // uniform: every thread returns
+    const long long a0 = (long long)blockIdx.x * kAttPerWG + (long long)threadIdx.x * kAttPerThread;
+    unsigned mask = 0;
+    for (int q = 0; q < kAttPerThread; ++q) {
+        if (a0 + q >= A) break;
+        double x1, x2, r2;
+        attempt(words, base, a0 + q, x1, x2, r2);
+        mask |= (unsigned)accepted(r2) << q;
+    }
+    // this thread's first pair: the workgroup's offset + the accepted attempts of the threads before it
+    const int c = __popc(mask);
+    int incl = c;
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    for (int d = 1; d < 64; d <<= 1) {
+        const int v = __shfl_up(incl, d);
+        if (lane >= d) incl += v;
+    }
+    if (lane == 63) s_tmp[wave] = incl;
+    __syncthreads();   // also publishes s_log
+    long long q = offsets[blockIdx.x] + incl - c;
+    for (int w = 0; w < wave; ++w) q += s_tmp[w];
+    if (blockIdx.x == 0 && threadIdx.x == 0 && o) emit(sh, 0u, cached);   // the cached Gaussian comes first
+    while (mask && q < pairs) {
+        const int b = __ffs(mask) - 1;
+        mask &= mask - 1;
+        double x1, x2, r2;
+        attempt(words, base, a0 + b, x1, x2, r2);
+        const double f = sqrt(-2.0 * np_glibc_log(s_log, r2) / r2);
+        const double g1 = f * x1, g2 = f * x2;   // legacy_gauss returns f x2 and caches f x1
+        const unsigned m = (unsigned)(o + 2 * q);
+        emit(sh, m, g2);
+        if ((long long)m + 1 < n) emit(sh, m + 1, g1);
+        if (q == pairs - 1) {
+            res->last_attempt = a0 + b;
+            res->last_fx1 = g1;
+        }
+        ++q;
+    }
+}
+
+// the state NumPy leaves: the key array holding the last consumed word and the position after it
+__global__ __launch_bounds__(kNT) void np_state_kernel(const uint32_t* __restrict__ words, long long base,
+                                                       const NpResult* res, long long need, mppi_np_state* st) {
+    if (res->status || res->last_attempt < 0) return;
+    const long long qw = base + 4 * (res->last_attempt + 1) - 1;
+    const long long blk = qw / kN;
+    for (int i = threadIdx.x; i < kN; i += kNT) st->key[i] = words[blk * kN + i];
+    if (threadIdx.x == 0) {
+        st->pos = (int)(qw - blk * kN) + 1;
+        st->has_gauss = (int)(need & 1);
+        st->gauss = (need & 1) ? res->last_fx1 : 0.0;
+    }
+}
+
+}  // namespace
+
+struct NpHostOut {
+    mppi_np_state st;
+    int status;
+};
+
+struct mppi_np_ctx {
+    int device = 0;
+    double* d_log = nullptr;
+    uint32_t* d_key = nullptr;      // the draw's starting key array
+    uint32_t* d_seq = nullptr;      // kSeqBlocks blocks
+    uint16_t* d_bits = nullptr;     // (streams - 1) jump polynomials of block stride P, as set-bit lists
+    int* d_nbits = nullptr;
+    int poly_P = 0, poly_streams = 0;
+    uint32_t* d_jumped = nullptr;
+    uint32_t* d_words = nullptr;
+    size_t words_cap = 0;           // words
+    int* d_counts = nullptr;
+    long long* d_offsets = nullptr;
+    size_t counts_cap = 0;          // workgroups
+    NpResult* d_res = nullptr;
+    mppi_np_state* d_state = nullptr;
+    NpHostOut* h_out = nullptr;     // page-locked: the draw's state and status read-back
+    uint32_t* h_key = nullptr;          // page-locked staging of the starting key array
+    hipEvent_t done = nullptr;
+    bool pending = false;
+};
+
+namespace {
+
+#define NP_CHECK(expr)                                                                    \
+    do {                                                                                  \
+        hipError_t e_ = (expr);                                                           \
+        if (e_ != hipSuccess) return fail(MPPI_E_HIP, std::string(#expr) + ": " + hipGetErrorString(e_)); \
+    } while (0)
+
+struct Plan {
+    long long need, pairs, A, nblk;
+    int P, streams;
+};
+
+// attempts generated: 4/3 of the pairs plus 4096 (acceptance pi/4: 1.27 attempts per pair expected), as the
+// host path (np_legacy_gauss.c); the block stride P of the streams from a cost model of the two parallel
+// phases measured on MI355X: jumps, LDS-bound, ~40 us per round of 128 streams; twists ~0.13 us per block
+Plan make_plan(long long n, int pos, int has_gauss) {
+    Plan p;
+    p.need = n - (has_gauss ? 1 : 0);
+    p.pairs = (p.need + 1) / 2;
+    p.A = p.pairs + p.pairs / 3 + 4096;
+    p.nblk = (pos + 4 * p.A + kN - 1) / kN + 1;
+    double best = 1e30;
+    p.P = 64;
+    p.streams = 1;
+    for (int P = 64; P <= (1 << 20); P <<= 1) {
+        const long long streams = (p.nblk - 1 + P - 1) / P;
+        if (streams > MPPI_NP_MAX_STREAMS) continue;
+        const double cost = (double)((streams - 1 + 127) / 128) * 40.0 + P * 0.13;
+        if (cost < best) {
+            best = cost;
+            p.P = P;
+            p.streams = (int)(streams < 1 ? 1 : streams);
+        }
+    }
+    return p;
+}
+
+}  // namespace
+
+extern "C" {
+
+int mppi_np_ctx_create(int device, const double* log_params, mppi_np_ctx** out) {
+    if (!out || !log_params) return fail(MPPI_E_ARG, "null argument");
+    *out = nullptr;
+    NP_CHECK(hipSetDevice(device));
+    mppi_np_ctx* c = new mppi_np_ctx();
+    c->device = device;
+    hipError_t e;
+    if ((e = hipMalloc(&c->d_log, NPLOG_NDATA * sizeof(double))) != hipSuccess ||
+        (e = hipMemcpy(c->d_log, log_params, NPLOG_NDATA * sizeof(double), hipMemcpyHostToDevice)) != hipSuccess ||
+        (e = hipMalloc(&c->d_key, kN * sizeof(uint32_t))) != hipSuccess ||
+        (e = hipMalloc(&c->d_seq, (size_t)kSeqBlocks * kN * sizeof(uint32_t))) != hipSuccess ||
+        (e = hipMalloc(&c->d_res, sizeof(NpResult))) != hipSuccess ||
+        (e = hipMalloc(&c->d_state, sizeof(mppi_np_state))) != hipSuccess ||
+        (e = hipHostMalloc(&c->h_out, sizeof(NpHostOut), hipHostMallocDefault)) != hipSuccess ||
+        (e = hipHostMalloc(&c->h_key, kN * sizeof(uint32_t), hipHostMallocDefault)) != hipSuccess ||
+        (e = hipEventCreateWithFlags(&c->done, hipEventDisableTiming)) != hipSuccess) {
+        mppi_np_ctx_destroy(c);
+        return fail(MPPI_E_HIP, std::string("mppi_np_ctx_create: ") + hipGetErrorString(e));
+    }
+    if (hipFuncSetAttribute((const void*)np_jump_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
+                            (int)((kSeqPad + kN) * sizeof(uint32_t))) != hipSuccess) {
+        mppi_np_ctx_destroy(c);
+        return fail(MPPI_E_HIP, "mppi_np_ctx_create: the jump kernel's LDS");
+    }
+    *out = c;
+    return MPPI_OK;
+}
+
+void mppi_np_ctx_destroy(mppi_np_ctx* c) {
+    if (!c) return;
+    if (c->pending && c->done) (void)hipEventSynchronize(c->done);
+    (void)hipFree(c->d_log);
+    (void)hipFree(c->d_key);
+    (void)hipFree(c->d_seq);
+    (void)hipFree(c->d_bits);
+    (void)hipFree(c->d_nbits);
+    (void)hipFree(c->d_jumped);
+    (void)hipFree(c->d_words);
+    (void)hipFree(c->d_counts);
+    (void)hipFree(c->d_offsets);
+    (void)hipFree(c->d_res);
+    (void)hipFree(c->d_state);
+    if (c->h_out) (void)hipHostFree(c->h_out);
+    if (c->h_key) (void)hipHostFree(c->h_key);
+    if (c->done) (void)hipEventDestroy(c->done);
+    delete c;
+}
+
+int mppi_np_plan(const mppi_np_ctx* c, long long n, int pos, int has_gauss, int* block_stride, int* streams) {
+    if (!c || !block_stride || !streams) return fail(MPPI_E_ARG, "null argument");
+    if (n < 2 || n > MPPI_NP_MAX_NORMALS || pos < 0 || pos > kN) return fail(MPPI_E_ARG, "mppi_np_plan: bad n or pos");
+    const Plan p = make_plan(n, pos, has_gauss);
+    *block_stride = p.P;
+    *streams = p.streams;
+    return MPPI_OK;
+}
+
+int mppi_np_set_jumps(mppi_np_ctx* c, int block_stride, int streams, const unsigned long long* polys, int words) {
+    if (!c || (streams > 1 && !polys)) return fail(MPPI_E_ARG, "null argument");
+    if (words != kPolyWords || block_stride < 1 || streams < 1 || streams > MPPI_NP_MAX_STREAMS)
+        return fail(MPPI_E_ARG, "mppi_np_set_jumps: bad stride, stream count or polynomial size");
+    NP_CHECK(hipSetDevice(c->device));
+    if (c->pending) NP_CHECK(hipEventSynchronize(c->done));   // the buffers may be in use by the last draw
+    (void)hipFree(c->d_bits);
+    (void)hipFree(c->d_nbits);
+    (void)hipFree(c->d_jumped);
+    c->d_bits = nullptr;
+    c->d_nbits = nullptr;
+    c->d_jumped = nullptr;
+    c->poly_P = c->poly_streams = 0;
+    if (streams > 1) {
+        const size_t ns = (size_t)(streams - 1);
+        std::vector<uint16_t> lists(ns * kJListStride, (uint16_t)kSeqPad);
+        std::vector<int> counts(ns);
+        for (size_t q = 0; q < ns; ++q) {
+            int nb = 0;
+            for (int w = 0; w < kPolyWords; ++w)
+                for (uint64_t m = polys[q * kPolyWords + w]; m; m &= m - 1) {
+                    const int d = 64 * w + __builtin_ctzll(m);
+                    if (d >= kDeg) return fail(MPPI_E_ARG, "mppi_np_set_jumps: a polynomial of degree >= 19937");
+                    lists[q * kJListStride + nb++] = (uint16_t)d;
+                }
+            counts[q] = (nb + kJBatch - 1) / kJBatch * kJBatch;
+        }
+        NP_CHECK(hipMalloc(&c->d_bits, lists.size() * sizeof(uint16_t)));
+        NP_CHECK(hipMemcpy(c->d_bits, lists.data(), lists.size() * sizeof(uint16_t), hipMemcpyHostToDevice));
+        NP_CHECK(hipMalloc(&c->d_nbits, ns * sizeof(int)));
+        NP_CHECK(hipMemcpy(c->d_nbits, counts.data(), ns * sizeof(int), hipMemcpyHostToDevice));
+        NP_CHECK(hipMalloc(&c->d_jumped, ns * kN * sizeof(uint32_t)));
+    }
+    c->poly_P = block_stride;
+    c->poly_streams = streams;
+    return MPPI_OK;
+}
+
+int mppi_np_draw(mppi_np_ctx* c, void* stream, const mppi_np_state* st, long long n, const mppi_np_target* tgt) {
+    if (!c || !st || !tgt || !tgt->out_dev) return fail(MPPI_E_ARG, "null argument");
+    if (n < 2 || n > MPPI_NP_MAX_NORMALS || st->pos < 0 || st->pos > kN)
+        return fail(MPPI_E_ARG, "mppi_np_draw: bad n or state position");
+    if (tgt->du < 1 || tgt->du > MPPI_NP_MAX_DU || tgt->K < 1 || tgt->T < 1 || tgt->K * tgt->T * tgt->du != n ||
+        tgt->k_offset < 0 || tgt->K_local < 0 || tgt->k_offset + tgt->K_local > tgt->K)
+        return fail(MPPI_E_ARG, "mppi_np_draw: the target's (K, T, du) and slice must match n");
+    for (int d = 0; d < tgt->du; ++d)
+        if (tgt->src[d] < 0 || tgt->src[d] >= tgt->du) return fail(MPPI_E_ARG, "mppi_np_draw: bad src");
+    const Plan p = make_plan(n, st->pos, st->has_gauss);
+    if (p.P != c->poly_P || p.streams > c->poly_streams)
+        return fail(MPPI_E_ARG, "mppi_np_draw: the jump polynomials of mppi_np_plan's stride and count are not set");
+    NP_CHECK(hipSetDevice(c->device));
+    hipStream_t s = (hipStream_t)stream;
+    if (c->pending) NP_CHECK(hipEventSynchronize(c->done));
+    const size_t words = (size_t)p.nblk * kN;
+    if (words > c->words_cap) {
+        (void)hipFree(c->d_words);
+        c->d_words = nullptr;
+        c->words_cap = 0;
+        NP_CHECK(hipMalloc(&c->d_words, words * sizeof(uint32_t)));
+        c->words_cap = words;
+    }
+    const long long nwg = (p.A + kAttPerWG - 1) / kAttPerWG;
+    if ((size_t)nwg > c->counts_cap) {
+        (void)hipFree(c->d_counts);
+        (void)hipFree(c->d_offsets);
+        c->d_counts = nullptr;
+        c->d_offsets = nullptr;
+        c->counts_cap = 0;
+        NP_CHECK(hipMalloc(&c->d_counts, nwg * sizeof(int)));
+        NP_CHECK(hipMalloc(&c->d_offsets, nwg * sizeof(long long)));
+        c->counts_cap = (size_t)nwg;
+    }
+    memcpy(c->h_key, st->key, kN * sizeof(uint32_t));
+    NP_CHECK(hipMemcpyAsync(c->d_key, c->h_key, kN * sizeof(uint32_t), hipMemcpyHostToDevice, s));
+    if (p.streams > 1) {
+        hipLaunchKernelGGL(np_seq_kernel, dim3(1), dim3(kNT), 0, s, c->d_key, c->d_seq);
+        hipLaunchKernelGGL(np_jump_kernel, dim3((kN + kJT - 1) / kJT, p.streams - 1), dim3(kJT),
+                           (kSeqPad + kN) * sizeof(uint32_t), s, c->d_seq, c->d_bits, c->d_nbits, c->d_jumped);
+    }
+    hipLaunchKernelGGL(np_gen_kernel, dim3(p.streams), dim3(kNT), 0, s, c->d_key, c->d_jumped, c->d_words, p.P,
+                       (int)p.nblk);
+    hipLaunchKernelGGL(np_count_kernel, dim3((unsigned)nwg), dim3(kNT), 0, s, c->d_words, (long long)st->pos, p.A,
+                       c->d_counts);
+    hipLaunchKernelGGL(np_scan_kernel, dim3(1), dim3(kScanT), 0, s, c->d_counts, c->d_offsets, (int)nwg, p.pairs,
+                       c->d_res);
+    NpShape sh;
+    sh.out = (float*)tgt->out_dev;
+    sh.per_k = (unsigned)(tgt->T * tgt->du);
+    sh.du = (unsigned)tgt->du;
+    sh.k_offset = (unsigned)tgt->k_offset;
+    sh.K_local = (unsigned)tgt->K_local;
+    sh.st = tgt->stride_t;
+    sh.sk = tgt->stride_k;
+    sh.sd = tgt->stride_d;
+    for (int d = 0; d < MPPI_NP_MAX_DU; ++d) {
+        sh.src[d] = d < tgt->du ? tgt->src[d] : 0;
+        sh.scale[d] = d < tgt->du ? tgt->scale[d] : 0.0;
+        sh.mean[d] = d < tgt->du ? tgt->mean[d] : 0.0;
+    }
+    hipLaunchKernelGGL(np_write_kernel, dim3((unsigned)nwg), dim3(kNT), 0, s, c->d_words, (long long)st->pos, p.A,
+                       c->d_offsets, c->d_log, sh, p.pairs, n, st->has_gauss ? 1 : 0, st->gauss, c->d_res);
+    hipLaunchKernelGGL(np_state_kernel, dim3(1), dim3(kNT), 0, s, c->d_words, (long long)st->pos, c->d_res, p.need,
+                       c->d_state);
+    NP_CHECK(hipGetLastError());
+    NP_CHECK(hipMemcpyAsync(&c->h_out->st, c->d_state, sizeof(mppi_np_state), hipMemcpyDeviceToHost, s));
+    NP_CHECK(hipMemcpyAsync(&c->h_out->status, &c->d_res->status, sizeof(int), hipMemcpyDeviceToHost, s));
+    NP_CHECK(hipEventRecord(c->done, s));
+    c->pending = true;
+    return MPPI_OK;
+}
+
+int mppi_np_draw_result(mppi_np_ctx* c, mppi_np_state* st_out) {
+    if (!c || !st_out) return fail(MPPI_E_ARG, "null argument");
+    if (!c->pending) return fail(MPPI_E_ARG, "mppi_np_draw_result: no draw pending");
+    c->pending = false;
+    NP_CHECK(hipEventSynchronize(c->done));
+    if (c->h_out->status != 0)
+        return fail(MPPI_E_RETRY, "mppi_np_draw: fewer accepted attempts than pairs wanted (nothing written)");
+    *st_out = c->h_out->st;
+    return MPPI_OK;
+}
+
+}  // extern "C"

@@ -28,6 +28,8 @@
 // Host code, never on the device path; the Python side (controller.py,
 // legacy_multivariate_normal) does the rest of multivariate_normal with
 // NumPy's own calls.
+#define _GNU_SOURCE
+#include <link.h>
 #include <math.h>
 #include <pthread.h>
 #include <stdio.h>
@@ -38,6 +40,8 @@
 
 #define MT_N 624
 #define MT_M 397
+
+#include "np_glibc_log.h"
 
 // AVX2 instances of the integer-only loops where the CPU has it (the same bits either way)
 #if defined(__x86_64__) && defined(__GNUC__) && !defined(__clang__)
@@ -235,23 +239,37 @@ static int char_poly_init(void) {
     if (L != MT_DEG) return -1;
     memset(g_cp.p, 0, sizeof(g_cp.p));
     g_cp.nterms = 0;
+    int top = 0;
     for (int64_t i = 0; i <= L; ++i)
         if (bit_get(C, i)) {   // c_i x^i  ->  x^(L - i)
             bit_flip(g_cp.p, L - i);
-            if (L - i < MT_DEG) g_cp.terms[g_cp.nterms++] = (int)(L - i);
+            if (L - i < MT_DEG) {
+                g_cp.terms[g_cp.nterms++] = (int)(L - i);
+                if (L - i > top) top = (int)(L - i);
+            }
         }
-    return bit_get(g_cp.p, MT_DEG) && bit_get(g_cp.p, 0) ? 0 : -1;
+    // reduce_mod's word-at-a-time order needs a gap of more than 64 below the leading term (it is 623)
+    return bit_get(g_cp.p, MT_DEG) && bit_get(g_cp.p, 0) && MT_DEG - top > 64 ? 0 : -1;
 }
 
 // a (bits 0 .. 2 MT_DEG, 2 PW words) reduced mod P in place: each set bit i >= MT_DEG is replaced by the
-// terms of P below x^MT_DEG shifted by i - MT_DEG (the leading term cancels it); top down, so bits flipped
-// at or above MT_DEG are handled after.
+// terms of P below x^MT_DEG shifted by i - MT_DEG (the leading term cancels it).  A word at a time, top down:
+// P's highest term below x^MT_DEG is x^19314 (623 below), so the bits a word's high part maps to lie at least
+// 623 positions lower, in words not yet visited (checked when P is found: g_cp.gap).
 static void reduce_mod(uint64_t* a) {
-    for (int64_t i = 2 * MT_DEG; i >= MT_DEG; --i) {
-        if (!bit_get(a, i)) continue;
-        bit_flip(a, i);
-        const int64_t sh = i - MT_DEG;
-        for (int e = 0; e < g_cp.nterms; ++e) bit_flip(a, sh + g_cp.terms[e]);
+    const int64_t w0 = MT_DEG >> 6;
+    for (int64_t w = (2 * MT_DEG) >> 6; w >= w0; --w) {
+        uint64_t v = a[w];
+        if (w == w0) v &= ~0ull << (MT_DEG & 63);   // the bits >= MT_DEG of the lowest such word
+        if (!v) continue;
+        a[w] ^= v;
+        for (int e = 0; e < g_cp.nterms; ++e) {   // v x^(64 w) -> v x^(64 w - MT_DEG + term)
+            const int64_t pos = 64 * w - MT_DEG + g_cp.terms[e];
+            const int64_t q = pos >> 6;
+            const int sh = (int)(pos & 63);
+            a[q] ^= v << sh;
+            if (sh) a[q + 1] ^= v >> (64 - sh);
+        }
     }
 }
 
@@ -626,4 +644,107 @@ int mppi_np_jump_config(int min_blocks) {
     pthread_mutex_unlock(&g_initmu);
     pthread_mutex_unlock(&g_mu);
     return r;
+}
+
+// ------------------------------------------------------------------ the device draw's inputs
+// The device draw of the same stream (mppi_rocm.h mppi_np_*) needs two things only the host has: the jump
+// polynomials (x^J mod P for the block offsets its generator streams start at) and glibc's log constants.
+
+// x^J mod P into out[PW] (bit e = coefficient of x^e); 0, or -1 when the jump machinery is unavailable
+int mppi_np_jump_poly(uint64_t J, uint64_t* out) {
+    pthread_mutex_lock(&g_initmu);
+    jump_init_locked();
+    const int ready = g_cp.ready;
+    pthread_mutex_unlock(&g_initmu);
+    if (ready != 1 || !out) return -1;
+    const uint64_t* p = jump_poly(J);
+    if (!p) return -1;
+    memcpy(out, p, PW * sizeof(uint64_t));
+    return 0;
+}
+
+int mppi_np_poly_words(void) { return PW; }
+
+// glibc's struct log_data in the loaded libm: ln2hi, ln2lo, then poly[5] (poly[0] = -0x1.0000000000001p-1) and
+// poly1[11] (poly1[0] = -0.5) — found by that signature in libm's read-only segments.
+typedef struct {
+    const double* hit[4];
+    int n;
+} LogScan;
+
+static int log_scan_cb(struct dl_phdr_info* info, size_t size, void* data) {
+    (void)size;
+    LogScan* sc = (LogScan*)data;
+    if (!info->dlpi_name || !strstr(info->dlpi_name, "libm.so")) return 0;
+    const double sig[3] = {0x1.62e42fefa3800p-1, 0x1.ef35793c76730p-45, -0x1.0000000000001p-1};
+    for (int h = 0; h < info->dlpi_phnum; ++h) {
+        const ElfW(Phdr)* ph = &info->dlpi_phdr[h];
+        if (ph->p_type != PT_LOAD || !(ph->p_flags & PF_R) || (ph->p_flags & PF_X) || ph->p_memsz < sizeof(sig))
+            continue;
+        const char* b = (const char*)(info->dlpi_addr + ph->p_vaddr);
+        for (size_t o = 0; o + NPLOG_NDATA * sizeof(double) <= ph->p_memsz; o += 8) {
+            if (memcmp(b + o, sig, sizeof(sig)) != 0) continue;
+            const double* d = (const double*)(b + o);
+            if (d[7] == -0.5 && sc->n < 4) sc->hit[sc->n++] = d;
+        }
+    }
+    return 0;
+}
+
+// values the check compares: accepted polar r2 (the draw's domain), the near-1 band, spread exponents
+static double log_check_value(uint64_t* st, int kind) {
+    *st ^= *st << 13;
+    *st ^= *st >> 7;
+    *st ^= *st << 17;
+    const uint64_t r = *st;
+    if (kind == 0) {   // r2 = x1^2 + x2^2 of two legacy doubles, as an accepted attempt makes it
+        const double x1 = 2.0 * legacy_double((uint32_t)r, (uint32_t)(r >> 32)) - 1.0;
+        *st ^= *st << 13;
+        *st ^= *st >> 7;
+        *st ^= *st << 17;
+        const double x2 = 2.0 * legacy_double((uint32_t)*st, (uint32_t)(*st >> 32)) - 1.0;
+        const double r2 = x1 * x1 + x2 * x2;
+        return r2 < 1.0 && r2 != 0.0 ? r2 : 0.5;
+    }
+    if (kind == 1) return 0.93 + (double)(r >> 11) * 0x1p-53 * 0.07;   // [0.93, 1): glibc's near-1 branch
+    const uint64_t e = 1023 - 1 - (r % 105);                            // [2^-105, 1)
+    return nplog_asdouble((e << 52) | (r >> 12));
+}
+
+// The constants of np_glibc_log (NPLOG_NDATA doubles) into out, after np_glibc_log on them equalled libm's
+// log() bit for bit on `samples` inputs of each kind above.  0, or -1 (not found, or a mismatch: the libm in
+// this process is not the variant np_glibc_log reproduces, and the device draw must not be used).
+int mppi_np_log_params(double* out, int samples) {
+    LogScan sc;
+    memset(&sc, 0, sizeof(sc));
+    dl_iterate_phdr(log_scan_cb, &sc);
+    for (int h = 0; h < sc.n; ++h) {
+        const double* D = sc.hit[h];
+        uint64_t st = 0x9E3779B97F4A7C15ull;
+        int ok = 1;
+        for (int kind = 0; kind < 3 && ok; ++kind)
+            for (int i = 0; i < samples; ++i) {
+                volatile double x = log_check_value(&st, kind);   // volatile: log() on run-time values
+                const double a = log(x), b = np_glibc_log(D, x);
+                if (memcmp(&a, &b, 8) != 0) {
+                    ok = 0;
+                    break;
+                }
+            }
+        if (ok) {
+            memcpy(out, D, NPLOG_NDATA * sizeof(double));
+            return 0;
+        }
+    }
+    return -1;
+}
+
+// Tests: np_glibc_log against libm's log on n given values; returns the number that differ
+int64_t mppi_np_log_mismatches(const double* D, const double* x, int64_t n) {
+    int64_t bad = 0;
+    for (int64_t i = 0; i < n; ++i) {
+        const double a = log(x[i]), b = np_glibc_log(D, x[i]);
+        bad += memcmp(&a, &b, 8) != 0;
+    }
+    return bad;
 }

@@ -410,6 +410,83 @@ class RolloutEngine:
             raise ValueError(f"noise must be a contiguous fp32 {(self.T, self.K_local, 2)} tensor on {self.device}")
 
 
+class NpDeviceStream:
+    """The reference's noise draw (control.py:154-164: np.random.multivariate_normal on NumPy's legacy global
+    RandomState) generated on the device bit for bit (include/mppi_rocm.h mppi_np_*): the MT19937 words, the
+    polar method with glibc's log, the Sigma transform (a scaled column permutation) and the fp32 rounding,
+    straight into an engine's noise buffer; the RNG state is read from and written back to np.random, as
+    NumPy's own draw leaves it.  One per device; raises RuntimeError at construction when the host pieces it
+    needs (hostrng.log_params, hostrng.jump_polys) are unavailable."""
+
+    def __init__(self, device: torch.device):
+        from . import hostrng
+        self._lib = N.load()
+        self.device = device
+        params = hostrng.log_params()
+        if params is None:
+            raise RuntimeError("the device NumPy draw needs libm's log constants (hostrng.log_params)")
+        self._params = params
+        ctx = C.c_void_p()
+        with torch.cuda.device(device):
+            N.check(self._lib.mppi_np_ctx_create(device.index, params.ctypes.data, C.byref(ctx)), "mppi_np_ctx_create")
+        self._ctx = ctx
+        self._jumps = (0, 0)   # (block stride, streams) uploaded
+        self._st = N.NpStateC()
+        self._tgt = N.NpTargetC()
+
+    def close(self) -> None:
+        if getattr(self, "_ctx", None):
+            self._lib.mppi_np_ctx_destroy(self._ctx)
+            self._ctx = None
+
+    def __del__(self):  # pragma: no cover - best effort
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def draw(self, state, shape, plan, out: torch.Tensor, stream, k_offset: int, K_local: int, strides) -> None:
+        """Queue the draw of the (K, T, du) standard normals `shape` from `state` (np.random.get_state()) through
+        `plan` (hostrng.monomial_plan: src, scale, mean) into `out` (fp32 device), samples [k_offset, k_offset +
+        K_local) at strides (t, k, d); result() returns the state it leaves."""
+        from . import hostrng
+        K, T, du = shape
+        n = K * T * du
+        pos, has_gauss = int(state[2]), int(state[3])
+        P, ns = C.c_int(), C.c_int()
+        N.check(self._lib.mppi_np_plan(self._ctx, n, pos, has_gauss, C.byref(P), C.byref(ns)), "mppi_np_plan")
+        if self._jumps[0] != P.value or self._jumps[1] < ns.value:
+            polys = hostrng.jump_polys(P.value, ns.value)
+            if polys is None:
+                raise RuntimeError("MT19937 jump polynomials unavailable")
+            polys = np.ascontiguousarray(polys)
+            N.check(self._lib.mppi_np_set_jumps(self._ctx, P.value, ns.value, polys.ctypes.data if polys.size else None,
+                                                N.NP_POLY_WORDS), "mppi_np_set_jumps")
+            self._jumps = (P.value, ns.value)
+        st = self._st
+        C.memmove(st.key, np.ascontiguousarray(state[1], dtype=np.uint32).ctypes.data, 624 * 4)
+        st.pos, st.has_gauss, st.gauss = pos, has_gauss, float(state[4])
+        t = self._tgt
+        t.out_dev = out.data_ptr()
+        t.K, t.T, t.du, t.k_offset, t.K_local = K, T, du, int(k_offset), int(K_local)
+        t.stride_t, t.stride_k, t.stride_d = (int(x) for x in strides)
+        src, scale, mean = plan[:3]
+        for d in range(du):
+            t.src[d], t.scale[d], t.mean[d] = int(src[d]), float(scale[d]), float(mean[d])
+        N.check(self._lib.mppi_np_draw(self._ctx, C.c_void_p(stream), C.byref(st), n, C.byref(t)), "mppi_np_draw")
+
+    def result(self):
+        """The state the last draw leaves, as np.random.get_state()'s tuple (waits for the draw), or None when
+        the draw could not complete (nothing written)."""
+        st = self._st
+        rc = self._lib.mppi_np_draw_result(self._ctx, C.byref(st))
+        if rc == N.MPPI_E_RETRY:
+            return None   # too few accepted attempts (never seen): nothing written, np.random untouched
+        N.check(rc, "mppi_np_draw_result")
+        key = np.frombuffer(st.key, dtype=np.uint32).copy()
+        return ("MT19937", key, st.pos, st.has_gauss, st.gauss)
+
+
 def exploit_count(param_exploration: float, K: int) -> int:
     """Number of samples with ``k < (1 - expl) * K`` (control.py:98)."""
     thr = (1.0 - param_exploration) * K

@@ -25,8 +25,53 @@ def _load():
         f.restype = C.c_int
         f.argtypes = [C.c_void_p, C.POINTER(C.c_int), C.POINTER(C.c_int), C.POINTER(C.c_double), C.c_void_p,
                       C.c_int64, C.c_int]
+        lib.mppi_np_log_params.restype = C.c_int
+        lib.mppi_np_log_params.argtypes = [C.c_void_p, C.c_int]
+        lib.mppi_np_jump_poly.restype = C.c_int
+        lib.mppi_np_jump_poly.argtypes = [C.c_uint64, C.c_void_p]
+        lib.mppi_np_poly_words.restype = C.c_int
+        lib.mppi_np_log_mismatches.restype = C.c_int64
+        lib.mppi_np_log_mismatches.argtypes = [C.c_void_p, C.c_void_p, C.c_int64]
         _lib = lib
     return _lib
+
+
+def log_params():
+    """glibc's log constants for the device draw (include/mppi_rocm.h mppi_np_*): NPLOG_NDATA float64 values read
+    from this process's libm, accepted only after the C replica of the log (csrc/np_glibc_log.h) matched libm's
+    log() on 600k inputs (np_legacy_gauss.c mppi_np_log_params); None when unavailable or mismatched (the
+    device draw is then not used).  Cached."""
+    global _log_params
+    if _log_params is None:
+        lib = _load()
+        out = np.zeros(274)
+        _log_params = out if lib is not None and lib.mppi_np_log_params(out.ctypes.data, 200000) == 0 else False
+    return _log_params if _log_params is not False else None
+
+
+_log_params = None
+_jump_cache = {}
+
+
+def jump_polys(block_stride: int, streams: int) -> np.ndarray | None:
+    """x^(624 (block_stride s - 1)) mod P for s = 1 .. streams - 1 as a (streams - 1, 312) uint64 array (the
+    MT19937 jump polynomials of the device draw's generator streams; np_legacy_gauss.c mppi_np_jump_poly), or
+    None when the jump machinery is unavailable.  Cached per block stride (grown as needed)."""
+    lib = _load()
+    if lib is None:
+        return None
+    words = lib.mppi_np_poly_words()
+    have = _jump_cache.get(block_stride)
+    if have is None or have.shape[0] < streams - 1:
+        out = np.zeros((max(streams - 1, 0), words), dtype=np.uint64)
+        n0 = 0 if have is None else have.shape[0]
+        if n0:
+            out[:n0] = have
+        for s in range(n0 + 1, streams):
+            if lib.mppi_np_jump_poly(624 * (block_stride * s - 1), out[s - 1].ctypes.data) != 0:
+                return None
+        _jump_cache[block_stride] = have = out
+    return have[:streams - 1]
 
 
 def _threads() -> int:
@@ -90,13 +135,8 @@ def multivariate_normal(mean, cov, size) -> np.ndarray:
     return x
 
 
-def monomial_transform(mean, cov):
-    """multivariate_normal's transform x = z @ (sqrt(s)[:, None] * v) + mean (NumPy's svd of cov, its
-    positive-semidefinite check and warning) when that matrix has at most one nonzero per column: then
-    x[..., j] = z[..., src[j]] * scale[j] + mean[j] exactly (the other products are exact zeros), so the
-    device can apply it to the standard normals.  Returns (src, scale, mean) as float64 / int64 arrays, or None
-    for another shape of transform (the caller keeps NumPy's np.dot).  Run.py's Sigma = 20 I and the chain's
-    diagonal Sigma are of this kind."""
+def monomial_plan(mean, cov):
+    """monomial_transform without NumPy's positive-semidefinite warning: (src, scale, mean, psd) or None."""
     mean = np.array(mean)
     cov = np.array(cov)
     if len(mean.shape) != 1 or len(cov.shape) != 2 or cov.shape[0] != cov.shape[1] or mean.shape[0] != cov.shape[0]:
@@ -108,10 +148,23 @@ def monomial_transform(mean, cov):
     if not np.all(nz.sum(axis=0) <= 1):   # a zero column (singular cov) is x = mean: z * 0 + mean
         return None
     psd = np.allclose(np.dot(v.T * s, v), cov, rtol=1e-8, atol=1e-8)
-    if not psd:
-        warnings.warn("covariance is not symmetric positive-semidefinite.", RuntimeWarning)
     src = np.argmax(nz, axis=0).astype(np.int64)
-    return src, m[src, np.arange(m.shape[1])].astype(np.float64), mean.astype(np.float64)
+    return src, m[src, np.arange(m.shape[1])].astype(np.float64), mean.astype(np.float64), bool(psd)
+
+
+def monomial_transform(mean, cov):
+    """multivariate_normal's transform x = z @ (sqrt(s)[:, None] * v) + mean (NumPy's svd of cov, its
+    positive-semidefinite check and warning) when that matrix has at most one nonzero per column: then
+    x[..., j] = z[..., src[j]] * scale[j] + mean[j] exactly (the other products are exact zeros), so the
+    device can apply it to the standard normals.  Returns (src, scale, mean) as float64 / int64 arrays, or None
+    for another shape of transform (the caller keeps NumPy's np.dot).  Run.py's Sigma = 20 I and the chain's
+    diagonal Sigma are of this kind."""
+    plan = monomial_plan(mean, cov)
+    if plan is None:
+        return None
+    if not plan[3]:
+        warnings.warn("covariance is not symmetric positive-semidefinite.", RuntimeWarning)
+    return plan[:3]
 
 
 class StdNoise:

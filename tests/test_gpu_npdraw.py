@@ -1,0 +1,133 @@
+"""GPU: the reference's noise stream drawn on the device (include/mppi_rocm.h mppi_np_*, engine.NpDeviceStream).
+
+control.py:163 draws eps = np.random.multivariate_normal(mu, Sigma, (K, T)) on NumPy's legacy global RandomState.
+The device draw must give NumPy's values bit for bit (after the fp32 rounding of the upload) in the engine's noise
+layout, and leave the RNG state NumPy's draw leaves (key array, position, cached Gaussian).  The expected values
+here are NumPy's own multivariate_normal from the same state (the reference's call, not a restatement).
+Covered: config 3's size (8.4 M normals: ~4 % of the logs take glibc's near-1 branch), config 2's, odd sample
+counts, a state with a cached Gaussian and an odd count (the draw starts with it and leaves a new one), states at
+arbitrary word positions, a Sigma whose transform permutes the components, rank slices, and the drop-in
+controller with the device draw against the host draw over a closed loop.
+"""
+import numpy as np
+import pytest
+
+torch = pytest.importorskip("torch")
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def nd():
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    torch.cuda.set_device(0)
+    from mppi_robotarm_amd.engine import NpDeviceStream
+    d = NpDeviceStream(torch.device("cuda", 0))
+    yield d
+    d.close()
+
+
+def _numpy_draw(K, T, sigma):
+    x = np.random.multivariate_normal(np.zeros(sigma.shape[0]), sigma, (K, T))
+    return x.astype(np.float32), np.random.get_state()
+
+
+def _device_draw(nd, K, T, sigma, k_offset=0, K_local=None):
+    from mppi_robotarm_amd import hostrng
+    du = sigma.shape[0]
+    K_local = K if K_local is None else K_local
+    plan = hostrng.monomial_plan(np.zeros(du), sigma)
+    assert plan is not None
+    out = torch.full((T, K_local, du), float("nan"), dtype=torch.float32, device="cuda")
+    nd.draw(np.random.get_state(), (K, T, du), plan, out, torch.cuda.current_stream().cuda_stream, k_offset, K_local,
+            (K_local * du, du, 1))
+    st = nd.result()
+    return out.cpu().numpy(), st
+
+
+def _same_state(a, b):
+    return a[0] == b[0] and np.array_equal(a[1], b[1]) and a[2:] == b[2:]
+
+
+CASES = [
+    (65536, 64, 0, "runpy"),       # config 3
+    (4096, 32, 1, "runpy"),        # config 2
+    (4097, 33, 2, "runpy"),        # odd K and T
+    (512, 64, 3, "permuted"),      # Sigma's transform swaps the components
+    (128, 129, 4, "scaled"),       # just over the size the controller hands to the device
+]
+SIGMAS = {"runpy": np.eye(2) * 20.0, "permuted": np.diag([2.0, 9.0]), "scaled": np.diag([0.3, 7.0])}
+
+
+@pytest.mark.parametrize("K,T,seed,sig", CASES)
+@pytest.mark.parametrize("start", ["fresh", "offset", "cached"])
+def test_device_draw_equals_numpy(nd, K, T, seed, sig, start):
+    sigma = SIGMAS[sig]
+    np.random.seed(seed)
+    if start == "offset":
+        np.random.random_sample(seed * 37 + 101)          # the state mid key array
+    elif start == "cached":
+        np.random.standard_normal(3)                      # an odd count: a cached Gaussian
+    st0 = np.random.get_state()
+    want, st_want = _numpy_draw(K, T, sigma)
+    np.random.set_state(st0)
+    got, st_got = _device_draw(nd, K, T, sigma)
+    assert st_got is not None
+    np.testing.assert_array_equal(got, want.transpose(1, 0, 2))
+    assert _same_state(st_got, st_want)
+
+
+def test_odd_normal_count_leaves_the_cached_gaussian(nd):
+    """du = 1 and an odd K T: the draw ends on half a pair; NumPy caches f x1 for the next call."""
+    sigma = np.array([[4.0]])
+    np.random.seed(9)
+    st0 = np.random.get_state()
+    want, st_want = _numpy_draw(257, 129, sigma)
+    assert st_want[3] == 1
+    np.random.set_state(st0)
+    got, st_got = _device_draw(nd, 257, 129, sigma)
+    np.testing.assert_array_equal(got, want.transpose(1, 0, 2))
+    assert _same_state(st_got, st_want)
+
+
+def test_rank_slices_are_slices_of_the_whole_draw(nd):
+    K, T, sigma = 3000, 20, SIGMAS["runpy"]
+    np.random.seed(5)
+    st0 = np.random.get_state()
+    full, st_full = _device_draw(nd, K, T, sigma)
+    for off, kl in ((0, 1000), (1000, 1001), (2001, 999)):
+        np.random.set_state(st0)
+        part, st_part = _device_draw(nd, K, T, sigma, off, kl)
+        np.testing.assert_array_equal(part, full[:, off:off + kl])
+        assert _same_state(st_part, st_full)   # every rank leaves the same state
+
+
+def _loop(device_draw: bool, ticks=4, K=4096, T=32):
+    from mppi_robotarm_amd.controller import MPPIControllerForPathTracking
+    from mppi_robotarm_amd.params import X0_RUNPY, runpy_config
+    from conftest import load_paths
+    kw = runpy_config()
+    kw.update(number_of_samples_K=K, horizon_step_T=T, visualze_sampled_trajs=False)
+    c = MPPIControllerForPathTracking(ref_path=load_paths()["xydq_circle"], verbose=False, device=0,
+                                      numpy_noise_on_device=device_draw, **kw)
+    np.random.seed(21)
+    x, out = X0_RUNPY.copy(), []
+    for i in range(ticks):
+        u0, u_seq, opt, _ = c.calc_control_input(x)
+        out.append((u_seq.copy(), opt.copy()))
+        x = x + 0.002 * (i + 1)
+    used = c._npdev
+    c.close()
+    return out, np.random.get_state(), used
+
+
+def test_controller_device_draw_equals_host_draw():
+    """The drop-in with its default noise: the device draw gives the host draw's steps bit for bit and leaves
+    np.random where the host draw (NumPy's values and state, tests/test_hostrng.py) leaves it."""
+    a, st_a, used = _loop(True)
+    b, st_b, _ = _loop(False)
+    assert used, "the controller did not take the device draw"
+    for (ua, oa), (ub, ob) in zip(a, b):
+        np.testing.assert_array_equal(ua, ub)
+        np.testing.assert_array_equal(oa, ob)
+    assert _same_state(st_a, st_b)

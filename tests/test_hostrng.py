@@ -124,3 +124,61 @@ def test_std_noise_equals_numpy(cov):
     s0 = np.random.get_state()
     assert hostrng.multivariate_normal_std(np.zeros(2), np.array([[20.0, 5.0], [5.0, 10.0]]), size, buf) is None
     assert _state_eq(s0, np.random.get_state())
+
+
+# ---------------------------------------------------------------- the device draw's host inputs
+
+def test_log_replica_equals_libm_log():
+    """csrc/np_glibc_log.h on the constants read from libm (hostrng.log_params) equals libm's log() -- the log
+    NumPy's legacy_gauss calls -- bit for bit: random values over (0, 1), the near-1 branch and both its
+    edges, the smallest r2 an accepted polar attempt can have, powers of two and their neighbours."""
+    D = hostrng.log_params()
+    assert D is not None and D.shape == (274,)
+    lib = hostrng._load()
+    rng = np.random.default_rng(0)
+    lo, hi = 1.0 - 2.0 ** -4, 1.0 + float.fromhex("0x1.09p-4")
+    edges = [np.nextafter(lo, 0), lo, np.nextafter(lo, 2), np.nextafter(1.0, 0), 1.0, np.nextafter(hi, 0), hi,
+             np.nextafter(hi, 2), 2.0 ** -104, 2.0 ** -52, 0.5, np.nextafter(0.5, 0), np.nextafter(0.5, 1)]
+    pw = 2.0 ** -np.arange(1, 105)
+    x = np.concatenate([rng.random(2_000_000), lo + rng.random(500_000) * (1 - lo), np.array(edges), pw,
+                        np.nextafter(pw, 0), np.nextafter(pw, 1)])
+    x = np.ascontiguousarray(x[(x > 0) & (x <= 1)])
+    assert lib.mppi_np_log_mismatches(D.ctypes.data, x.ctypes.data, x.size) == 0
+
+
+def _mt_blocks(key, nblk):
+    """nblk key arrays from `key` by NumPy's twist (vectorised over the three in-place phases)."""
+    out = np.empty((nblk, 624), dtype=np.uint32)
+    out[0] = key
+    A, UP, LO = np.uint32(0x9908b0df), np.uint32(0x80000000), np.uint32(0x7fffffff)
+
+    def mix(a, b):
+        y = (a & UP) | (b & LO)
+        return (y >> np.uint32(1)) ^ ((np.uint32(0) - (y & np.uint32(1))) & A)
+    for b in range(1, nblk):
+        o, k = out[b - 1], out[b]
+        k[:227] = o[397:624] ^ mix(o[:227], o[1:228])
+        k[227:454] = k[0:227] ^ mix(o[227:454], o[228:455])
+        k[454:623] = k[227:396] ^ mix(o[454:623], o[455:624])
+        k[623] = k[396] ^ mix(o[623:624], k[0:1])[0]
+    return out
+
+
+@pytest.mark.parametrize("P,s", [(64, 1), (64, 3), (512, 2)])
+def test_jump_polynomials_reach_the_stream_starts(P, s):
+    """hostrng.jump_polys: the window form of the jump (the XOR of the word sequence's windows at the
+    polynomial's set bits, as np_jump_kernel evaluates it) then one twist gives key array P s exactly -- the
+    generator streams' starting blocks of the device draw."""
+    np.random.seed(17)
+    key = np.random.get_state()[1].astype(np.uint32)
+    nblk = P * s + 1
+    blocks = _mt_blocks(key, max(nblk, 35))
+    poly = hostrng.jump_polys(P, s + 1)[s - 1]
+    bits = np.nonzero(np.unpackbits(poly.view(np.uint8), bitorder="little"))[0]
+    assert bits.max() < 19937
+    seq = blocks[:35].reshape(-1)
+    jumped = np.zeros(624, dtype=np.uint32)
+    for d in bits:
+        jumped ^= seq[d:d + 624]
+    nxt = _mt_blocks(jumped, 2)[1]
+    np.testing.assert_array_equal(nxt, blocks[P * s])
