@@ -31,6 +31,7 @@
 #include <hip/hip_runtime.h>
 
 #include <stdint.h>
+#include <stdlib.h>
 #include <string.h>
 
 #include <string>
@@ -51,13 +52,17 @@ constexpr uint32_t kMatA = 0x9908b0dfu, kUp = 0x80000000u, kLo = 0x7fffffffu;
 constexpr int kDeg = 19937;
 constexpr int kPolyWords = MPPI_NP_POLY_WORDS;        // 312 x 64 bits: a polynomial of degree < 19937
 constexpr int kSeqBlocks = (kDeg + kN) / kN + 1;      // 34: the windows d + j < 19937 + 624 of the jumps
-constexpr int kNT = 256;                              // threads of the twist / attempt kernels
-constexpr int kJT = 320;                              // threads of a jump workgroup (2 per stream: 640 >= 624)
+constexpr int kNT = 256;                              // threads of the attempt kernels
+constexpr int kTT = 640;                              // threads of the twist kernels: one word per thread
+constexpr int kJT = 640;                              // threads of a jump workgroup: every output word
+constexpr int kJSplit = 4;                            // workgroups per stream, each a quarter of the set bits
 constexpr int kJBatch = 16;                           // set bits of a jump polynomial read per batch
 constexpr int kSeqPad = kSeqBlocks * kN;              // list padding: s_seq[kSeqPad + j] = 0 for j < 624
-constexpr int kJListStride = ((kDeg + 1 + kJBatch - 1) / kJBatch) * kJBatch;   // uint16 per stream's list
-constexpr int kAttPerThread = 8;
-constexpr int kAttPerWG = kNT * kAttPerThread;
+constexpr int kJListStride = ((kDeg + 1 + kJSplit * kJBatch - 1) / (kJSplit * kJBatch)) * kJSplit * kJBatch;
+constexpr int kJPart = kJListStride / kJSplit;        // list entries per workgroup (a multiple of kJBatch)
+constexpr int kAttRounds = 8;                         // attempts per thread, interleaved: attempt a0 + 256 r + t
+constexpr int kAttPerWG = kNT * kAttRounds;
+constexpr size_t kJumpLds = (kSeqPad + kN + kJPart) * sizeof(uint32_t);   // 107 KB
 constexpr int kScanT = 1024;
 
 __device__ __forceinline__ uint32_t mt_mix(uint32_t a, uint32_t b) {
@@ -68,22 +73,14 @@ __device__ __forceinline__ uint32_t mt_mix(uint32_t a, uint32_t b) {
 // The key array after o (LDS) into k (LDS).  NumPy's twist (in place, word order) is k[i] = o[i + 397] ^
 // mix(o[i], o[i + 1]) for i < 227, k[i] = k[i - 227] ^ mix(o[i], o[i + 1]) up to 622, and k[623] =
 // k[396] ^ mix(o[623], k[0]); substituting the earlier k's, every word depends on o only.
-__device__ __forceinline__ void twist_block(const uint32_t* o, uint32_t* k) {
-    for (int i = threadIdx.x; i < kN; i += blockDim.x) {
-        uint32_t v;
-        if (i < kN - kM) {
-            v = o[i + kM] ^ mt_mix(o[i], o[i + 1]);
-        } else if (i < 2 * (kN - kM)) {
-            v = o[i + 170] ^ mt_mix(o[i - 227], o[i - 226]) ^ mt_mix(o[i], o[i + 1]);
-        } else if (i < kN - 1) {
-            v = o[i - 57] ^ mt_mix(o[i - 454], o[i - 453]) ^ mt_mix(o[i - 227], o[i - 226]) ^ mt_mix(o[i], o[i + 1]);
-        } else {
-            const uint32_t k0 = o[kM] ^ mt_mix(o[0], o[1]);
-            const uint32_t k396 = o[566] ^ mt_mix(o[169], o[170]) ^ mt_mix(o[396], o[397]);
-            v = k396 ^ mt_mix(o[623], k0);
-        }
-        k[i] = v;
-    }
+__device__ __forceinline__ uint32_t twist_word(const uint32_t* o, int i) {
+    if (i < kN - kM) return o[i + kM] ^ mt_mix(o[i], o[i + 1]);
+    if (i < 2 * (kN - kM)) return o[i + 170] ^ mt_mix(o[i - 227], o[i - 226]) ^ mt_mix(o[i], o[i + 1]);
+    if (i < kN - 1)
+        return o[i - 57] ^ mt_mix(o[i - 454], o[i - 453]) ^ mt_mix(o[i - 227], o[i - 226]) ^ mt_mix(o[i], o[i + 1]);
+    const uint32_t k0 = o[kM] ^ mt_mix(o[0], o[1]);
+    const uint32_t k396 = o[566] ^ mt_mix(o[169], o[170]) ^ mt_mix(o[396], o[397]);
+    return k396 ^ mt_mix(o[623], k0);
 }
 
 __device__ __forceinline__ uint32_t temper(uint32_t y) {
@@ -128,87 +125,128 @@ struct NpShape {
 };
 
 // ------------------------------------------------------------------ generation
-__global__ __launch_bounds__(kNT) void np_seq_kernel(const uint32_t* __restrict__ key, uint32_t* __restrict__ seq) {
+__global__ __launch_bounds__(kTT) void np_seq_kernel(const uint32_t* __restrict__ key, uint32_t* __restrict__ seq) {
     __shared__ uint32_t buf[2][kN];
-    for (int i = threadIdx.x; i < kN; i += kNT) {
-        buf[0][i] = key[i];
-        seq[i] = key[i];
+    const int i = threadIdx.x;
+    uint32_t v = i < kN ? key[i] : 0u;
+    if (i < kN) {
+        buf[0][i] = v;
+        seq[i] = v;
     }
     __syncthreads();
     for (int b = 1; b < kSeqBlocks; ++b) {
-        twist_block(buf[(b - 1) & 1], buf[b & 1]);
-        __syncthreads();   // the next twist writes the buffer this one read; the stores below read the other
-        for (int i = threadIdx.x; i < kN; i += kNT) seq[(size_t)b * kN + i] = buf[b & 1][i];
+        if (i < kN) {
+            v = twist_word(buf[(b - 1) & 1], i);
+            buf[b & 1][i] = v;
+            seq[(size_t)b * kN + i] = v;
+        }
+        __syncthreads();   // the next twist reads this block and writes the buffer this one read
     }
 }
 
 // stream s = blockIdx.y + 1 starts at block P s: its jump polynomial is x^(624 (P s - 1)) mod P, giving block
 // P s - 1 up to the 31 low bits of its word 0 (outside the 19937-bit state); np_gen_kernel twists once more.
-// The polynomial comes as the list of its set bits (mppi_np_set_jumps), padded to a multiple of kJBatch with
-// kSeqPad (a window of zero words past the sequence), so each batch's LDS reads are issued together.
-__global__ __launch_bounds__(kJT) void np_jump_kernel(const uint32_t* __restrict__ seq, const uint16_t* __restrict__ bits,
-                                                      const int* __restrict__ nbits, uint32_t* __restrict__ jumped) {
-    extern __shared__ uint32_t s_seq[];   // kSeqBlocks x 624 words, then 624 zero words: 87 KB
-    const uint4* src = reinterpret_cast<const uint4*>(seq);
-    for (int i = threadIdx.x; i < kSeqBlocks * kN / 4; i += kJT) reinterpret_cast<uint4*>(s_seq)[i] = src[i];
-    for (int i = kSeqBlocks * kN + threadIdx.x; i < kSeqPad + kN; i += kJT) s_seq[i] = 0u;
+// The polynomial comes as the list of its set bits (mppi_np_set_jumps) as LDS byte offsets, split over
+// kJSplit workgroups (blockIdx.x), each list part padded to kJPart entries with the offset of kSeqPad (a window
+// of zero words past the sequence); each workgroup writes its partial XOR of every output word and
+// np_gen_kernel XORs the parts.
+// Per batch of kJBatch bits: the positions (one broadcast LDS read per 8), then the 16 windows' reads, issued
+// together; the next batch's positions are read before this batch's XORs.
+__global__ __launch_bounds__(kJT) void np_jump_kernel(const uint32_t* __restrict__ seq, const uint32_t* __restrict__ bits,
+                                                      const int* __restrict__ nbits, uint32_t* __restrict__ parts) {
+    extern __shared__ uint32_t s_seq[];   // kSeqBlocks x 624 words, 624 zero words, then the list part
+    uint32_t* s_list = s_seq + kSeqPad + kN;
+    {   // every load in flight before the first LDS store
+        constexpr int kVec = kSeqBlocks * kN / 4, kIt = (kVec + kJT - 1) / kJT;
+        const uint4* src = reinterpret_cast<const uint4*>(seq);
+        uint4 v[kIt];
+#pragma unroll
+        for (int q = 0; q < kIt; ++q) {
+            const int i = threadIdx.x + q * kJT;
+            if (i < kVec) v[q] = src[i];
+        }
+        const uint4* lsrc = reinterpret_cast<const uint4*>(bits + (size_t)blockIdx.y * kJListStride + blockIdx.x * kJPart);
+        constexpr int kLVec = kJPart / 4, kLIt = (kLVec + kJT - 1) / kJT;
+        uint4 l[kLIt];
+#pragma unroll
+        for (int q = 0; q < kLIt; ++q) {
+            const int i = threadIdx.x + q * kJT;
+            if (i < kLVec) l[q] = lsrc[i];
+        }
+#pragma unroll
+        for (int q = 0; q < kIt; ++q) {
+            const int i = threadIdx.x + q * kJT;
+            if (i < kVec) reinterpret_cast<uint4*>(s_seq)[i] = v[q];
+        }
+#pragma unroll
+        for (int q = 0; q < kLIt; ++q) {
+            const int i = threadIdx.x + q * kJT;
+            if (i < kLVec) reinterpret_cast<uint4*>(s_list)[i] = l[q];
+        }
+        if (threadIdx.x < kN) s_seq[kSeqPad + threadIdx.x] = 0u;
+    }
+    const int nb = min(max(nbits[blockIdx.y] - (int)blockIdx.x * kJPart, 0), kJPart);   // a multiple of kJBatch
     __syncthreads();
-    const int j = blockIdx.x * kJT + threadIdx.x;
-    const int jj = j < kN ? j : kN - 1;   // the idle lanes read in bounds and store nothing
-    const int nb = nbits[blockIdx.y];     // a multiple of kJBatch
-    const uint4* lst = reinterpret_cast<const uint4*>(bits + (size_t)blockIdx.y * kJListStride);
+    const uint32_t jb = 4u * (threadIdx.x < kN ? threadIdx.x : kN - 1);   // idle lanes read in bounds, store nothing
+    const uint4* L = reinterpret_cast<const uint4*>(s_list);
+    const char* S = reinterpret_cast<const char*>(s_seq);
     uint32_t acc0 = 0, acc1 = 0;
     for (int b = 0; b < nb; b += kJBatch) {
-        // kJBatch positions (the same for every lane: scalar loads), then their reads, then the XORs
-        uint32_t d[kJBatch / 2];
+        uint32_t d[kJBatch];   // byte offsets of the windows (broadcast LDS reads)
 #pragma unroll
-        for (int q = 0; q < kJBatch / 8; ++q) {
-            const uint4 v = lst[b / 8 + q];
-            d[4 * q + 0] = __builtin_amdgcn_readfirstlane(v.x);
-            d[4 * q + 1] = __builtin_amdgcn_readfirstlane(v.y);
-            d[4 * q + 2] = __builtin_amdgcn_readfirstlane(v.z);
-            d[4 * q + 3] = __builtin_amdgcn_readfirstlane(v.w);
+        for (int q = 0; q < kJBatch / 4; ++q) {
+            const uint4 v = L[b / 4 + q];
+            d[4 * q] = v.x;
+            d[4 * q + 1] = v.y;
+            d[4 * q + 2] = v.z;
+            d[4 * q + 3] = v.w;
         }
         uint32_t r[kJBatch];
 #pragma unroll
-        for (int q = 0; q < kJBatch / 2; ++q) {
-            r[2 * q] = s_seq[(d[q] & 0xFFFFu) + jj];
-            r[2 * q + 1] = s_seq[(d[q] >> 16) + jj];
-        }
+        for (int q = 0; q < kJBatch; ++q) r[q] = *reinterpret_cast<const uint32_t*>(S + (d[q] + jb));
 #pragma unroll
         for (int q = 0; q < kJBatch; q += 2) {
             acc0 ^= r[q];
             acc1 ^= r[q + 1];
         }
     }
-    if (j < kN) jumped[(size_t)blockIdx.y * kN + j] = acc0 ^ acc1;
+    if (threadIdx.x < kN) parts[((size_t)blockIdx.y * kJSplit + blockIdx.x) * kN + threadIdx.x] = acc0 ^ acc1;
 }
 
 // stream s: blocks [1 + P s, min(1 + P (s + 1), nblk)); stream 0 also writes block 0 (the state's key array)
-__global__ __launch_bounds__(kNT) void np_gen_kernel(const uint32_t* __restrict__ key, const uint32_t* __restrict__ jumped,
+__global__ __launch_bounds__(kTT) void np_gen_kernel(const uint32_t* __restrict__ key, const uint32_t* __restrict__ parts,
                                                      uint32_t* __restrict__ words, int P, int nblk) {
     __shared__ uint32_t buf[2][kN];
-    const int s = blockIdx.x;
+    const int s = blockIdx.x, i = threadIdx.x;
     const int b0 = 1 + P * s, b1 = min(1 + P * (s + 1), nblk);
     if (s == 0) {
-        for (int i = threadIdx.x; i < kN; i += kNT) {
-            buf[0][i] = key[i];
-            words[i] = key[i];
+        if (i < kN) {
+            const uint32_t v = key[i];
+            buf[0][i] = v;
+            words[i] = v;
         }
         __syncthreads();
     } else {
-        for (int i = threadIdx.x; i < kN; i += kNT) buf[1][i] = jumped[(size_t)(s - 1) * kN + i];
+        if (i < kN) {
+            const uint32_t* q = parts + (size_t)(s - 1) * kJSplit * kN + i;
+            uint32_t v = 0;
+#pragma unroll
+            for (int h = 0; h < kJSplit; ++h) v ^= q[h * kN];
+            buf[1][i] = v;
+        }
         __syncthreads();
-        twist_block(buf[1], buf[0]);   // block P s, exactly
+        if (i < kN) buf[0][i] = twist_word(buf[1], i);   // block P s, exactly
         __syncthreads();
     }
     int cur = 0;
     for (int b = b0; b < b1; ++b) {
-        twist_block(buf[cur], buf[cur ^ 1]);
+        if (i < kN) {
+            const uint32_t v = twist_word(buf[cur], i);
+            buf[cur ^ 1][i] = v;
+            words[(size_t)b * kN + i] = v;
+        }
         __syncthreads();
         cur ^= 1;
-        uint32_t* dst = words + (size_t)b * kN;
-        for (int i = threadIdx.x; i < kN; i += kNT) dst[i] = buf[cur][i];
     }
 }
 
@@ -223,16 +261,20 @@ __device__ __forceinline__ int block_sum(int v, int* s_tmp) {
     return t;
 }
 
+// attempt a0 + 256 r + t for round r of thread t: each round's loads are one coalesced 4 KB run
 __global__ __launch_bounds__(kNT) void np_count_kernel(const uint32_t* __restrict__ words, long long base,
                                                        long long A, int* __restrict__ counts) {
     __shared__ int s_tmp[kNT / 64];
-    const long long a0 = (long long)blockIdx.x * kAttPerWG + (long long)threadIdx.x * kAttPerThread;
+    const long long a0 = (long long)blockIdx.x * kAttPerWG + threadIdx.x;
     int c = 0;
-    for (int q = 0; q < kAttPerThread; ++q) {
-        if (a0 + q >= A) break;
-        double x1, x2, r2;
-        attempt(words, base, a0 + q, x1, x2, r2);
-        c += accepted(r2);
+#pragma unroll
+    for (int r = 0; r < kAttRounds; ++r) {
+        const long long a = a0 + (long long)r * kNT;
+        if (a < A) {
+            double x1, x2, r2;
+            attempt(words, base, a, x1, x2, r2);
+            c += accepted(r2);
+        }
     }
     c = block_sum(c, s_tmp);
     if (threadIdx.x == 0) counts[blockIdx.x] = c;
@@ -281,45 +323,53 @@ __global__ __launch_bounds__(kNT) void np_write_kernel(const uint32_t* __restric
                                                        const double* __restrict__ logd, NpShape sh, long long pairs,
                                                        long long n, int o, double cached, NpResult* res) {
     __shared__ double s_log[NPLOG_NDATA];
-    __shared__ int s_tmp[kNT / 64];
+    __shared__ int s_cnt[kAttRounds][kNT / 64];
     for (int i = threadIdx.x; i < NPLOG_NDATA; i += kNT) s_log[i] = logd[i];
     if (res->status) return;   // uniform: every thread returns
-    const long long a0 = (long long)blockIdx.x * kAttPerWG + (long long)threadIdx.x * kAttPerThread;
-    unsigned mask = 0;
-    for (int q = 0; q < kAttPerThread; ++q) {
-        if (a0 + q >= A) break;
-        double x1, x2, r2;
-        attempt(words, base, a0 + q, x1, x2, r2);
-        mask |= (unsigned)accepted(r2) << q;
-    }
-    // this thread's first pair: the workgroup's offset + the accepted attempts of the threads before it
-    const int c = __popc(mask);
-    int incl = c;
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-    for (int d = 1; d < 64; d <<= 1) {
-        const int v = __shfl_up(incl, d);
-        if (lane >= d) incl += v;
+    const long long a0 = (long long)blockIdx.x * kAttPerWG + threadIdx.x;
+    double x1[kAttRounds], x2[kAttRounds], r2[kAttRounds];
+    unsigned mask = 0;
+#pragma unroll
+    for (int r = 0; r < kAttRounds; ++r) {
+        const long long a = a0 + (long long)r * kNT;
+        r2[r] = 2.0;
+        if (a < A) attempt(words, base, a, x1[r], x2[r], r2[r]);
+        const bool acc = accepted(r2[r]);
+        mask |= (unsigned)acc << r;
+        const unsigned long long bal = __ballot(acc);
+        if (lane == 0) s_cnt[r][wave] = __popcll(bal);
     }
-    if (lane == 63) s_tmp[wave] = incl;
     __syncthreads();   // also publishes s_log
-    long long q = offsets[blockIdx.x] + incl - c;
-    for (int w = 0; w < wave; ++w) q += s_tmp[w];
+    // pair index of this thread's attempt in round r: the workgroup's offset, all accepted attempts of the
+    // rounds before r, those of round r in earlier waves, and those of earlier lanes of this wave
+    long long q0 = offsets[blockIdx.x];
     if (blockIdx.x == 0 && threadIdx.x == 0 && o) emit(sh, 0u, cached);   // the cached Gaussian comes first
-    while (mask && q < pairs) {
-        const int b = __ffs(mask) - 1;
-        mask &= mask - 1;
-        double x1, x2, r2;
-        attempt(words, base, a0 + b, x1, x2, r2);
-        const double f = sqrt(-2.0 * np_glibc_log(s_log, r2) / r2);
-        const double g1 = f * x1, g2 = f * x2;   // legacy_gauss returns f x2 and caches f x1
-        const unsigned m = (unsigned)(o + 2 * q);
-        emit(sh, m, g2);
-        if ((long long)m + 1 < n) emit(sh, m + 1, g1);
-        if (q == pairs - 1) {
-            res->last_attempt = a0 + b;
-            res->last_fx1 = g1;
+    const unsigned long long lt = (1ull << lane) - 1ull;
+#pragma unroll
+    for (int r = 0; r < kAttRounds; ++r) {
+        const bool acc = (mask >> r) & 1u;
+        const unsigned long long bal = __ballot(acc);
+        long long q = q0 + __popcll(bal & lt);
+        int before = 0, round = 0;
+        for (int w = 0; w < kNT / 64; ++w) {
+            const int cw = s_cnt[r][w];
+            before += w < wave ? cw : 0;
+            round += cw;
         }
-        ++q;
+        q += before;
+        if (acc && q < pairs) {
+            const double f = sqrt(-2.0 * np_glibc_log(s_log, r2[r]) / r2[r]);
+            const double g1 = f * x1[r], g2 = f * x2[r];   // legacy_gauss returns f x2 and caches f x1
+            const unsigned m = (unsigned)(o + 2 * q);
+            emit(sh, m, g2);
+            if ((long long)m + 1 < n) emit(sh, m + 1, g1);
+            if (q == pairs - 1) {
+                res->last_attempt = a0 + (long long)r * kNT;
+                res->last_fx1 = g1;
+            }
+        }
+        q0 += round;
     }
 }
 
@@ -349,7 +399,7 @@ struct mppi_np_ctx {
     double* d_log = nullptr;
     uint32_t* d_key = nullptr;      // the draw's starting key array
     uint32_t* d_seq = nullptr;      // kSeqBlocks blocks
-    uint16_t* d_bits = nullptr;     // (streams - 1) jump polynomials of block stride P, as set-bit lists
+    uint32_t* d_bits = nullptr;     // (streams - 1) jump polynomials of block stride P, as set-bit byte offsets
     int* d_nbits = nullptr;
     int poly_P = 0, poly_streams = 0;
     uint32_t* d_jumped = nullptr;
@@ -381,20 +431,23 @@ struct Plan {
 
 // attempts generated: 4/3 of the pairs plus 4096 (acceptance pi/4: 1.27 attempts per pair expected), as the
 // host path (np_legacy_gauss.c); the block stride P of the streams from a cost model of the two parallel
-// phases measured on MI355X: jumps, LDS-bound, ~40 us per round of 128 streams; twists ~0.13 us per block
+// phases on MI355X: the jumps run in rounds of 64 streams (kJSplit workgroups each, one per CU) of kJumpRoundUs,
+// a stream twists its P blocks at kBlockUs each (MPPI_NP_STRIDE forces P, for measurements)
+constexpr double kJumpRoundUs = 40.0, kBlockUs = 0.4;
 Plan make_plan(long long n, int pos, int has_gauss) {
     Plan p;
     p.need = n - (has_gauss ? 1 : 0);
     p.pairs = (p.need + 1) / 2;
     p.A = p.pairs + p.pairs / 3 + 4096;
     p.nblk = (pos + 4 * p.A + kN - 1) / kN + 1;
+    static const int forced = getenv("MPPI_NP_STRIDE") ? atoi(getenv("MPPI_NP_STRIDE")) : 0;
     double best = 1e30;
     p.P = 64;
     p.streams = 1;
-    for (int P = 64; P <= (1 << 20); P <<= 1) {
+    for (int P = 16; P <= (1 << 22); P <<= 1) {
         const long long streams = (p.nblk - 1 + P - 1) / P;
-        if (streams > MPPI_NP_MAX_STREAMS) continue;
-        const double cost = (double)((streams - 1 + 127) / 128) * 40.0 + P * 0.13;
+        if (streams > MPPI_NP_MAX_STREAMS || (forced && P != forced)) continue;
+        const double cost = (double)((streams - 1 + 63) / 64) * kJumpRoundUs + P * kBlockUs;
         if (cost < best) {
             best = cost;
             p.P = P;
@@ -428,7 +481,7 @@ int mppi_np_ctx_create(int device, const double* log_params, mppi_np_ctx** out) 
         return fail(MPPI_E_HIP, std::string("mppi_np_ctx_create: ") + hipGetErrorString(e));
     }
     if (hipFuncSetAttribute((const void*)np_jump_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
-                            (int)((kSeqPad + kN) * sizeof(uint32_t))) != hipSuccess) {
+                            (int)kJumpLds) != hipSuccess) {
         mppi_np_ctx_destroy(c);
         return fail(MPPI_E_HIP, "mppi_np_ctx_create: the jump kernel's LDS");
     }
@@ -480,7 +533,7 @@ int mppi_np_set_jumps(mppi_np_ctx* c, int block_stride, int streams, const unsig
     c->poly_P = c->poly_streams = 0;
     if (streams > 1) {
         const size_t ns = (size_t)(streams - 1);
-        std::vector<uint16_t> lists(ns * kJListStride, (uint16_t)kSeqPad);
+        std::vector<uint32_t> lists(ns * kJListStride, 4u * kSeqPad);
         std::vector<int> counts(ns);
         for (size_t q = 0; q < ns; ++q) {
             int nb = 0;
@@ -488,15 +541,15 @@ int mppi_np_set_jumps(mppi_np_ctx* c, int block_stride, int streams, const unsig
                 for (uint64_t m = polys[q * kPolyWords + w]; m; m &= m - 1) {
                     const int d = 64 * w + __builtin_ctzll(m);
                     if (d >= kDeg) return fail(MPPI_E_ARG, "mppi_np_set_jumps: a polynomial of degree >= 19937");
-                    lists[q * kJListStride + nb++] = (uint16_t)d;
+                    lists[q * kJListStride + nb++] = 4u * (uint32_t)d;
                 }
             counts[q] = (nb + kJBatch - 1) / kJBatch * kJBatch;
         }
-        NP_CHECK(hipMalloc(&c->d_bits, lists.size() * sizeof(uint16_t)));
-        NP_CHECK(hipMemcpy(c->d_bits, lists.data(), lists.size() * sizeof(uint16_t), hipMemcpyHostToDevice));
+        NP_CHECK(hipMalloc(&c->d_bits, lists.size() * sizeof(uint32_t)));
+        NP_CHECK(hipMemcpy(c->d_bits, lists.data(), lists.size() * sizeof(uint32_t), hipMemcpyHostToDevice));
         NP_CHECK(hipMalloc(&c->d_nbits, ns * sizeof(int)));
         NP_CHECK(hipMemcpy(c->d_nbits, counts.data(), ns * sizeof(int), hipMemcpyHostToDevice));
-        NP_CHECK(hipMalloc(&c->d_jumped, ns * kN * sizeof(uint32_t)));
+        NP_CHECK(hipMalloc(&c->d_jumped, ns * kJSplit * kN * sizeof(uint32_t)));
     }
     c->poly_P = block_stride;
     c->poly_streams = streams;
@@ -540,11 +593,11 @@ int mppi_np_draw(mppi_np_ctx* c, void* stream, const mppi_np_state* st, long lon
     memcpy(c->h_key, st->key, kN * sizeof(uint32_t));
     NP_CHECK(hipMemcpyAsync(c->d_key, c->h_key, kN * sizeof(uint32_t), hipMemcpyHostToDevice, s));
     if (p.streams > 1) {
-        hipLaunchKernelGGL(np_seq_kernel, dim3(1), dim3(kNT), 0, s, c->d_key, c->d_seq);
-        hipLaunchKernelGGL(np_jump_kernel, dim3((kN + kJT - 1) / kJT, p.streams - 1), dim3(kJT),
-                           (kSeqPad + kN) * sizeof(uint32_t), s, c->d_seq, c->d_bits, c->d_nbits, c->d_jumped);
+        hipLaunchKernelGGL(np_seq_kernel, dim3(1), dim3(kTT), 0, s, c->d_key, c->d_seq);
+        hipLaunchKernelGGL(np_jump_kernel, dim3(kJSplit, p.streams - 1), dim3(kJT), kJumpLds, s, c->d_seq, c->d_bits,
+                           c->d_nbits, c->d_jumped);
     }
-    hipLaunchKernelGGL(np_gen_kernel, dim3(p.streams), dim3(kNT), 0, s, c->d_key, c->d_jumped, c->d_words, p.P,
+    hipLaunchKernelGGL(np_gen_kernel, dim3(p.streams), dim3(kTT), 0, s, c->d_key, c->d_jumped, c->d_words, p.P,
                        (int)p.nblk);
     hipLaunchKernelGGL(np_count_kernel, dim3((unsigned)nwg), dim3(kNT), 0, s, c->d_words, (long long)st->pos, p.A,
                        c->d_counts);

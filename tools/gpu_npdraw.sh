@@ -1,5 +1,6 @@
 #!/bin/bash
-# GPU box: the device NumPy-draw tests, its timing, and a rocprofv3 kernel-trace of the timing run.
+# GPU box: the device NumPy-draw tests, its timing (the stride the plan picks, then forced strides), and a
+# rocprofv3 kernel-trace of the timing run.
 set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 export TMPDIR=/tmp
@@ -8,6 +9,8 @@ timeout -k 10 300 python -u -m pytest tests/test_gpu_npdraw.py -x -v --timeout 1
 rc=$?; echo "tests rc=$rc"; tail -3 $O/tests.log; [ $rc -le 1 ] || exit $rc
 timeout -k 10 300 python tools/npdraw_bench.py > $O/bench.txt 2>&1
 rc=$?; echo "bench rc=$rc"; cat $O/bench.txt; [ $rc -eq 0 ] || exit $rc
-timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/prof -o run -- python tools/npdraw_bench.py > $O/prof.log 2>&1
-rc=$?; echo "prof rc=$rc"
+for P in ${STRIDES:-128 256 512}; do
+  MPPI_NP_STRIDE=$P timeout -k 10 120 rocprofv3 --kernel-trace --stats --output-format csv -d $O/prof_$P -o run -- python tools/npdraw_bench.py 65536 64 > $O/prof_$P.log 2>&1
+  rc=$?; echo "prof P=$P rc=$rc"; [ $rc -eq 0 ] || exit $rc
+done
 exit 0
