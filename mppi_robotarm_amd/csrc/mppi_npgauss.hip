@@ -54,15 +54,16 @@ constexpr int kPolyWords = MPPI_NP_POLY_WORDS;        // 312 x 64 bits: a polyno
 constexpr int kSeqBlocks = (kDeg + kN) / kN + 1;      // 34: the windows d + j < 19937 + 624 of the jumps
 constexpr int kNT = 256;                              // threads of the attempt kernels
 constexpr int kTT = 640;                              // threads of the twist kernels: one word per thread
-constexpr int kJT = 640;                              // threads of a jump workgroup: every output word
+constexpr int kJT = 320;                              // threads of a jump workgroup: two output words each
+constexpr int kJHalf = 320;                           // the second word of a lane: 5 x 64 words on
 constexpr int kJSplit = 4;                            // workgroups per stream, each a quarter of the set bits
-constexpr int kJBatch = 16;                           // set bits of a jump polynomial read per batch
-constexpr int kSeqPad = kSeqBlocks * kN;              // list padding: s_seq[kSeqPad + j] = 0 for j < 624
+constexpr int kJBatch = 32;                           // set bits of a jump polynomial read per batch
+constexpr int kSeqPad = kSeqBlocks * kN;              // list padding: s_seq[kSeqPad + j] = 0 for j < 640
 constexpr int kJListStride = ((kDeg + 1 + kJSplit * kJBatch - 1) / (kJSplit * kJBatch)) * kJSplit * kJBatch;
 constexpr int kJPart = kJListStride / kJSplit;        // list entries per workgroup (a multiple of kJBatch)
 constexpr int kAttRounds = 8;                         // attempts per thread, interleaved: attempt a0 + 256 r + t
 constexpr int kAttPerWG = kNT * kAttRounds;
-constexpr size_t kJumpLds = (kSeqPad + kN + kJPart) * sizeof(uint32_t);   // 107 KB
+constexpr size_t kJumpLds = (kSeqPad + 2 * kJHalf) * sizeof(uint32_t);   // 87 KB
 constexpr int kScanT = 1024;
 
 __device__ __forceinline__ uint32_t mt_mix(uint32_t a, uint32_t b) {
@@ -149,13 +150,11 @@ __global__ __launch_bounds__(kTT) void np_seq_kernel(const uint32_t* __restrict_
 // The polynomial comes as the list of its set bits (mppi_np_set_jumps) as LDS byte offsets, split over
 // kJSplit workgroups (blockIdx.x), each list part padded to kJPart entries with the offset of kSeqPad (a window
 // of zero words past the sequence); each workgroup writes its partial XOR of every output word and
-// np_gen_kernel XORs the parts.
-// Per batch of kJBatch bits: the positions (one broadcast LDS read per 8), then the 16 windows' reads, issued
-// together; the next batch's positions are read before this batch's XORs.
+// np_gen_kernel XORs the parts.  Per batch of kJBatch bits: the offsets by scalar loads, then every window
+// read of the batch issued together (one ds_read2st64 per bit and lane: its two output words), then XOR3s.
 __global__ __launch_bounds__(kJT) void np_jump_kernel(const uint32_t* __restrict__ seq, const uint32_t* __restrict__ bits,
                                                       const int* __restrict__ nbits, uint32_t* __restrict__ parts) {
-    extern __shared__ uint32_t s_seq[];   // kSeqBlocks x 624 words, 624 zero words, then the list part
-    uint32_t* s_list = s_seq + kSeqPad + kN;
+    extern __shared__ uint32_t s_seq[];   // kSeqBlocks x 624 words, then 640 zero words (the padding's window)
     {   // every load in flight before the first LDS store
         constexpr int kVec = kSeqBlocks * kN / 4, kIt = (kVec + kJT - 1) / kJT;
         const uint4* src = reinterpret_cast<const uint4*>(seq);
@@ -165,52 +164,37 @@ __global__ __launch_bounds__(kJT) void np_jump_kernel(const uint32_t* __restrict
             const int i = threadIdx.x + q * kJT;
             if (i < kVec) v[q] = src[i];
         }
-        const uint4* lsrc = reinterpret_cast<const uint4*>(bits + (size_t)blockIdx.y * kJListStride + blockIdx.x * kJPart);
-        constexpr int kLVec = kJPart / 4, kLIt = (kLVec + kJT - 1) / kJT;
-        uint4 l[kLIt];
-#pragma unroll
-        for (int q = 0; q < kLIt; ++q) {
-            const int i = threadIdx.x + q * kJT;
-            if (i < kLVec) l[q] = lsrc[i];
-        }
 #pragma unroll
         for (int q = 0; q < kIt; ++q) {
             const int i = threadIdx.x + q * kJT;
             if (i < kVec) reinterpret_cast<uint4*>(s_seq)[i] = v[q];
         }
-#pragma unroll
-        for (int q = 0; q < kLIt; ++q) {
-            const int i = threadIdx.x + q * kJT;
-            if (i < kLVec) reinterpret_cast<uint4*>(s_list)[i] = l[q];
-        }
-        if (threadIdx.x < kN) s_seq[kSeqPad + threadIdx.x] = 0u;
+        for (int i = threadIdx.x; i < 2 * kJHalf; i += kJT) s_seq[kSeqPad + i] = 0u;
     }
     const int nb = min(max(nbits[blockIdx.y] - (int)blockIdx.x * kJPart, 0), kJPart);   // a multiple of kJBatch
     __syncthreads();
-    const uint32_t jb = 4u * (threadIdx.x < kN ? threadIdx.x : kN - 1);   // idle lanes read in bounds, store nothing
-    const uint4* L = reinterpret_cast<const uint4*>(s_list);
+    // lane t: output words t and t + 320 (< 624), read as one ds_read2st64_b32 (offset1 = 5 x 64 words)
+    const uint32_t jb = 4u * threadIdx.x;
+    const uint32_t* L = bits + (size_t)blockIdx.y * kJListStride + blockIdx.x * kJPart;   // scalar loads
     const char* S = reinterpret_cast<const char*>(s_seq);
-    uint32_t acc0 = 0, acc1 = 0;
+    uint32_t lo = 0, hi = 0;
     for (int b = 0; b < nb; b += kJBatch) {
-        uint32_t d[kJBatch];   // byte offsets of the windows (broadcast LDS reads)
+        uint32_t r[kJBatch], h[kJBatch];
 #pragma unroll
-        for (int q = 0; q < kJBatch / 4; ++q) {
-            const uint4 v = L[b / 4 + q];
-            d[4 * q] = v.x;
-            d[4 * q + 1] = v.y;
-            d[4 * q + 2] = v.z;
-            d[4 * q + 3] = v.w;
+        for (int q = 0; q < kJBatch; ++q) {
+            const char* a = S + (L[b + q] + jb);
+            r[q] = *reinterpret_cast<const uint32_t*>(a);
+            h[q] = *reinterpret_cast<const uint32_t*>(a + 4 * kJHalf);
         }
-        uint32_t r[kJBatch];
-#pragma unroll
-        for (int q = 0; q < kJBatch; ++q) r[q] = *reinterpret_cast<const uint32_t*>(S + (d[q] + jb));
 #pragma unroll
         for (int q = 0; q < kJBatch; q += 2) {
-            acc0 ^= r[q];
-            acc1 ^= r[q + 1];
+            lo = lo ^ r[q] ^ r[q + 1];
+            hi = hi ^ h[q] ^ h[q + 1];
         }
     }
-    if (threadIdx.x < kN) parts[((size_t)blockIdx.y * kJSplit + blockIdx.x) * kN + threadIdx.x] = acc0 ^ acc1;
+    uint32_t* out = parts + ((size_t)blockIdx.y * kJSplit + blockIdx.x) * kN;
+    out[threadIdx.x] = lo;
+    if (threadIdx.x + kJHalf < kN) out[threadIdx.x + kJHalf] = hi;
 }
 
 // stream s: blocks [1 + P s, min(1 + P (s + 1), nblk)); stream 0 also writes block 0 (the state's key array)
