@@ -63,7 +63,7 @@ constexpr int kJListStride = ((kDeg + 1 + kJSplit * kJBatch - 1) / (kJSplit * kJ
 constexpr int kJPart = kJListStride / kJSplit;        // list entries per workgroup (a multiple of kJBatch)
 constexpr int kAttRounds = 8;                         // attempts per thread, interleaved: attempt a0 + 256 r + t
 constexpr int kAttPerWG = kNT * kAttRounds;
-constexpr size_t kJumpLds = (kSeqPad + 2 * kJHalf) * sizeof(uint32_t);   // 87 KB
+constexpr size_t kJumpLds = (kSeqPad + 2 * kJHalf + kJPart) * sizeof(uint32_t);   // 107 KB
 constexpr int kScanT = 1024;
 
 __device__ __forceinline__ uint32_t mt_mix(uint32_t a, uint32_t b) {
@@ -150,39 +150,63 @@ __global__ __launch_bounds__(kTT) void np_seq_kernel(const uint32_t* __restrict_
 // The polynomial comes as the list of its set bits (mppi_np_set_jumps) as LDS byte offsets, split over
 // kJSplit workgroups (blockIdx.x), each list part padded to kJPart entries with the offset of kSeqPad (a window
 // of zero words past the sequence); each workgroup writes its partial XOR of every output word and
-// np_gen_kernel XORs the parts.  Per batch of kJBatch bits: the offsets by scalar loads, then every window
-// read of the batch issued together (one ds_read2st64 per bit and lane: its two output words), then XOR3s.
+// np_gen_kernel XORs the parts.  Per batch of kJBatch bits: the offsets (broadcast LDS reads), then every
+// window read of the batch issued together (one ds_read2st64 per bit and lane: its two output words), then XOR3s.
 __global__ __launch_bounds__(kJT) void np_jump_kernel(const uint32_t* __restrict__ seq, const uint32_t* __restrict__ bits,
                                                       const int* __restrict__ nbits, uint32_t* __restrict__ parts) {
-    extern __shared__ uint32_t s_seq[];   // kSeqBlocks x 624 words, then 640 zero words (the padding's window)
+    extern __shared__ uint32_t s_seq[];   // kSeqBlocks x 624 words, 640 zero words, then the list part
+    uint32_t* s_list = s_seq + kSeqPad + 2 * kJHalf;
     {   // every load in flight before the first LDS store
         constexpr int kVec = kSeqBlocks * kN / 4, kIt = (kVec + kJT - 1) / kJT;
+        constexpr int kLVec = kJPart / 4, kLIt = (kLVec + kJT - 1) / kJT;
         const uint4* src = reinterpret_cast<const uint4*>(seq);
-        uint4 v[kIt];
+        const uint4* lsrc = reinterpret_cast<const uint4*>(bits + (size_t)blockIdx.y * kJListStride + blockIdx.x * kJPart);
+        uint4 v[kIt], l[kLIt];
 #pragma unroll
         for (int q = 0; q < kIt; ++q) {
             const int i = threadIdx.x + q * kJT;
             if (i < kVec) v[q] = src[i];
         }
 #pragma unroll
+        for (int q = 0; q < kLIt; ++q) {
+            const int i = threadIdx.x + q * kJT;
+            if (i < kLVec) l[q] = lsrc[i];
+        }
+#pragma unroll
         for (int q = 0; q < kIt; ++q) {
             const int i = threadIdx.x + q * kJT;
             if (i < kVec) reinterpret_cast<uint4*>(s_seq)[i] = v[q];
+        }
+#pragma unroll
+        for (int q = 0; q < kLIt; ++q) {
+            const int i = threadIdx.x + q * kJT;
+            if (i < kLVec) reinterpret_cast<uint4*>(s_list)[i] = l[q];
         }
         for (int i = threadIdx.x; i < 2 * kJHalf; i += kJT) s_seq[kSeqPad + i] = 0u;
     }
     const int nb = min(max(nbits[blockIdx.y] - (int)blockIdx.x * kJPart, 0), kJPart);   // a multiple of kJBatch
     __syncthreads();
-    // lane t: output words t and t + 320 (< 624), read as one ds_read2st64_b32 (offset1 = 5 x 64 words)
+    // lane t: output words t and t + 320 (< 624), read as one ds_read2st64_b32 (offset1 = 5 x 64 words); the
+    // window offsets come from the list in LDS (broadcast reads, in order with the window reads: no scalar
+    // load's wait couples to them)
     const uint32_t jb = 4u * threadIdx.x;
-    const uint32_t* L = bits + (size_t)blockIdx.y * kJListStride + blockIdx.x * kJPart;   // scalar loads
+    const uint4* L = reinterpret_cast<const uint4*>(s_list);
     const char* S = reinterpret_cast<const char*>(s_seq);
     uint32_t lo = 0, hi = 0;
     for (int b = 0; b < nb; b += kJBatch) {
+        uint32_t d[kJBatch];
+#pragma unroll
+        for (int q = 0; q < kJBatch / 4; ++q) {
+            const uint4 e = L[b / 4 + q];
+            d[4 * q] = e.x;
+            d[4 * q + 1] = e.y;
+            d[4 * q + 2] = e.z;
+            d[4 * q + 3] = e.w;
+        }
         uint32_t r[kJBatch], h[kJBatch];
 #pragma unroll
         for (int q = 0; q < kJBatch; ++q) {
-            const char* a = S + (L[b + q] + jb);
+            const char* a = S + (d[q] + jb);
             r[q] = *reinterpret_cast<const uint32_t*>(a);
             h[q] = *reinterpret_cast<const uint32_t*>(a + 4 * kJHalf);
         }
