@@ -54,8 +54,9 @@ constexpr int kPolyWords = MPPI_NP_POLY_WORDS;        // 312 x 64 bits: a polyno
 constexpr int kSeqBlocks = (kDeg + kN) / kN + 1;      // 34: the windows d + j < 19937 + 624 of the jumps
 constexpr int kNT = 256;                              // threads of the attempt kernels
 constexpr int kTT = 640;                              // threads of the twist kernels: one word per thread
-constexpr int kJT = 320;                              // threads of a jump workgroup: two output words each
-constexpr int kJHalf = 320;                           // the second word of a lane: 5 x 64 words on
+constexpr int kJHalf = 320;                           // lanes of a jump group; a lane's second word: 5 x 64 on
+constexpr int kJGroups = 3;                           // groups of a jump workgroup, each a share of the bits
+constexpr int kJT = kJGroups * kJHalf;                // threads of a jump workgroup (15 waves)
 constexpr int kJSplit = 4;                            // workgroups per stream, each a quarter of the set bits
 constexpr int kJBatch = 32;                           // set bits of a jump polynomial read per batch
 constexpr int kSeqPad = kSeqBlocks * kN;              // list padding: s_seq[kSeqPad + j] = 0 for j < 640
@@ -186,14 +187,18 @@ __global__ __launch_bounds__(kJT) void np_jump_kernel(const uint32_t* __restrict
     }
     const int nb = min(max(nbits[blockIdx.y] - (int)blockIdx.x * kJPart, 0), kJPart);   // a multiple of kJBatch
     __syncthreads();
-    // lane t: output words t and t + 320 (< 624), read as one ds_read2st64_b32 (offset1 = 5 x 64 words); the
-    // window offsets come from the list in LDS (broadcast reads, in order with the window reads: no scalar
-    // load's wait couples to them)
-    const uint32_t jb = 4u * threadIdx.x;
+    // kJGroups groups of kJHalf lanes, each a contiguous share of the list part; lane t of a group: output words
+    // t and t + 320 (< 624), read as one ds_read2st64_b32 (offset1 = 5 x 64 words); the window offsets come
+    // from the list in LDS (broadcast reads, in order with the window reads: no scalar load's wait couples to
+    // them); the groups' XORs meet in LDS at the end
+    const int grp = threadIdx.x / kJHalf, t = threadIdx.x - grp * kJHalf;
+    const int per = (nb / kJBatch + kJGroups - 1) / kJGroups * kJBatch;
+    const int b0 = grp * per, b1 = min(b0 + per, nb);
+    const uint32_t jb = 4u * t;
     const uint4* L = reinterpret_cast<const uint4*>(s_list);
     const char* S = reinterpret_cast<const char*>(s_seq);
     uint32_t lo = 0, hi = 0;
-    for (int b = 0; b < nb; b += kJBatch) {
+    for (int b = b0; b < b1; b += kJBatch) {
         uint32_t d[kJBatch];
 #pragma unroll
         for (int q = 0; q < kJBatch / 4; ++q) {
@@ -216,9 +221,22 @@ __global__ __launch_bounds__(kJT) void np_jump_kernel(const uint32_t* __restrict
             hi = hi ^ h[q] ^ h[q + 1];
         }
     }
-    uint32_t* out = parts + ((size_t)blockIdx.y * kJSplit + blockIdx.x) * kN;
-    out[threadIdx.x] = lo;
-    if (threadIdx.x + kJHalf < kN) out[threadIdx.x + kJHalf] = hi;
+    __syncthreads();   // every group is done with the sequence: its first words hold the groups' results
+    if (grp > 0) {
+        s_seq[(grp - 1) * 2 * kJHalf + t] = lo;
+        s_seq[(grp - 1) * 2 * kJHalf + kJHalf + t] = hi;
+    }
+    __syncthreads();
+    if (grp == 0) {
+#pragma unroll
+        for (int g = 1; g < kJGroups; ++g) {
+            lo ^= s_seq[(g - 1) * 2 * kJHalf + t];
+            hi ^= s_seq[(g - 1) * 2 * kJHalf + kJHalf + t];
+        }
+        uint32_t* out = parts + ((size_t)blockIdx.y * kJSplit + blockIdx.x) * kN;
+        out[t] = lo;
+        if (t + kJHalf < kN) out[t + kJHalf] = hi;
+    }
 }
 
 // stream s: blocks [1 + P s, min(1 + P (s + 1), nblk)); stream 0 also writes block 0 (the state's key array)
