@@ -457,9 +457,10 @@ struct Plan {
 
 // attempts generated: 4/3 of the pairs plus 4096 (acceptance pi/4: 1.27 attempts per pair expected), as the
 // host path (np_legacy_gauss.c); the block stride P of the streams from a cost model of the two parallel
-// phases on MI355X: the jumps run in rounds of 64 streams (kJSplit workgroups each, one per CU) of kJumpRoundUs,
-// a stream twists its P blocks at kBlockUs each (MPPI_NP_STRIDE forces P, for measurements)
-constexpr double kJumpRoundUs = 40.0, kBlockUs = 0.4;
+// phases, measured on MI355X (profiles/r15np/): the jumps run in rounds of 64 streams (kJSplit workgroups each,
+// one per CU) of ~70 us, a stream twists its P blocks at ~0.38 us each (MPPI_NP_STRIDE forces P, for
+// measurements).  Config 3 (8.4 M normals, 35.9 k blocks): P = 256, 141 streams.
+constexpr double kJumpRoundUs = 70.0, kBlockUs = 0.38;
 Plan make_plan(long long n, int pos, int has_gauss) {
     Plan p;
     p.need = n - (has_gauss ? 1 : 0);
