@@ -364,7 +364,8 @@ class ChainMPPIController:
                  terminal_cost_weight: np.ndarray = np.array([5.0, 5.0, 50.0, 50.0]),
                  visualize_optimal_traj=True, visualze_sampled_trajs=False, *, chain: ChainParams = ChainParams(),
                  u_init=None, device: int | None = None, verbose: bool = False, noise: str = "numpy", seed: int = 0,
-                 process_group=None, exchange: str = "auto", precision: str = "auto") -> None:
+                 process_group=None, exchange: str = "auto", precision: str = "auto",
+                 numpy_noise_on_device: bool = True) -> None:
         self.chain = chain
         if precision not in ("auto", "f32", "f64"):
             raise ValueError("precision must be 'auto', 'f32' or 'f64'")
@@ -403,6 +404,8 @@ class ChainMPPIController:
         self._step_count = 0
         self.keep_costs = False
         self.last_S = None
+        self.numpy_noise_on_device = numpy_noise_on_device   # noise="numpy": the same stream drawn on the device
+        self._npdev = None             # its engine.NpDeviceStream (False: unavailable here)
 
     # the per-engine fields: the active engine's live here, the others' are parked in _slots
     _SLOT = ("_engine", "_engine_built_for", "_xmode", "_noise_ready", "_noise_dev", "_partial", "_S_dev",
@@ -506,6 +509,57 @@ class ChainMPPIController:
         std = hostrng.multivariate_normal_std(np.zeros(self.dim_u), sigma, (self.K, self.T), self._zbuf.numpy())
         return std if std is not None else self._calc_epsilon(sigma, self.K, self.T, self.dim_u)
 
+    def _device_reference_noise(self, prec: str):
+        """control.py:84 on the device, as MPPIControllerForPathTracking._device_reference_noise: NumPy's stream
+        (values and RNG state) drawn into the noise buffer of the `prec` engine, the one the step runs on first
+        (a step re-run in the other precision copies it over).  None: the host path draws."""
+        from .controller import DeviceDrawn
+        if not self.numpy_noise_on_device or self._npdev is False:
+            return None
+        if "_calc_epsilon" in self.__dict__ or type(self)._calc_epsilon is not ChainMPPIController._calc_epsilon:
+            return None
+        sig = self.Sigma
+        if not (isinstance(sig, np.ndarray) and sig.shape == (self.dim_u, self.dim_u)):
+            return None
+        n = int(self.K) * int(self.T) * self.dim_u
+        if n < hostrng._MIN_NORMALS or n >= 2 ** 31:
+            return None
+        state = np.random.get_state()
+        if state[0] != "MT19937":
+            return None
+        plan = hostrng.monomial_plan(np.zeros(self.dim_u), sig)
+        if plan is None:
+            return None
+        self._activate(prec)
+        key = self._engine_key()
+        if key != self._engine_built_for:
+            try:
+                np.linalg.inv(sig)
+            except np.linalg.LinAlgError:
+                return None
+        eng = self._get_engine(key)
+        if self._npdev is None:
+            try:
+                from .engine import NpDeviceStream
+                self._npdev = NpDeviceStream(eng.device)
+            except (RuntimeError, OSError):
+                self._npdev = False
+                return None
+        if not plan[3]:
+            import warnings
+            warnings.warn("covariance is not symmetric positive-semidefinite.", RuntimeWarning)   # NumPy's
+        eng._sync_stream()
+        kl = eng.K_local
+        self._npdev.draw(state, (int(self.K), int(self.T), self.dim_u), plan, self._noise_dev, eng.stream.cuda_stream,
+                         eng.k_offset, kl, (self.dim_u * kl, 1, kl))   # [T][n][K_local]
+        new = self._npdev.result()
+        if new is None:
+            return None
+        np.random.set_state(new)
+        d = DeviceDrawn(float(np.sum(new[1][:16], dtype=np.float64)) + new[2])
+        d.buf = self._noise_dev
+        return d
+
     def _calc_epsilon(self, sigma, size_sample, size_time_step, size_dim_u):
         """control.py:154-164 — NumPy's legacy global RNG, n-dimensional"""
         if sigma.shape[0] != sigma.shape[1] or sigma.shape[0] != size_dim_u or size_dim_u < 1:
@@ -520,15 +574,17 @@ class ChainMPPIController:
         if self.prev_waypoints_idx >= self.ref_path.shape[0] - 1:
             print("[ERROR] Reached the end of the reference path.")
             raise IndexError
+        auto = self.precision == "auto"
+        prec = ("f64" if self._spread else "f32") if auto else self.precision
         if self.noise_source == "numpy":
-            epsilon = self._reference_noise()
+            epsilon = self._device_reference_noise(prec)
+            if epsilon is None:
+                epsilon = self._reference_noise()
         else:
             epsilon = None
         step = self._step_count
         self._step_count += 1
         window = self.ref_path[self.prev_waypoints_idx:(self.prev_waypoints_idx + SEARCH_IDX_LEN)]
-        auto = self.precision == "auto"
-        prec = ("f64" if self._spread else "f32") if auto else self.precision
         out = self._device_step_x(prec, x0, window, u, epsilon, step)
         if auto:
             self._spread = self.last_eta - 1.0 > self.ETA_TOL
@@ -568,7 +624,11 @@ class ChainMPPIController:
         if key != self._engine_built_for:
             np.linalg.inv(self.Sigma)                      # LinAlgError as control.py:106 (Sigma checked when it changes)
         eng = self._get_engine(key)
-        if isinstance(epsilon, hostrng.StdNoise):
+        if getattr(epsilon, "buf", None) is not None:     # a device draw (DeviceDrawn), into one engine's buffer
+            if epsilon.buf is not self._noise_dev:
+                eng._sync_stream()
+                self._noise_dev.copy_(epsilon.buf)         # the step re-run in the other precision
+        elif isinstance(epsilon, hostrng.StdNoise):
             self._zbuf_ev = eng.upload_std_noise(epsilon, self._zbuf, self._noise_dev)
         elif epsilon is not None:
             eng.upload_noise(epsilon[eng.k_offset:eng.k_offset + eng.K_local], out=self._noise_dev)
@@ -650,6 +710,9 @@ class ChainMPPIController:
         self._xmode = None
 
     def close(self):
+        if self._npdev:
+            self._npdev.close()
+        self._npdev = None
         self._close_active()
         for parked in self._slots.values():
             if parked.get("_engine") is not None:

@@ -131,3 +131,35 @@ def test_controller_device_draw_equals_host_draw():
         np.testing.assert_array_equal(ua, ub)
         np.testing.assert_array_equal(oa, ob)
     assert _same_state(st_a, st_b)
+
+
+def _chain_loop(device_draw: bool, lam: float, ticks=3, K=4096, T=16):
+    from mppi_robotarm_amd.chain import CHAIN7_X0, ChainMPPIController, gravity_torque
+    from conftest import load_paths
+    c = ChainMPPIController(0.006, load_paths()["xydq_circle"], T, K, param_lambda=lam, device=0,
+                            u_init=gravity_torque(CHAIN7_X0[:7]), numpy_noise_on_device=device_draw)
+    np.random.seed(4)
+    out, precs = [], []
+    for i in range(ticks):
+        c.prev_waypoints_idx = 0
+        u0, u_seq, opt, _ = c.calc_control_input(CHAIN7_X0)
+        out.append((u_seq.copy(), opt.copy()))
+        precs.append(c.last_precision)
+    used = c._npdev
+    c.close()
+    return out, np.random.get_state(), used, precs
+
+
+@pytest.mark.parametrize("lam", [100.0, 3.0e5])
+def test_chain_controller_device_draw_equals_host_draw(lam):
+    """The 7-link drop-in's default noise on the device: the host draw's steps bit for bit; at lambda = 3e5 the
+    weights spread and precision="auto" re-runs each step in fp64 on the other engine (the draw copied into its
+    noise buffer)."""
+    a, st_a, used, precs = _chain_loop(True, lam)
+    b, st_b, _, precs_b = _chain_loop(False, lam)
+    assert used, "the chain controller did not take the device draw"
+    assert precs == precs_b and ("f64" in precs) == (lam > 1e4)
+    for (ua, oa), (ub, ob) in zip(a, b):
+        np.testing.assert_array_equal(ua, ub)
+        np.testing.assert_array_equal(oa, ob)
+    assert _same_state(st_a, st_b)

@@ -152,19 +152,25 @@ def test_harness_plant_matches_reference_loop():
 
 
 def test_bench_valu_roofline_from_committed_counters():
-    """bench.py's VALU issue roofline from the committed PMC summary: one wave per SIMD at c3,
-    two at c5; fractions of the SIMD's issue rate in (0, 1]."""
+    """bench.py's VALU issue roofline from the committed PMC summary against the committed issue-rate
+    microbenchmark (profiles/ubench_issue.json, tools/ubench_issue.hip): one wave per SIMD at c3 (priced also
+    against the lone-wave rate), two at c5; fractions in (0, 1]."""
     import json
     import os
     import bench
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    lone_ns, simd_ns = bench.issue_ceilings()
+    assert simd_ns < lone_ns   # more waves per SIMD issue faster than one alone
     for name, kern_ms, wps in (("traffic.json", 0.0293, 1.0), ("traffic_c5.json", 0.250, 2.0)):
         tj = json.load(open(os.path.join(root, "profiles", name)))
         v = bench.valu_roofline(tj, kern_ms)
         assert v["waves_per_simd"] == wps and 0.0 < v["frac"] <= 1.0
-        assert v["frac"] == pytest.approx(tj["valu_insts_per_launch"] / bench.SIMDS * bench.SIMD_ISSUE_CYC
-                                          / (kern_ms * 1e-3 * bench.CLOCK_HZ))
+        per_simd = tj["valu_insts_per_launch"] / min(tj["waves_per_launch"], bench.SIMDS)
+        assert v["frac"] == pytest.approx(per_simd / (kern_ms * 1e6) * simd_ns)
         assert ("frac_one_wave_ceiling" in v) == (wps == 1.0)
+        if wps == 1.0:
+            assert 0.0 < v["frac_one_wave_ceiling"] <= 1.0
+            assert v["frac_one_wave_ceiling"] == pytest.approx(per_simd / (kern_ms * 1e6) * lone_ns)
     assert bench.valu_roofline({}, 0.03) is None
 
 
