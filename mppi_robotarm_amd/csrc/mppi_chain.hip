@@ -45,6 +45,9 @@ constexpr int kCMaxVals = kMaxT * kCMax;    // T N values per row, at most
 #ifndef MPPI_CHAIN_CPU
 #define MPPI_CHAIN_CPU 2
 #endif
+#ifndef MPPI_CHAIN_LIST   // A/B variant, not the product: list rows (mppi_device.h) with the poll hand-off
+#define MPPI_CHAIN_LIST 0
+#endif
 constexpr int kCPF = MPPI_CHAIN_CPF;        // noise steps in flight per lane (N rows each)
 #ifndef MPPI_Q4_PF
 #define MPPI_Q4_PF 4   // 2 and 4 measured: equal at K = 16384, 4 -2.1 % at K = 32768 (profiles/r13/chain_quad_ring_depth_ab.txt)
@@ -479,7 +482,7 @@ __device__ __forceinline__ void chain_nominal_prefetch(const ChainStep* s, int T
 // max(A_i, B_j) over i + j = k).  80 min / max for the four windows against 4 x 58 with median10, and one
 // pass of the workgroup instead of four; the same element is selected, so the same bits.
 template <int N>
-__device__ void chain_update_block(ChainStep* nxt, const ChainConst& c, CScratch& sm, const double (&u4)[kMedRun]) {
+__device__ __forceinline__ void chain_update_block(ChainStep* nxt, const ChainConst& c, CScratch& sm, const double (&u4)[kMedRun]) {
     const int tid = threadIdx.x, T = c.T;
     const int q = tid / N, d = tid - q * N, t0 = kMedRun * q;
     if (t0 < T) {
@@ -1117,8 +1120,17 @@ __global__ __launch_bounds__(kCT) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
         publish(blockIdx.x * stride + 1, eta_b);
     }
     nl = __builtin_amdgcn_readfirstlane(nl);
+    // MPPI_CHAIN_LIST (A/B variant): a row with few weighted samples publishes them, not its columns (list rows,
+    // mppi_device.h); the merges that need them gather from the noise
+    constexpr bool kList = POLL && MPPI_CHAIN_LIST;
     if (skip) {
         // no merge reads this row past rho
+    } else if (kList && nl <= kListMax && 2 * nl + 1 <= nval) {
+        if (tid == 0) publish(blockIdx.x * stride + 2, list_mode_word(nl));
+        if (tid < nl) {
+            publish(blockIdx.x * stride + 3 + 2 * tid, (double)s_k[tid]);
+            publish(blockIdx.x * stride + 4 + 2 * tid, s_e[tid]);
+        }
     } else if (nl <= kSparseMax) {
         // column (t, d) = t N + d of the noise is the row noise[col K : col K + K]
         for (int col = tid; col < nval; col += kCT) {
@@ -1164,15 +1176,19 @@ __global__ __launch_bounds__(kCT) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
     if constexpr (POLL) {
         if ((int)blockIdx.x != g * kGroup) return;
         STAMP(3, NOW());
+        const ListSrc ls{noise, K};
         if (ngroups == 1) {
-            merge_rows_block<kCT, kCMaxCh, true, true>(slab_r, 0, gsz, geo, c.inv_lambda, sm, nullptr, 0, partial_out,
-                                                       w_eps_out, tag, tmo);
+            merge_rows_block<kCT, kCMaxCh, true, true, decltype(sm), kList>(slab_r, 0, gsz, geo, c.inv_lambda, sm,
+                                                                            nullptr, 0, partial_out, w_eps_out, tag,
+                                                                            tmo, 0ull, nullptr, ls);
         } else if (blockIdx.x == 0 && nrows <= kDirectRows &&
-                   direct_merge<kCT, kCMaxCh, true>(slab_r, nrows, geo, c.inv_lambda, sm, partial_out, w_eps_out, tag,
-                                                    tmo)) {
+                   direct_merge<kCT, kCMaxCh, true, decltype(sm), kList>(slab_r, nrows, geo, c.inv_lambda, sm,
+                                                                         partial_out, w_eps_out, tag, tmo, nullptr,
+                                                                         ls)) {
         } else {
-            merge_rows_block<kCT, kCMaxCh, false, true>(slab_r, g * kGroup, gsz, geo, c.inv_lambda, sm, &gslab_r, g,
-                                                        nullptr, nullptr, tag, tmo);
+            merge_rows_block<kCT, kCMaxCh, false, true, decltype(sm), kList>(slab_r, g * kGroup, gsz, geo,
+                                                                             c.inv_lambda, sm, &gslab_r, g, nullptr,
+                                                                             nullptr, tag, tmo, 0ull, nullptr, ls);
             STAMP(10, NOW());
             if (blockIdx.x != 0) return;
             STAMP(4, NOW());

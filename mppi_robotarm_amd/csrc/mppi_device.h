@@ -522,6 +522,91 @@ __device__ __forceinline__ void put_final(double rho, const double (&acc)[MAXCH]
     __syncthreads();
 }
 
+// ------------------------------------------------------------ list rows
+// A workgroup row whose weighted samples are few (nl <= kListMax) can carry them instead of its noise columns
+// (the chain kernel, poll hand-off): slot 2 holds the mode word {lo = nl, hi = kListHi} (a signalling NaN, which
+// no column sum is), slots 3 + 2l and 4 + 2l the l-th weighted sample's local index and weight, ascending.  The
+// merger that needs the row's columns gathers them from the noise itself with the row gather's operations in its
+// order (gather_col_n: fp64 fma over l from 0), so a list row merges to the same bits as the column row it
+// replaces, and only the rows that carry weight in some merge are ever gathered: a row's own gather cannot know
+// that, and read a cache line per value for every row (the chain's [T][n][K] noise).  An A/B variant
+// (MPPI_CHAIN_LIST, TRIED.md): the shard's traffic 1.14x -> 1.04x, but +2.7 % time, the merger's header poll
+// and noise gather being on the critical path where the rows' own gathers ran beside the merge.
+#ifndef MPPI_LIST_MAX
+#define MPPI_LIST_MAX 2
+#endif
+constexpr int kListMax = MPPI_LIST_MAX;
+constexpr unsigned kListHi = 0x7ff4c0deu;
+struct ListSrc {
+    const float* noise = nullptr;   // the row's column j (t n + d) of sample k at noise[j K + k]
+    int K = 0;
+};
+__device__ __forceinline__ double list_mode_word(int nl) {
+    return __longlong_as_double((long long)(((unsigned long long)kListHi << 32) | (unsigned)nl));
+}
+
+// The lane's row header at granule offset `off` (kOffRange: none): eta (slot 1), the mode word and, for a list
+// row, its entries, polled until valid.  nl = 0: the row carries columns.  True if a poll gave up.
+__device__ __forceinline__ bool poll_list_header(__amdgpu_buffer_rsrc_t rows, int off, unsigned tag, double& eta,
+                                                 int& nl, int (&k)[kListMax], double (&w)[kListMax], unsigned* tmo,
+                                                 unsigned long long deadline) {
+    const int lane = threadIdx.x & 63;
+    u32x4 h[2 + 2 * kListMax];
+    bool gave_up = false;
+    for (unsigned spins = 0;; ++spins) {
+        asm volatile("" ::: "memory");
+#pragma unroll
+        for (int s = 0; s < 2 + 2 * kListMax; ++s) h[s] = ld_gran(rows, off + 1 + s);
+        const int n = h[1][2] == kListHi ? (int)(h[1][0] & 0xffu) : 0;
+        bool ok = gran_ok(h[0], tag) && gran_ok(h[1], tag);
+#pragma unroll
+        for (int l = 0; l < kListMax; ++l) ok = ok && (l >= n || (gran_ok(h[2 + 2 * l], tag) && gran_ok(h[3 + 2 * l], tag)));
+        if (__all(off >= kOffRange || ok)) break;
+        MPPI_SPIN_OR_GIVE_UP_L(spins, deadline, tmo, lane, gave_up = true);
+    }
+    eta = gran_val(h[0]);
+    nl = h[1][2] == kListHi ? min((int)(h[1][0] & 0xffu), kListMax) : 0;
+#pragma unroll
+    for (int l = 0; l < kListMax; ++l) {
+        k[l] = l < nl ? (int)gran_val(h[2 + 2 * l]) : 0;
+        w[l] = gran_val(h[3 + 2 * l]);
+    }
+    return gave_up;
+}
+
+// Entries of a load batch (x[j]: row b0 + j / MAXCH of the lanes' headers, merged column tid + (j % MAXCH) NT)
+// for the list rows among them; column rows' entries are left as loaded.  Merged column 0 is eta, column 1 + c
+// the noise column c.
+template <int NT, int MAXCH, int LB>
+__device__ __forceinline__ void list_entries(double (&x)[LB], int b0, int nb, int nl_l, const int (&k_l)[kListMax],
+                                             const double (&w_l)[kListMax], double eta_l, int ncol, const ListSrc& ls) {
+    const int tid = threadIdx.x;
+    float e[LB][kListMax];
+#pragma unroll
+    for (int j = 0; j < LB; ++j) {
+        const int i = min(b0 + j / MAXCH, 63), col = tid + (j % MAXCH) * NT;
+        const int nli = b0 + j / MAXCH < nb ? __builtin_amdgcn_readlane(nl_l, i) : 0;   // uniform
+        const size_t cb = (size_t)min(max(col - 1, 0), ncol - 2) * ls.K;
+#pragma unroll
+        for (int l = 0; l < kListMax; ++l) {
+            const int kk = __builtin_amdgcn_readlane(k_l[l], i);
+            e[j][l] = l < nli ? ls.noise[cb + kk] : 0.f;
+        }
+    }
+#pragma unroll
+    for (int j = 0; j < LB; ++j) {
+        const int i = min(b0 + j / MAXCH, 63), col = tid + (j % MAXCH) * NT;
+        const int nli = b0 + j / MAXCH < nb ? __builtin_amdgcn_readlane(nl_l, i) : 0;
+        if (nli > 0) {
+            double a = 0.0;
+#pragma unroll
+            for (int l = 0; l < kListMax; ++l)
+                if (l < nli) a = fma(readlane_f64(w_l[l], i), (double)e[j][l], a);
+            x[j] = col == 0 ? readlane_f64(eta_l, i) : col < ncol ? a : 0.0;
+        }
+    }
+}
+
 // Merge n rows (read write-through from `rows`, rows row0 .. row0 + n - 1) with
 // a log-sum-exp rescale: rho = min rho_i, s_i = exp((rho - rho_i) / lambda),
 // eta = sum s_i eta_i, N = sum s_i N_i, in ascending row order (deterministic);
@@ -541,14 +626,15 @@ __device__ __forceinline__ void put_final(double rho, const double (&acc)[MAXCH]
 //   rows that carry weight, 16 / MAXCH rows per load batch.
 // The merged row goes to out_wt (same format, next level) or, with `final`,
 // to put_final.
-template <int NT, int MAXCH, bool final, bool GRAN, class SM>
+template <int NT, int MAXCH, bool final, bool GRAN, class SM, bool LIST = false>
 __device__ __forceinline__ void merge_rows_block(__amdgpu_buffer_rsrc_t rows, int row0, int n, const RowGeo& geo,
                                                  double inv_lambda, SM& sm, const __amdgpu_buffer_rsrc_t* out_wt,
                                                  int out_idx, double* out_row, double* w_eps_out, unsigned tag,
                                                  unsigned* tmo, unsigned long long deadline = 0ull,
-                                                 bool* failed = nullptr) {
+                                                 bool* failed = nullptr, const ListSrc& ls = ListSrc{}) {
     // deadline / failed: the polls' deadline (s_memrealtime; 0: the spin bound alone), and (when given) whether
-    // any poll of the workgroup gave up (uniform)
+    // any poll of the workgroup gave up (uniform).  LIST (GRAN only): the rows may be list rows (above).
+    static_assert(!LIST || GRAN, "list rows: poll hand-off");
     constexpr bool EAGER = !GRAN && MAXCH == 1;  // one round trip per round of 32 rows
     constexpr int LB = EAGER ? 32 : 16;         // loads per batch per thread
     constexpr int RB = LB / MAXCH;              // rows per load batch
@@ -618,8 +704,14 @@ __device__ __forceinline__ void merge_rows_block(__amdgpu_buffer_rsrc_t rows, in
         } else {
             // lane k < nrr: the round's k-th weighted row (ascending)
             const int krow = lane < nrr ? select_bit(rel, lane) : 0;
+            // LIST: every weighted row's header first (eta with it)
+            int nl_l = 0, k_l[kListMax];
+            double w_l[kListMax];
+            if constexpr (LIST)
+                gave_up |= poll_list_header(rows, lane < nrr ? (rb + krow) * stride : kOffRange, tag, eta_l, nl_l, k_l,
+                                            w_l, tmo, deadline);
             for (int b0 = 0; b0 < nrr; b0 += RB) {
-                const bool eta_on = b0 == 0 && lane < nrr;
+                const bool eta_on = !LIST && b0 == 0 && lane < nrr;
                 const int eidx = eta_on ? (rb + krow) * stride + 1 : kOffRange;
                 double x[LB];
                 if constexpr (GRAN) {
@@ -631,7 +723,8 @@ __device__ __forceinline__ void merge_rows_block(__amdgpu_buffer_rsrc_t rows, in
 #pragma unroll
                         for (int j = 0; j < LB; ++j) {
                             const int i = b0 + j / MAXCH, col = tid + (j % MAXCH) * NT;
-                            const bool on = i < nrr && col < ncol;
+                            const bool on = i < nrr && col < ncol &&
+                                            (!LIST || __builtin_amdgcn_readlane(nl_l, min(i, 63)) == 0);
                             gv[j] = ld_gran(rows, on ? (rb + __builtin_amdgcn_readlane(krow, i)) * stride + 1 + col
                                                      : kOffRange);
                             ok = ok && (!on || gran_ok(gv[j], tag));
@@ -639,9 +732,10 @@ __device__ __forceinline__ void merge_rows_block(__amdgpu_buffer_rsrc_t rows, in
                         if (__all(ok)) break;
                         MPPI_SPIN_OR_GIVE_UP_L(spins, deadline, tmo, lane, gave_up = true);
                     }
-                    if (b0 == 0) eta_l = gran_val(ge);
+                    if (!LIST && b0 == 0) eta_l = gran_val(ge);
 #pragma unroll
                     for (int j = 0; j < LB; ++j) x[j] = gran_val(gv[j]);
+                    if constexpr (LIST) list_entries<NT, MAXCH, LB>(x, b0, nrr, nl_l, k_l, w_l, eta_l, ncol, ls);
                 } else {
                     if (b0 == 0) eta_l = ld_wt(rows, eidx);
 #pragma unroll
@@ -689,10 +783,12 @@ __device__ __forceinline__ void merge_rows_block(__amdgpu_buffer_rsrc_t rows, in
 // on the critical path instead of two.  Returns false (uniformly) when more rows
 // carry weight; the caller then merges through the group rows.  Wave-local
 // like merge_rows_block; the result goes out as in a final merge.
-template <int NT, int MAXCH, bool GRAN, class SM>
+template <int NT, int MAXCH, bool GRAN, class SM, bool LIST = false>
 __device__ __forceinline__ bool direct_merge(__amdgpu_buffer_rsrc_t rows, int n, const RowGeo& geo,
                                              double inv_lambda, SM& sm, double* out_row, double* w_eps_out,
-                                             unsigned tag, unsigned* tmo, unsigned long long* dbg = nullptr) {
+                                             unsigned tag, unsigned* tmo, unsigned long long* dbg = nullptr,
+                                             const ListSrc& ls = ListSrc{}) {
+    static_assert(!LIST || (GRAN && MAXCH > 1), "list rows: poll hand-off, one row group");
     constexpr int P = kDirectRows / 64;
     constexpr int LB = 16;                      // loads per batch per thread
     constexpr int RB = LB / MAXCH;              // rows per load batch
@@ -781,27 +877,35 @@ __device__ __forceinline__ bool direct_merge(__amdgpu_buffer_rsrc_t rows, int n,
     if (G == 1) {
         // one group: the rows of a batch are wave-uniform (v_readlane); eta as a
         // scalar in the same row order as column 0
+        // LIST: every weighted row's header first (eta with it)
+        int nl_l = 0, k_l[kListMax];
+        double w_l[kListMax];
+        if constexpr (LIST)
+            (void)poll_list_header(rows, mine ? row * stride : kOffRange, tag, eta_k, nl_l, k_l, w_l, tmo, 0ull);
         for (int b0 = 0; b0 < nrel; b0 += RB) {
             double v[LB];
             if constexpr (GRAN) {
+                const bool eta_on = !LIST && b0 == 0 && mine;
                 u32x4 ge, gv[LB];
                 for (unsigned spins = 0;; ++spins) {
                     asm volatile("" ::: "memory");
-                    ge = ld_gran(rows, (b0 == 0 && mine) ? row * stride + 1 : kOffRange);
-                    bool ok = !(b0 == 0 && mine) || gran_ok(ge, tag);
+                    ge = ld_gran(rows, eta_on ? row * stride + 1 : kOffRange);
+                    bool ok = !eta_on || gran_ok(ge, tag);
 #pragma unroll
                     for (int j = 0; j < LB; ++j) {
                         const int i = b0 + j / MAXCH, col = tid + (j % MAXCH) * NT;
-                        const bool on = i < nrel && col < ncol;
+                        const bool on = i < nrel && col < ncol &&
+                                        (!LIST || __builtin_amdgcn_readlane(nl_l, min(i, 63)) == 0);
                         gv[j] = ld_gran(rows, on ? __builtin_amdgcn_readlane(row, i) * stride + 1 + col : kOffRange);
                         ok = ok && (!on || gran_ok(gv[j], tag));
                     }
                     if (__all(ok)) break;
                     MPPI_SPIN_OR_GIVE_UP(spins, tmo, lane);
                 }
-                if (b0 == 0) eta_k = gran_val(ge);
+                if (!LIST && b0 == 0) eta_k = gran_val(ge);
 #pragma unroll
                 for (int j = 0; j < LB; ++j) v[j] = gran_val(gv[j]);
+                if constexpr (LIST) list_entries<NT, MAXCH, LB>(v, b0, nrel, nl_l, k_l, w_l, eta_k, ncol, ls);
             } else {
                 if (b0 == 0) eta_k = ld_wt(rows, mine ? row * stride + 1 : kOffRange);
 #pragma unroll
