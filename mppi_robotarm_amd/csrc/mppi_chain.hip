@@ -26,6 +26,7 @@
 
 #include <string>
 
+#define MPPI_CHAIN_TU
 #include "mppi_device.h"
 #include "mppi_host.h"
 #include "mppi_rocm.h"
@@ -45,9 +46,15 @@ constexpr int kCMaxVals = kMaxT * kCMax;    // T N values per row, at most
 #ifndef MPPI_CHAIN_CPU
 #define MPPI_CHAIN_CPU 2
 #endif
-#ifndef MPPI_CHAIN_LIST   // A/B variant, not the product: list rows (mppi_device.h) with the poll hand-off
+#ifndef MPPI_CHAIN_LIST   // list-only rows with the poll hand-off (mppi_device.h "list rows"); 0: every row gathers
 #define MPPI_CHAIN_LIST 0
 #endif
+#ifndef MPPI_CHAIN_PRED_NATS
+#define MPPI_CHAIN_PRED_NATS 60.0
+#endif
+// a row is predicted weightless when its rho_b lies this many lambdas above the predicted minimum: the merge
+// floor 2^-64 (44.4) and 15.6 more
+constexpr double kPredNats = MPPI_CHAIN_PRED_NATS;
 constexpr int kCPF = MPPI_CHAIN_CPF;        // noise steps in flight per lane (N rows each)
 #ifndef MPPI_Q4_PF
 #define MPPI_Q4_PF 4   // 2 and 4 measured: equal at K = 16384, 4 -2.1 % at K = 32768 (profiles/r13/chain_quad_ring_depth_ab.txt)
@@ -925,7 +932,7 @@ __global__ __launch_bounds__(kCT) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
     __shared__ int s_k[kCT];
     __shared__ double s_e[kCT];
     __shared__ unsigned s_flag, s_parity;
-    __shared__ double s_run;
+    __shared__ double s_run, s_pred;
     __shared__ CScratch sm;
 
     static_assert(LPS == 1 || (LPS == 4 && !F64), "lanes per sample: 1, or 4 for the fp32 rollout");
@@ -945,7 +952,9 @@ __global__ __launch_bounds__(kCT) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
     STAMP(8, (unsigned long long)__builtin_amdgcn_s_getreg(0xF804));   // HW_ID
     STAMP(9, (unsigned long long)__builtin_amdgcn_s_getreg(0xF814));   // XCC_ID
 #endif
-    const unsigned tag_v = POLL ? __hip_atomic_load(epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) + 1u : 0u;
+    // poll tags stay below kListTagBit (list-only rows set it, mppi_device.h) and never 0 (fresh memory)
+    unsigned tag_v = POLL ? (__hip_atomic_load(epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) + 1u) & ~kListTagBit : 0u;
+    if (POLL && tag_v == 0u) tag_v = 1u;
     double u_cur[kMedRun];
     chain_nominal_prefetch<N>(st, T, flags & MPPI_FLAG_FUSED_UPDATE, u_cur);
     double S = 0.0;
@@ -1051,8 +1060,10 @@ __global__ __launch_bounds__(kCT) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
     // finishing spread out) the atomic's fresher return skips more gathers (measured: +1.7 % with the early
     // read at config 5, -1.7 % at its shard)
     constexpr bool kEarlyRun = LPS == 4;
-    unsigned long long run0 = ~0ull;
+    constexpr bool kList = POLL && MPPI_CHAIN_LIST;
+    unsigned long long run0 = ~0ull, prev0 = ~0ull;
     if (kEarlyRun && tid == 0) run0 = __hip_atomic_load(runmin, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (kList && tid == 0) prev0 = __hip_atomic_load(runmin + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     const double rho_b = block_min_f64<kCT>(owner ? S : INFINITY, sm);
     // fp64, like the reference's weights; a wave whose samples all lie below the
     // floor (exp(-44.4) = 2^-64: the usual case, S spread >> lambda) skips the exp
@@ -1075,12 +1086,15 @@ __global__ __launch_bounds__(kCT) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
     // algorithmic bytes at config 5).
     if (tid == 0) {
         const unsigned long long key = ord_key(rho_b);
+        unsigned long long run;
         if constexpr (kEarlyRun) {
-            s_run = ord_val(min(run0, key));
+            run = min(run0, key);
         } else {
             const unsigned long long old = __hip_atomic_fetch_min(runmin, key, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            s_run = ord_val(old < key ? old : key);
+            run = old < key ? old : key;
         }
+        s_run = ord_val(run);
+        s_pred = ord_val(min(run, prev0));
     }
     __syncthreads();
     const bool skip = exp((s_run - rho_b) * c.inv_lambda) < kMergeFloor;   // uniform
@@ -1115,17 +1129,21 @@ __global__ __launch_bounds__(kCT) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
         else st_wt(slab_r, idx, v);
     };
     // rho_b and eta_b leave first (see rollout_kernel in mppi_rocm.hip)
+    nl = __builtin_amdgcn_readfirstlane(nl);
+    // List-only rows (poll hand-off, list rows in mppi_device.h): a row with few weighted samples whose rho_b lies
+    // kPredNats beyond the predicted minimum — the running minimum so far or the last launch's merged rho, the
+    // better of the two — publishes its samples instead of gathering its columns.  The prediction only steers
+    // traffic: a list-only row that does carry weight (the minimum jumped up) is gathered by the merger.
+    const bool lonly = kList && !skip && nl <= kListMax && 2 * nl + 1 <= nval &&
+                       (rho_b - s_pred) * c.inv_lambda > kPredNats;   // uniform (NaN: no prediction)
     if (tid == 0) {
-        publish(blockIdx.x * stride, skip ? INFINITY : rho_b);
+        if constexpr (POLL) st_gran(slab_r, blockIdx.x * stride, skip ? INFINITY : rho_b, lonly ? tag | kListTagBit : tag);
+        else publish(blockIdx.x * stride, skip ? INFINITY : rho_b);
         publish(blockIdx.x * stride + 1, eta_b);
     }
-    nl = __builtin_amdgcn_readfirstlane(nl);
-    // MPPI_CHAIN_LIST (A/B variant): a row with few weighted samples publishes them, not its columns (list rows,
-    // mppi_device.h); the merges that need them gather from the noise
-    constexpr bool kList = POLL && MPPI_CHAIN_LIST;
     if (skip) {
         // no merge reads this row past rho
-    } else if (kList && nl <= kListMax && 2 * nl + 1 <= nval) {
+    } else if (lonly) {
         if (tid == 0) publish(blockIdx.x * stride + 2, list_mode_word(nl));
         if (tid < nl) {
             publish(blockIdx.x * stride + 3 + 2 * tid, (double)s_k[tid]);
@@ -1198,6 +1216,7 @@ __global__ __launch_bounds__(kCT) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
         if (threadIdx.x == 0) {
             __hip_atomic_store(epoch, tag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             __hip_atomic_store(runmin, ~0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);   // every row is in
+            if (kList) __hip_atomic_store(runmin + 1, ord_key(sm.rho_fin), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         }
     } else {
         if (!arrive_last(counters + g, (unsigned)gsz, &s_flag, c.acquire != 0)) return;

@@ -440,11 +440,18 @@ constexpr unsigned kSpinMax = 1u << 20;
 __device__ __forceinline__ void report_timeout(unsigned* tmo) {
     if (tmo) __hip_atomic_store(tmo, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
 }
+#if defined(MPPI_LIST_DEBUG) && defined(MPPI_CHAIN_TU)   // diagnostic builds: which poll gave up
+#define MPPI_GIVE_UP_TRACE(lane) \
+    if ((lane) == 0) printf("poll gave up: block %d thread %d line %d\n", (int)blockIdx.x, (int)threadIdx.x, __LINE__)
+#else
+#define MPPI_GIVE_UP_TRACE(lane) (void)0
+#endif
 #define MPPI_SPIN_OR_GIVE_UP(spins, tmo, lane) MPPI_SPIN_OR_GIVE_UP_L(spins, 0ull, tmo, lane, (void)0)
 // with a deadline of its own (s_memrealtime ticks, 100 MHz; 0: the spin bound alone) and a statement run
 // when it gives up (the exchange's polls)
 #define MPPI_SPIN_OR_GIVE_UP_L(spins, deadline, tmo, lane, on_give_up)                                   \
     if (spins >= kSpinMax || ((deadline) && __builtin_amdgcn_s_memrealtime() > (deadline))) {            \
+        MPPI_GIVE_UP_TRACE(lane);                                                                        \
         if ((lane) == 0) report_timeout(tmo);                                                            \
         on_give_up;                                                                                      \
         break;                                                                                           \
@@ -471,6 +478,7 @@ struct MergeScratch {
     double rho[kDirectRows];  // direct merge: the rows' rho, polled by wave 0
     double part[2 * kDirectRows];  // direct merge: per row-group column sums (one group per ncol threads)
     double eta;                    // the final merge's eta = sum_k e^{-(S_k - rho)/lambda} (>= 1; 1: one-hot)
+    double rho_fin;                // the final merge's rho
     int nrel;
 };
 
@@ -508,6 +516,7 @@ __device__ __forceinline__ void put_final(double rho, const double (&acc)[MAXCH]
         if (col == 0) {
             sm.nrel = nrel;
             sm.eta = eta;
+            sm.rho_fin = rho;
             if (out_row) {
                 out_row[0] = rho;
                 out_row[1] = acc[ch];
@@ -529,9 +538,7 @@ __device__ __forceinline__ void put_final(double rho, const double (&acc)[MAXCH]
 // merger that needs the row's columns gathers them from the noise itself with the row gather's operations in its
 // order (gather_col_n: fp64 fma over l from 0), so a list row merges to the same bits as the column row it
 // replaces, and only the rows that carry weight in some merge are ever gathered: a row's own gather cannot know
-// that, and read a cache line per value for every row (the chain's [T][n][K] noise).  An A/B variant
-// (MPPI_CHAIN_LIST, TRIED.md): the shard's traffic 1.14x -> 1.04x, but +2.7 % time, the merger's header poll
-// and noise gather being on the critical path where the rows' own gathers ran beside the merge.
+// that, and read a cache line per value for every row (the chain's [T][n][K] noise).
 #ifndef MPPI_LIST_MAX
 #define MPPI_LIST_MAX 2
 #endif
@@ -541,6 +548,18 @@ struct ListSrc {
     const float* noise = nullptr;   // the row's column j (t n + d) of sample k at noise[j K + k]
     int K = 0;
 };
+// A list-only row (its columns not published) says so in its rho granule: both tag words carry kListTagBit
+// (tags stay below it), so the merger knows from the rho poll which weighted rows it must gather itself, and a
+// row that gathered costs the merge nothing more than before.
+constexpr unsigned kListTagBit = 0x80000000u;
+__device__ __forceinline__ bool gran_ok_lst(u32x4 x, unsigned tag) {
+    return (x[1] & ~kListTagBit) == tag && x[3] == x[1];
+}
+__device__ __forceinline__ bool gran_lst(u32x4 x) { return (x[1] & kListTagBit) != 0u; }
+__device__ __forceinline__ int* list_flags_lds() {   // the direct merge's per-row list-only flags
+    __shared__ int f[kDirectRows];
+    return f;
+}
 __device__ __forceinline__ double list_mode_word(int nl) {
     return __longlong_as_double((long long)(((unsigned long long)kListHi << 32) | (unsigned)nl));
 }
@@ -652,15 +671,17 @@ __device__ __forceinline__ void merge_rows_block(__amdgpu_buffer_rsrc_t rows, in
         const int rb = row0 + r0;
         const int lrow = lane < nr ? (rb + lane) * stride : kOffRange;
         double rho_r, eta_l = 0.0, v[EAGER ? LB : 1];
+        bool lst_r = false;   // LIST: this lane's row is list-only
         if constexpr (GRAN) {
             u32x4 gr;
             for (unsigned spins = 0;; ++spins) {
                 asm volatile("" ::: "memory");
                 gr = ld_gran(rows, lrow);
-                if (__all(lane >= nr || gran_ok(gr, tag))) break;
+                if (__all(lane >= nr || (LIST ? gran_ok_lst(gr, tag) : gran_ok(gr, tag)))) break;
                 MPPI_SPIN_OR_GIVE_UP_L(spins, deadline, tmo, lane, gave_up = true);
             }
             rho_r = gran_val(gr);
+            lst_r = LIST && lane < nr && gran_lst(gr);
         } else if constexpr (!EAGER) {
             rho_r = ld_wt(rows, lrow);
         } else {
@@ -704,14 +725,18 @@ __device__ __forceinline__ void merge_rows_block(__amdgpu_buffer_rsrc_t rows, in
         } else {
             // lane k < nrr: the round's k-th weighted row (ascending)
             const int krow = lane < nrr ? select_bit(rel, lane) : 0;
-            // LIST: every weighted row's header first (eta with it)
+            // LIST: the list-only weighted rows' headers (eta with them) before their entries
             int nl_l = 0, k_l[kListMax];
             double w_l[kListMax];
-            if constexpr (LIST)
-                gave_up |= poll_list_header(rows, lane < nrr ? (rb + krow) * stride : kOffRange, tag, eta_l, nl_l, k_l,
-                                            w_l, tmo, deadline);
+            if constexpr (LIST) {
+                const bool need = lane < nrr && __shfl(lst_r ? 1 : 0, krow) != 0;
+                if (__any(need))
+                    gave_up |= poll_list_header(rows, need ? (rb + krow) * stride : kOffRange, tag, eta_l, nl_l, k_l,
+                                                w_l, tmo, deadline);
+                if (!need) nl_l = 0;
+            }
             for (int b0 = 0; b0 < nrr; b0 += RB) {
-                const bool eta_on = !LIST && b0 == 0 && lane < nrr;
+                const bool eta_on = b0 == 0 && lane < nrr && nl_l == 0;
                 const int eidx = eta_on ? (rb + krow) * stride + 1 : kOffRange;
                 double x[LB];
                 if constexpr (GRAN) {
@@ -732,7 +757,7 @@ __device__ __forceinline__ void merge_rows_block(__amdgpu_buffer_rsrc_t rows, in
                         if (__all(ok)) break;
                         MPPI_SPIN_OR_GIVE_UP_L(spins, deadline, tmo, lane, gave_up = true);
                     }
-                    if (!LIST && b0 == 0) eta_l = gran_val(ge);
+                    if (eta_on) eta_l = gran_val(ge);
 #pragma unroll
                     for (int j = 0; j < LB; ++j) x[j] = gran_val(gv[j]);
                     if constexpr (LIST) list_entries<NT, MAXCH, LB>(x, b0, nrr, nl_l, k_l, w_l, eta_l, ncol, ls);
@@ -808,13 +833,16 @@ __device__ __forceinline__ bool direct_merge(__amdgpu_buffer_rsrc_t rows, int n,
                 for (int j = 0; j < P; ++j) {
                     const int r = lane + 64 * j;
                     gr[j] = ld_gran(rows, r < n ? r * stride : kOffRange);
-                    ok = ok && (r >= n || gran_ok(gr[j], tag));
+                    ok = ok && (r >= n || (LIST ? gran_ok_lst(gr[j], tag) : gran_ok(gr[j], tag)));
                 }
                 if (__all(ok)) break;
                 MPPI_SPIN_OR_GIVE_UP(spins, tmo, lane);
             }
 #pragma unroll
-            for (int j = 0; j < P; ++j) sm.rho[lane + 64 * j] = lane + 64 * j < n ? gran_val(gr[j]) : INFINITY;
+            for (int j = 0; j < P; ++j) {
+                sm.rho[lane + 64 * j] = lane + 64 * j < n ? gran_val(gr[j]) : INFINITY;
+                if constexpr (LIST) list_flags_lds()[lane + 64 * j] = gran_lst(gr[j]) ? 1 : 0;
+            }
         }
         __syncthreads();
 #pragma unroll
@@ -880,12 +908,16 @@ __device__ __forceinline__ bool direct_merge(__amdgpu_buffer_rsrc_t rows, int n,
         // LIST: every weighted row's header first (eta with it)
         int nl_l = 0, k_l[kListMax];
         double w_l[kListMax];
-        if constexpr (LIST)
-            (void)poll_list_header(rows, mine ? row * stride : kOffRange, tag, eta_k, nl_l, k_l, w_l, tmo, 0ull);
+        if constexpr (LIST) {
+            const bool need = mine && list_flags_lds()[row] != 0;
+            if (__any(need))
+                (void)poll_list_header(rows, need ? row * stride : kOffRange, tag, eta_k, nl_l, k_l, w_l, tmo, 0ull);
+            if (!need) nl_l = 0;
+        }
         for (int b0 = 0; b0 < nrel; b0 += RB) {
             double v[LB];
             if constexpr (GRAN) {
-                const bool eta_on = !LIST && b0 == 0 && mine;
+                const bool eta_on = b0 == 0 && mine && nl_l == 0;
                 u32x4 ge, gv[LB];
                 for (unsigned spins = 0;; ++spins) {
                     asm volatile("" ::: "memory");
@@ -902,7 +934,7 @@ __device__ __forceinline__ bool direct_merge(__amdgpu_buffer_rsrc_t rows, int n,
                     if (__all(ok)) break;
                     MPPI_SPIN_OR_GIVE_UP(spins, tmo, lane);
                 }
-                if (!LIST && b0 == 0) eta_k = gran_val(ge);
+                if (eta_on) eta_k = gran_val(ge);
 #pragma unroll
                 for (int j = 0; j < LB; ++j) v[j] = gran_val(gv[j]);
                 if constexpr (LIST) list_entries<NT, MAXCH, LB>(v, b0, nrel, nl_l, k_l, w_l, eta_k, ncol, ls);
