@@ -46,7 +46,7 @@ constexpr int kCMaxVals = kMaxT * kCMax;    // T N values per row, at most
 #ifndef MPPI_CHAIN_CPU
 #define MPPI_CHAIN_CPU 2
 #endif
-#ifndef MPPI_CHAIN_LIST   // list-only rows with the poll hand-off (mppi_device.h "list rows"); 0: every row gathers
+#ifndef MPPI_CHAIN_LIST   // A/B variant: list-only rows with the poll hand-off (mppi_device.h "list rows", TRIED.md)
 #define MPPI_CHAIN_LIST 0
 #endif
 #ifndef MPPI_CHAIN_PRED_NATS
@@ -1061,9 +1061,12 @@ __global__ __launch_bounds__(kCT) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
     // read at config 5, -1.7 % at its shard)
     constexpr bool kEarlyRun = LPS == 4;
     constexpr bool kList = POLL && MPPI_CHAIN_LIST;
-    unsigned long long run0 = ~0ull, prev0 = ~0ull;
+    unsigned long long run0 = ~0ull, prev0 = ~0ull, prev1 = ~0ull;   // prev: the last two launches' merged rho
     if (kEarlyRun && tid == 0) run0 = __hip_atomic_load(runmin, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    if (kList && tid == 0) prev0 = __hip_atomic_load(runmin + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (kList && tid == 0) {
+        prev0 = __hip_atomic_load(runmin + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        prev1 = __hip_atomic_load(runmin + 2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
     const double rho_b = block_min_f64<kCT>(owner ? S : INFINITY, sm);
     // fp64, like the reference's weights; a wave whose samples all lie below the
     // floor (exp(-44.4) = 2^-64: the usual case, S spread >> lambda) skips the exp
@@ -1094,7 +1097,10 @@ __global__ __launch_bounds__(kCT) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
             run = old < key ? old : key;
         }
         s_run = ord_val(run);
-        s_pred = ord_val(min(run, prev0));
+        // the last merged rho extrapolated by its last change (a drifting loop), when both are known
+        const double p0 = ord_val(prev0), p1 = ord_val(prev1);
+        const double pp = prev0 == ~0ull ? NAN : prev1 == ~0ull ? p0 : p0 + (p0 - p1);
+        s_pred = min_raw_f64(ord_val(run), pp);
     }
     __syncthreads();
     const bool skip = exp((s_run - rho_b) * c.inv_lambda) < kMergeFloor;   // uniform
@@ -1216,7 +1222,10 @@ __global__ __launch_bounds__(kCT) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
         if (threadIdx.x == 0) {
             __hip_atomic_store(epoch, tag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             __hip_atomic_store(runmin, ~0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);   // every row is in
-            if (kList) __hip_atomic_store(runmin + 1, ord_key(sm.rho_fin), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            if (kList) {
+                __hip_atomic_store(runmin + 2, prev0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                __hip_atomic_store(runmin + 1, ord_key(sm.rho_fin), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            }
         }
     } else {
         if (!arrive_last(counters + g, (unsigned)gsz, &s_flag, c.acquire != 0)) return;

@@ -538,7 +538,9 @@ __device__ __forceinline__ void put_final(double rho, const double (&acc)[MAXCH]
 // merger that needs the row's columns gathers them from the noise itself with the row gather's operations in its
 // order (gather_col_n: fp64 fma over l from 0), so a list row merges to the same bits as the column row it
 // replaces, and only the rows that carry weight in some merge are ever gathered: a row's own gather cannot know
-// that, and read a cache line per value for every row (the chain's [T][n][K] noise).
+// that, and read a cache line per value for every row (the chain's [T][n][K] noise).  Not the product: an A/B
+// variant (MPPI_CHAIN_LIST in mppi_chain.hip; TRIED.md) that cut the c5 shard's traffic 1.14x -> 1.04x at +1.9 %
+// time.
 #ifndef MPPI_LIST_MAX
 #define MPPI_LIST_MAX 2
 #endif
@@ -729,12 +731,15 @@ __device__ __forceinline__ void merge_rows_block(__amdgpu_buffer_rsrc_t rows, in
             int nl_l = 0, k_l[kListMax];
             double w_l[kListMax];
             if constexpr (LIST) {
-                const bool need = lane < nrr && __shfl(lst_r ? 1 : 0, krow) != 0;
+                // the shuffle runs in every lane: a cross-lane read returns nothing from a lane the EXEC mask has off
+                const int lst_k = __shfl(lst_r ? 1 : 0, krow);
+                const bool need = lane < nrr && lst_k != 0;
                 if (__any(need))
                     gave_up |= poll_list_header(rows, need ? (rb + krow) * stride : kOffRange, tag, eta_l, nl_l, k_l,
                                                 w_l, tmo, deadline);
                 if (!need) nl_l = 0;
             }
+            const unsigned long long lmask = LIST ? __ballot(nl_l != 0) : 0ull;   // the list rows among them
             for (int b0 = 0; b0 < nrr; b0 += RB) {
                 const bool eta_on = b0 == 0 && lane < nrr && nl_l == 0;
                 const int eidx = eta_on ? (rb + krow) * stride + 1 : kOffRange;
@@ -748,8 +753,7 @@ __device__ __forceinline__ void merge_rows_block(__amdgpu_buffer_rsrc_t rows, in
 #pragma unroll
                         for (int j = 0; j < LB; ++j) {
                             const int i = b0 + j / MAXCH, col = tid + (j % MAXCH) * NT;
-                            const bool on = i < nrr && col < ncol &&
-                                            (!LIST || __builtin_amdgcn_readlane(nl_l, min(i, 63)) == 0);
+                            const bool on = i < nrr && col < ncol && !((lmask >> min(i, 63)) & 1ull);
                             gv[j] = ld_gran(rows, on ? (rb + __builtin_amdgcn_readlane(krow, i)) * stride + 1 + col
                                                      : kOffRange);
                             ok = ok && (!on || gran_ok(gv[j], tag));
@@ -760,7 +764,7 @@ __device__ __forceinline__ void merge_rows_block(__amdgpu_buffer_rsrc_t rows, in
                     if (eta_on) eta_l = gran_val(ge);
 #pragma unroll
                     for (int j = 0; j < LB; ++j) x[j] = gran_val(gv[j]);
-                    if constexpr (LIST) list_entries<NT, MAXCH, LB>(x, b0, nrr, nl_l, k_l, w_l, eta_l, ncol, ls);
+                    if (LIST && lmask) list_entries<NT, MAXCH, LB>(x, b0, nrr, nl_l, k_l, w_l, eta_l, ncol, ls);
                 } else {
                     if (b0 == 0) eta_l = ld_wt(rows, eidx);
 #pragma unroll
@@ -914,6 +918,7 @@ __device__ __forceinline__ bool direct_merge(__amdgpu_buffer_rsrc_t rows, int n,
                 (void)poll_list_header(rows, need ? row * stride : kOffRange, tag, eta_k, nl_l, k_l, w_l, tmo, 0ull);
             if (!need) nl_l = 0;
         }
+        const unsigned long long lmask = LIST ? __ballot(nl_l != 0) : 0ull;   // the list rows among them
         for (int b0 = 0; b0 < nrel; b0 += RB) {
             double v[LB];
             if constexpr (GRAN) {
@@ -926,8 +931,7 @@ __device__ __forceinline__ bool direct_merge(__amdgpu_buffer_rsrc_t rows, int n,
 #pragma unroll
                     for (int j = 0; j < LB; ++j) {
                         const int i = b0 + j / MAXCH, col = tid + (j % MAXCH) * NT;
-                        const bool on = i < nrel && col < ncol &&
-                                        (!LIST || __builtin_amdgcn_readlane(nl_l, min(i, 63)) == 0);
+                        const bool on = i < nrel && col < ncol && !((lmask >> min(i, 63)) & 1ull);
                         gv[j] = ld_gran(rows, on ? __builtin_amdgcn_readlane(row, i) * stride + 1 + col : kOffRange);
                         ok = ok && (!on || gran_ok(gv[j], tag));
                     }
@@ -937,7 +941,7 @@ __device__ __forceinline__ bool direct_merge(__amdgpu_buffer_rsrc_t rows, int n,
                 if (eta_on) eta_k = gran_val(ge);
 #pragma unroll
                 for (int j = 0; j < LB; ++j) v[j] = gran_val(gv[j]);
-                if constexpr (LIST) list_entries<NT, MAXCH, LB>(v, b0, nrel, nl_l, k_l, w_l, eta_k, ncol, ls);
+                if (LIST && lmask) list_entries<NT, MAXCH, LB>(v, b0, nrel, nl_l, k_l, w_l, eta_k, ncol, ls);
             } else {
                 if (b0 == 0) eta_k = ld_wt(rows, mine ? row * stride + 1 : kOffRange);
 #pragma unroll
