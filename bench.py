@@ -277,7 +277,7 @@ def sampled_latency(K, T, device, calls=20, warm=5):
 def numpy_noise_latency(K, T, device, calls=20, warm=5):
     """calc_control_input back to back (ms, median) with the drop-in's default noise="numpy": the reference's
     own draw, np.random.multivariate_normal on the legacy global RNG (control.py:154-164), NumPy's values and
-    state (the standard normals threaded in C, hostrng; the transform on the device for run.py's Sigma)."""
+    state, drawn on the device (mppi_np_*, engine.NpDeviceStream; the host draw, hostrng, for other Sigmas)."""
     from mppi_robotarm_amd.controller import MPPIControllerForPathTracking
     from mppi_robotarm_amd.params import runpy_config
     path = np.load(os.path.join(ROOT, "tests", "golden", "paths.npz"))["xydq_circle"][:, :4]
@@ -295,13 +295,15 @@ def numpy_noise_latency(K, T, device, calls=20, warm=5):
     return float(np.median(ts[warm:])) * 1e3
 
 
-def chain_dropin_latency(K, T, device, precision="f32", calls=40, warm=10):
+def chain_dropin_latency(K, T, device, precision="f32", calls=40, warm=10, noise="device"):
     """The chain drop-in's calc_control_input back to back (ms, median) from the config-5 start state, the
-    start nominal re-staged before each call (the bench loop's reset: no plant between calls)."""
+    start nominal re-staged before each call (the bench loop's reset: no plant between calls).  noise="numpy":
+    the drop-in's default, the reference's own np.random.multivariate_normal stream (drawn on the device)."""
     from mppi_robotarm_amd.chain import CHAIN7_X0, ChainMPPIController, gravity_torque
     path = np.load(os.path.join(ROOT, "tests", "golden", "paths.npz"))["xydq_circle"][:, :4]
-    c = ChainMPPIController(0.006, path, T, K, u_init=gravity_torque(CHAIN7_X0[:7]), device=device, noise="device",
+    c = ChainMPPIController(0.006, path, T, K, u_init=gravity_torque(CHAIN7_X0[:7]), device=device, noise=noise,
                             precision=precision)
+    np.random.seed(0)
     u0 = c.u_prev.copy()
     ts = []
     for i in range(warm + calls):
@@ -606,17 +608,22 @@ def main():
                 "visualze_sampled_trajs=True, i.e. also the (K, T, 4) fp64 sampled_traj_list (134 MB at K = "
                 "65536) re-rolled on the device and read back every call; numpy_noise: back to back with the "
                 "drop-in's default noise='numpy', the reference's own np.random.multivariate_normal stream "
-                "(NumPy's values and RNG state) drawn on the host every call. "
+                "(NumPy's values and RNG state) drawn on the device every call (mppi_np_*). "
                 "ms_per_step is the device-resident loop")
         if world == 1 and c5:
             out["control_step_latency_back_to_back_ms"] = chain_dropin_latency(K, T, local_rank, args.precision)
+            progress("NumPy-noise leg")
+            out["control_step_latency_numpy_noise_ms"] = chain_dropin_latency(K, T, local_rank, args.precision,
+                                                                              calls=10, warm=3, noise="numpy")
             out["control_step_latency_def"] = (
                 "median wall time of ChainMPPIController.calc_control_input (noise='device') at this K, T, back "
                 "to back from the config-5 start state (no plant model exists for the build-defined chain, so no "
                 "closed loop): one fused launch (rollouts, soft-min, weighted noise, median filter, update, shift), "
                 "one read-back, fp64 optimal trajectory on the host, the next step's Philox draw queued behind "
                 "the launch (each call then also waits for the previous draw). 40 calls after 10 uncounted. "
-                "ms_per_step is the device-resident loop")
+                "numpy_noise: the same with the drop-in's default noise='numpy', the reference's own "
+                "np.random.multivariate_normal stream (NumPy's values and RNG state) drawn on the device every "
+                "call (10 calls after 3). ms_per_step is the device-resident loop")
         if world == 1 and args.cpu_seconds > 0:
             progress("CPU baseline")
             out["cpu_baseline"] = (cpu_baseline_c5(args, window, x0, u, K, T) if c5
