@@ -334,22 +334,18 @@ __global__ __launch_bounds__(kScanT) void np_scan_kernel(const int* __restrict__
     }
 }
 
-// z[m] (standard normal m of the draw) through the transform into the engine's layout, if sample k is this rank's
-__device__ __forceinline__ void emit(const NpShape& sh, unsigned m, double z) {
-    const unsigned k = m / sh.per_k, r = m - k * sh.per_k;
-    const unsigned t = r / sh.du, dd = r - t * sh.du;
-    if (k - sh.k_offset >= sh.K_local) return;   // unsigned: also k < k_offset
-    const long long at = (long long)t * sh.st + (long long)(k - sh.k_offset) * sh.sk;
-    for (unsigned d = 0; d < sh.du; ++d)
-        if ((unsigned)sh.src[d] == dd) sh.out[at + (long long)d * sh.sd] = (float)(z * sh.scale[d] + sh.mean[d]);
-}
-
+// The accepted attempts again: each pair's place from the prefix, f with glibc's log reproduced (np_glibc_log.h),
+// IEEE division and square root.  The workgroup's normals m in [m0, m1) (NumPy's (K, T, du) order) are staged in
+// LDS, then written through the transform in the engine's layout row by row: for each step t, the workgroup's
+// samples are contiguous there, so consecutive threads write consecutive addresses (written straight from the
+// attempts, every lane of a wave hit its own row: one cache line per 8 bytes).
 __global__ __launch_bounds__(kNT) void np_write_kernel(const uint32_t* __restrict__ words, long long base, long long A,
                                                        const long long* __restrict__ offsets,
                                                        const double* __restrict__ logd, NpShape sh, long long pairs,
                                                        long long n, int o, double cached, NpResult* res) {
     __shared__ double s_log[NPLOG_NDATA];
     __shared__ int s_cnt[kAttRounds][kNT / 64];
+    __shared__ double s_z[2 * kAttPerWG];
     for (int i = threadIdx.x; i < NPLOG_NDATA; i += kNT) s_log[i] = logd[i];
     if (res->status) return;   // uniform: every thread returns
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
@@ -369,8 +365,8 @@ __global__ __launch_bounds__(kNT) void np_write_kernel(const uint32_t* __restric
     __syncthreads();   // also publishes s_log
     // pair index of this thread's attempt in round r: the workgroup's offset, all accepted attempts of the
     // rounds before r, those of round r in earlier waves, and those of earlier lanes of this wave
-    long long q0 = offsets[blockIdx.x];
-    if (blockIdx.x == 0 && threadIdx.x == 0 && o) emit(sh, 0u, cached);   // the cached Gaussian comes first
+    const long long qw = offsets[blockIdx.x];
+    long long q0 = qw;
     const unsigned long long lt = (1ull << lane) - 1ull;
 #pragma unroll
     for (int r = 0; r < kAttRounds; ++r) {
@@ -387,15 +383,44 @@ __global__ __launch_bounds__(kNT) void np_write_kernel(const uint32_t* __restric
         if (acc && q < pairs) {
             const double f = sqrt(-2.0 * np_glibc_log(s_log, r2[r]) / r2[r]);
             const double g1 = f * x1[r], g2 = f * x2[r];   // legacy_gauss returns f x2 and caches f x1
-            const unsigned m = (unsigned)(o + 2 * q);
-            emit(sh, m, g2);
-            if ((long long)m + 1 < n) emit(sh, m + 1, g1);
+            const int lq = (int)(q - qw);
+            s_z[2 * lq] = g2;       // normal o + 2 q
+            s_z[2 * lq + 1] = g1;   // o + 2 q + 1
             if (q == pairs - 1) {
                 res->last_attempt = a0 + (long long)r * kNT;
                 res->last_fx1 = g1;
             }
         }
         q0 += round;
+    }
+    __syncthreads();
+    // normals [m0, m1) of this workgroup: pairs [qw, q0) below `pairs`; the cached Gaussian (m = 0) comes first
+    const long long zb = o + 2 * qw;   // normal of s_z[0]
+    const long long m0 = blockIdx.x == 0 ? 0 : zb;
+    const long long m1 = min(o + 2 * min(q0, pairs), n);
+    if (m1 <= m0) return;
+    const long long k_lo = m0 / sh.per_k, k_hi = (m1 - 1) / sh.per_k;
+    const long long s_lo = max(k_lo, (long long)sh.k_offset), s_hi = min(k_hi, (long long)sh.k_offset + sh.K_local - 1);
+    if (s_hi < s_lo) return;
+    const unsigned nk = (unsigned)(s_hi - s_lo + 1), du = sh.du;
+    const bool k_inner = sh.sk == 1;   // [T][n][K] (the chain): samples innermost; else (t, k, d) order
+    const unsigned per_t = nk * du, total = per_t * (sh.per_k / du);
+    for (unsigned e = threadIdx.x; e < total; e += kNT) {
+        const unsigned t = e / per_t, rem = e - t * per_t;
+        unsigned kk, d;
+        if (k_inner) {
+            d = rem / nk;
+            kk = rem - d * nk;
+        } else {
+            kk = rem / du;
+            d = rem - kk * du;
+        }
+        const long long k = s_lo + kk;
+        const long long m = k * sh.per_k + (long long)t * du + sh.src[d];
+        if (m < m0 || m >= m1) continue;
+        const double z = m < zb ? cached : s_z[m - zb];
+        sh.out[(long long)t * sh.st + (k - sh.k_offset) * sh.sk + (long long)d * sh.sd] =
+            (float)(z * sh.scale[d] + sh.mean[d]);
     }
 }
 

@@ -6,7 +6,7 @@ cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 export TMPDIR=/tmp
 O=gpurun_out/${1:-npdraw}; mkdir -p $O
 timeout -k 10 300 python -u -m pytest tests/test_gpu_npdraw.py -x -v --timeout 120 --timeout-method thread > $O/tests.log 2>&1
-rc=$?; echo "tests rc=$rc"; tail -3 $O/tests.log; [ $rc -le 1 ] || exit $rc
+rc=$?; echo "tests rc=$rc"; tail -3 $O/tests.log; [ $rc -eq 0 ] || exit $rc
 timeout -k 10 300 python tools/npdraw_bench.py > $O/bench.txt 2>&1
 rc=$?; echo "bench rc=$rc"; cat $O/bench.txt; [ $rc -eq 0 ] || exit $rc
 for P in ${STRIDES:-128 256 512}; do
