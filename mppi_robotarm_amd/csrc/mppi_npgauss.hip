@@ -7,11 +7,12 @@
 // -> the Sigma transform.  Sequential in NumPy; here every phase is parallel:
 //
 //   np_seq_kernel    the first 34 key arrays (blocks) after the state's: the word windows the jumps read.
-//   np_jump_kernel   the state of every generator stream's start: MT19937 is linear over GF(2), so the block
+//   np_jumpn_kernel  the state of every generator stream's start: MT19937 is linear over GF(2), so the block
 //                    J words on is sum_d phi_d F^d(key) with phi = x^J mod P (P: the characteristic
 //                    polynomial, found and powered on the host, np_legacy_gauss.c) and F^d(key) the window
-//                    [d, d + 624) of the word sequence: each output word is the XOR of ~10k sequence words at
-//                    phi's set bits (Haramoto et al. 2008, the window form).  The sequence sits in LDS.
+//                    [d, d + 624) of the word sequence (Haramoto et al. 2008, the window form): a table product
+//                    over 4-bit chunks of phi, the 16 entries of a chunk in each lane's registers (np_jump_kernel,
+//                    the XOR of the sequence words at phi's ~10k set bits from LDS, stays for A/B).
 //   np_gen_kernel    one workgroup per stream twists its range of blocks; a block's 624 words are each a
 //                    function of the previous block alone (the twist's in-block dependencies unrolled: up to
 //                    three tempering-free mix terms per word), so one barrier per block.
@@ -35,6 +36,7 @@
 #include <string.h>
 
 #include <string>
+#include <algorithm>
 #include <vector>
 
 #include "mppi_host.h"
@@ -62,6 +64,17 @@ constexpr int kJBatch = 32;                           // set bits of a jump poly
 constexpr int kSeqPad = kSeqBlocks * kN;              // list padding: s_seq[kSeqPad + j] = 0 for j < 640
 constexpr int kJListStride = ((kDeg + 1 + kJSplit * kJBatch - 1) / (kJSplit * kJBatch)) * kJSplit * kJBatch;
 constexpr int kJPart = kJListStride / kJSplit;        // list entries per workgroup (a multiple of kJBatch)
+#ifndef MPPI_NP_JUMP_WGS
+#define MPPI_NP_JUMP_WGS 512
+#endif
+#ifndef MPPI_NP_JUMP_TABLE
+#define MPPI_NP_JUMP_TABLE 1   // 0: the set-bit list jump (np_jump_kernel), for A/B
+#endif
+constexpr int kNibS = 32;                             // table jump: streams per workgroup
+constexpr int kNibW = kNibS / 8;                      // their nibbles of one chunk: 4 words
+constexpr int kChunks = (kDeg + 3) / 4;               // 4-bit chunks of a jump polynomial
+constexpr int kJNT = 640;                             // table jump threads: output word i per lane (< 624)
+constexpr int kJTableWGs = MPPI_NP_JUMP_WGS;                       // table jump: chunk ranges x stream groups, about
 constexpr int kAttRounds = 8;                         // attempts per thread, interleaved: attempt a0 + 256 r + t
 constexpr int kAttPerWG = kNT * kAttRounds;
 constexpr size_t kJumpLds = (kSeqPad + 2 * kJHalf + kJPart) * sizeof(uint32_t);   // 107 KB
@@ -239,9 +252,59 @@ __global__ __launch_bounds__(kJT) void np_jump_kernel(const uint32_t* __restrict
     }
 }
 
+// The same jumps as a table product (the Four Russians' method over GF(2), 4-bit chunks).  Output word i of
+// jump j is the XOR over the chunks c of T_c[nib_j(c)][i], where nib_j(c) holds the polynomial's bits 4c .. 4c + 3
+// and T_c[v][i] = XOR of seq[4c + b + i] over the set bits b of v: lane i builds its 16 table entries of a chunk in
+// registers from four sequence words, and each of the workgroup's 32 jumps picks its entry by the chunk's
+// (uniform) nibble — a register-indexed move and an XOR per jump and chunk, instead of ~2 LDS reads and XORs per
+// set bit.  Workgroup (r, g): chunks [r cpw, (r + 1) cpw) for jumps [32 g, 32 g + 32); each writes its partial
+// XOR of every output word, np_gen_kernel XORs the R parts.
+__global__ __launch_bounds__(kJNT) void np_jumpn_kernel(const uint32_t* __restrict__ seq, const uint32_t* __restrict__ nibs,
+                                                        int G, int cpw, int njumps, int R, uint32_t* __restrict__ parts) {
+    extern __shared__ uint32_t s_w[];   // sequence words [4 c0, 4 c1 + 627)
+    const int r = blockIdx.x, g = blockIdx.y, i = threadIdx.x;
+    const int c0 = r * cpw, c1 = min(c0 + cpw, kChunks);
+    const int w0 = 4 * c0, nw = 4 * (c1 - c0) + kN + 3;
+    for (int q = i; q < nw; q += kJNT) s_w[q] = seq[w0 + q];
+    __syncthreads();
+    uint32_t o[kNibS];
+#pragma unroll
+    for (int j = 0; j < kNibS; ++j) o[j] = 0u;
+    const int li = min(i, kN - 1);   // lanes past word 623 repeat it (never stored)
+    for (int c = c0; c < c1; ++c) {
+        const uint32_t* wp = s_w + 4 * (c - c0) + li;
+        const uint32_t a = wp[0], b = wp[1], e = wp[2], d = wp[3];
+        uint32_t T[16];
+        T[0] = 0u;
+        T[1] = a;
+        T[2] = b;
+        T[3] = a ^ b;
+        T[4] = e;
+        T[5] = e ^ a;
+        T[6] = e ^ b;
+        T[7] = e ^ T[3];
+#pragma unroll
+        for (int v = 0; v < 8; ++v) T[8 + v] = T[v] ^ d;
+        const uint32_t* nb = nibs + ((size_t)c * G + g) * kNibW;
+#pragma unroll
+        for (int w = 0; w < kNibW; ++w) {
+            const uint32_t word = __builtin_amdgcn_readfirstlane(nb[w]);
+#pragma unroll
+            for (int q = 0; q < 8; ++q) o[8 * w + q] ^= T[(word >> (4 * q)) & 15u];
+        }
+    }
+    if (i < kN) {
+#pragma unroll
+        for (int j = 0; j < kNibS; ++j) {
+            const int jj = g * kNibS + j;
+            if (jj < njumps) parts[((size_t)jj * R + r) * kN + i] = o[j];
+        }
+    }
+}
+
 // stream s: blocks [1 + P s, min(1 + P (s + 1), nblk)); stream 0 also writes block 0 (the state's key array)
 __global__ __launch_bounds__(kTT) void np_gen_kernel(const uint32_t* __restrict__ key, const uint32_t* __restrict__ parts,
-                                                     uint32_t* __restrict__ words, int P, int nblk) {
+                                                     uint32_t* __restrict__ words, int P, int nblk, int nparts) {
     __shared__ uint32_t buf[2][kN];
     const int s = blockIdx.x, i = threadIdx.x;
     const int b0 = 1 + P * s, b1 = min(1 + P * (s + 1), nblk);
@@ -254,10 +317,17 @@ __global__ __launch_bounds__(kTT) void np_gen_kernel(const uint32_t* __restrict_
         __syncthreads();
     } else {
         if (i < kN) {
-            const uint32_t* q = parts + (size_t)(s - 1) * kJSplit * kN + i;
+            const uint32_t* q = parts + (size_t)(s - 1) * nparts * kN + i;
             uint32_t v = 0;
+            int h = 0;
+            for (; h + 8 <= nparts; h += 8) {   // eight loads in flight
+                uint32_t x[8];
 #pragma unroll
-            for (int h = 0; h < kJSplit; ++h) v ^= q[h * kN];
+                for (int u = 0; u < 8; ++u) x[u] = q[(size_t)(h + u) * kN];
+#pragma unroll
+                for (int u = 0; u < 8; ++u) v ^= x[u];
+            }
+            for (; h < nparts; ++h) v ^= q[(size_t)h * kN];
             buf[1][i] = v;
         }
         __syncthreads();
@@ -453,6 +523,9 @@ struct mppi_np_ctx {
     uint32_t* d_bits = nullptr;     // (streams - 1) jump polynomials of block stride P, as set-bit byte offsets
     int* d_nbits = nullptr;
     int poly_P = 0, poly_streams = 0;
+    uint32_t* d_nibs = nullptr;     // table jump: the polynomials' 4-bit chunks, [chunk][group][4 words]
+    int jG = 0, jR = 0, jcpw = 0;   // table jump: stream groups, chunk ranges, chunks per range
+    int jparts = kJSplit;           // partial XORs per stream that np_gen_kernel combines
     uint32_t* d_jumped = nullptr;
     uint32_t* d_words = nullptr;
     size_t words_cap = 0;           // words
@@ -482,10 +555,11 @@ struct Plan {
 
 // attempts generated: 4/3 of the pairs plus 4096 (acceptance pi/4: 1.27 attempts per pair expected), as the
 // host path (np_legacy_gauss.c); the block stride P of the streams from a cost model of the two parallel
-// phases, measured on MI355X (profiles/r15np/): the jumps run in rounds of 64 streams (kJSplit workgroups each,
-// one per CU) of ~70 us, a stream twists its P blocks at ~0.38 us each (MPPI_NP_STRIDE forces P, for
-// measurements).  Config 3 (8.4 M normals, 35.9 k blocks): P = 256, 141 streams.
-constexpr double kJumpRoundUs = 70.0, kBlockUs = 0.38;
+// phases, measured on MI355X (profiles/r15np/, profiles/r15npj/): the table jump costs ~0.48 us per stream (the
+// list jump ran in rounds of 64 streams of ~70 us), a stream twists its P blocks at ~0.38 us each (MPPI_NP_STRIDE
+// forces P, for measurements).  Config 3 (8.4 M normals, 35.9 k blocks): P = 256, 141 streams.
+constexpr double kJumpRoundUs = 70.0, kBlockUs = 0.38;   // the set-bit list jump: rounds of 64 streams
+constexpr double kJumpStreamUs = 0.48;                     // the table jump: ~linear in the streams (67.8 us for 140)
 Plan make_plan(long long n, int pos, int has_gauss) {
     Plan p;
     p.need = n - (has_gauss ? 1 : 0);
@@ -499,7 +573,9 @@ Plan make_plan(long long n, int pos, int has_gauss) {
     for (int P = 16; P <= (1 << 22); P <<= 1) {
         const long long streams = (p.nblk - 1 + P - 1) / P;
         if (streams > MPPI_NP_MAX_STREAMS || (forced && P != forced)) continue;
-        const double cost = (double)((streams - 1 + 63) / 64) * kJumpRoundUs + P * kBlockUs;
+        const double jump = MPPI_NP_JUMP_TABLE ? (double)(streams - 1) * kJumpStreamUs
+                                               : (double)((streams - 1 + 63) / 64) * kJumpRoundUs;
+        const double cost = jump + P * kBlockUs;
         if (cost < best) {
             best = cost;
             p.P = P;
@@ -549,6 +625,7 @@ void mppi_np_ctx_destroy(mppi_np_ctx* c) {
     (void)hipFree(c->d_seq);
     (void)hipFree(c->d_bits);
     (void)hipFree(c->d_nbits);
+    (void)hipFree(c->d_nibs);
     (void)hipFree(c->d_jumped);
     (void)hipFree(c->d_words);
     (void)hipFree(c->d_counts);
@@ -578,12 +655,41 @@ int mppi_np_set_jumps(mppi_np_ctx* c, int block_stride, int streams, const unsig
     if (c->pending) NP_CHECK(hipEventSynchronize(c->done));   // the buffers may be in use by the last draw
     (void)hipFree(c->d_bits);
     (void)hipFree(c->d_nbits);
+    (void)hipFree(c->d_nibs);
     (void)hipFree(c->d_jumped);
     c->d_bits = nullptr;
     c->d_nbits = nullptr;
+    c->d_nibs = nullptr;
     c->d_jumped = nullptr;
     c->poly_P = c->poly_streams = 0;
-    if (streams > 1) {
+    if (streams > 1 && MPPI_NP_JUMP_TABLE) {
+        const int ns = streams - 1;
+        const int G = (ns + kNibS - 1) / kNibS;
+        int R = std::max(1, std::min(kChunks, (kJTableWGs + G - 1) / G));
+        const int cpw = (kChunks + R - 1) / R;
+        R = (kChunks + cpw - 1) / cpw;
+        std::vector<uint32_t> nibs((size_t)kChunks * G * kNibW, 0u);
+        for (int j = 0; j < ns; ++j)
+            for (int w = 0; w < kPolyWords; ++w) {
+                const uint64_t m = polys[(size_t)j * kPolyWords + w];
+                if (!m) continue;
+                if (64 * w + 63 - __builtin_clzll(m) >= kDeg)
+                    return fail(MPPI_E_ARG, "mppi_np_set_jumps: a polynomial of degree >= 19937");
+                for (int h = 0; h < 16; ++h) {   // the 16 chunks of this 64-bit word
+                    const uint32_t v = (uint32_t)(m >> (4 * h)) & 15u;
+                    const int ch = 16 * w + h;
+                    if (v && ch < kChunks)
+                        nibs[((size_t)ch * G + j / kNibS) * kNibW + (j % kNibS) / 8] |= v << (4 * (j % 8));
+                }
+            }
+        NP_CHECK(hipMalloc(&c->d_nibs, nibs.size() * sizeof(uint32_t)));
+        NP_CHECK(hipMemcpy(c->d_nibs, nibs.data(), nibs.size() * sizeof(uint32_t), hipMemcpyHostToDevice));
+        NP_CHECK(hipMalloc(&c->d_jumped, (size_t)ns * R * kN * sizeof(uint32_t)));
+        c->jG = G;
+        c->jR = R;
+        c->jcpw = cpw;
+        c->jparts = R;
+    } else if (streams > 1) {
         const size_t ns = (size_t)(streams - 1);
         std::vector<uint32_t> lists(ns * kJListStride, 4u * kSeqPad);
         std::vector<int> counts(ns);
@@ -602,6 +708,7 @@ int mppi_np_set_jumps(mppi_np_ctx* c, int block_stride, int streams, const unsig
         NP_CHECK(hipMalloc(&c->d_nbits, ns * sizeof(int)));
         NP_CHECK(hipMemcpy(c->d_nbits, counts.data(), ns * sizeof(int), hipMemcpyHostToDevice));
         NP_CHECK(hipMalloc(&c->d_jumped, ns * kJSplit * kN * sizeof(uint32_t)));
+        c->jparts = kJSplit;
     }
     c->poly_P = block_stride;
     c->poly_streams = streams;
@@ -646,11 +753,16 @@ int mppi_np_draw(mppi_np_ctx* c, void* stream, const mppi_np_state* st, long lon
     NP_CHECK(hipMemcpyAsync(c->d_key, c->h_key, kN * sizeof(uint32_t), hipMemcpyHostToDevice, s));
     if (p.streams > 1) {
         hipLaunchKernelGGL(np_seq_kernel, dim3(1), dim3(kTT), 0, s, c->d_key, c->d_seq);
-        hipLaunchKernelGGL(np_jump_kernel, dim3(kJSplit, p.streams - 1), dim3(kJT), kJumpLds, s, c->d_seq, c->d_bits,
-                           c->d_nbits, c->d_jumped);
+        if (MPPI_NP_JUMP_TABLE)
+            hipLaunchKernelGGL(np_jumpn_kernel, dim3(c->jR, c->jG), dim3(kJNT),
+                               (4 * c->jcpw + kN + 3) * sizeof(uint32_t), s, c->d_seq, c->d_nibs, c->jG, c->jcpw,
+                               p.streams - 1, c->jR, c->d_jumped);
+        else
+            hipLaunchKernelGGL(np_jump_kernel, dim3(kJSplit, p.streams - 1), dim3(kJT), kJumpLds, s, c->d_seq, c->d_bits,
+                               c->d_nbits, c->d_jumped);
     }
     hipLaunchKernelGGL(np_gen_kernel, dim3(p.streams), dim3(kTT), 0, s, c->d_key, c->d_jumped, c->d_words, p.P,
-                       (int)p.nblk);
+                       (int)p.nblk, c->jparts);
     hipLaunchKernelGGL(np_count_kernel, dim3((unsigned)nwg), dim3(kNT), 0, s, c->d_words, (long long)st->pos, p.A,
                        c->d_counts);
     hipLaunchKernelGGL(np_scan_kernel, dim3(1), dim3(kScanT), 0, s, c->d_counts, c->d_offsets, (int)nwg, p.pairs,
