@@ -55,7 +55,8 @@ constexpr int kDeg = 19937;
 constexpr int kPolyWords = MPPI_NP_POLY_WORDS;        // 312 x 64 bits: a polynomial of degree < 19937
 constexpr int kSeqBlocks = (kDeg + kN) / kN + 1;      // 34: the windows d + j < 19937 + 624 of the jumps
 constexpr int kNT = 256;                              // threads of the attempt kernels
-constexpr int kTT = 640;                              // threads of the twist kernels: one word per thread
+constexpr int kTT = 704;                              // threads of the twist kernels: one word per thread, the
+                                                      // twist's three ranges on whole waves (twist_slot)
 constexpr int kJHalf = 320;                           // lanes of a jump group; a lane's second word: 5 x 64 on
 constexpr int kJGroups = 3;                           // groups of a jump workgroup, each a share of the bits
 constexpr int kJT = kJGroups * kJHalf;                // threads of a jump workgroup (15 waves)
@@ -96,6 +97,14 @@ __device__ __forceinline__ uint32_t twist_word(const uint32_t* o, int i) {
     const uint32_t k0 = o[kM] ^ mt_mix(o[0], o[1]);
     const uint32_t k396 = o[566] ^ mt_mix(o[169], o[170]) ^ mt_mix(o[396], o[397]);
     return k396 ^ mt_mix(o[623], k0);
+}
+
+// The word a twist thread computes (-1: none): waves 0-3 words [0, 227), waves 4-7 [227, 454), waves 8-10
+// [454, 624), so each wave runs one branch of twist_word (the last one also word 623's)
+__device__ __forceinline__ int twist_slot(int t) {
+    if (t < 256) return t < kN - kM ? t : -1;
+    if (t < 512) return t - 256 < kN - kM ? t - 256 + (kN - kM) : -1;
+    return t - 512 < kN - 2 * (kN - kM) ? t - 512 + 2 * (kN - kM) : -1;
 }
 
 __device__ __forceinline__ uint32_t temper(uint32_t y) {
@@ -142,15 +151,15 @@ struct NpShape {
 // ------------------------------------------------------------------ generation
 __global__ __launch_bounds__(kTT) void np_seq_kernel(const uint32_t* __restrict__ key, uint32_t* __restrict__ seq) {
     __shared__ uint32_t buf[2][kN];
-    const int i = threadIdx.x;
-    uint32_t v = i < kN ? key[i] : 0u;
-    if (i < kN) {
+    const int i = twist_slot(threadIdx.x);
+    uint32_t v = i >= 0 ? key[i] : 0u;
+    if (i >= 0) {
         buf[0][i] = v;
         seq[i] = v;
     }
     __syncthreads();
     for (int b = 1; b < kSeqBlocks; ++b) {
-        if (i < kN) {
+        if (i >= 0) {
             v = twist_word(buf[(b - 1) & 1], i);
             buf[b & 1][i] = v;
             seq[(size_t)b * kN + i] = v;
@@ -306,17 +315,17 @@ __global__ __launch_bounds__(kJNT) void np_jumpn_kernel(const uint32_t* __restri
 __global__ __launch_bounds__(kTT) void np_gen_kernel(const uint32_t* __restrict__ key, const uint32_t* __restrict__ parts,
                                                      uint32_t* __restrict__ words, int P, int nblk, int nparts) {
     __shared__ uint32_t buf[2][kN];
-    const int s = blockIdx.x, i = threadIdx.x;
+    const int s = blockIdx.x, i = twist_slot(threadIdx.x);
     const int b0 = 1 + P * s, b1 = min(1 + P * (s + 1), nblk);
     if (s == 0) {
-        if (i < kN) {
+        if (i >= 0) {
             const uint32_t v = key[i];
             buf[0][i] = v;
             words[i] = v;
         }
         __syncthreads();
     } else {
-        if (i < kN) {
+        if (i >= 0) {
             const uint32_t* q = parts + (size_t)(s - 1) * nparts * kN + i;
             uint32_t v = 0;
             int h = 0;
@@ -331,12 +340,12 @@ __global__ __launch_bounds__(kTT) void np_gen_kernel(const uint32_t* __restrict_
             buf[1][i] = v;
         }
         __syncthreads();
-        if (i < kN) buf[0][i] = twist_word(buf[1], i);   // block P s, exactly
+        if (i >= 0) buf[0][i] = twist_word(buf[1], i);   // block P s, exactly
         __syncthreads();
     }
     int cur = 0;
     for (int b = b0; b < b1; ++b) {
-        if (i < kN) {
+        if (i >= 0) {
             const uint32_t v = twist_word(buf[cur], i);
             buf[cur ^ 1][i] = v;
             words[(size_t)b * kN + i] = v;
