@@ -674,7 +674,7 @@ int mppi_np_set_jumps(mppi_np_ctx* c, int block_stride, int streams, const unsig
     if (streams > 1 && MPPI_NP_JUMP_TABLE) {
         const int ns = streams - 1;
         const int G = (ns + kNibS - 1) / kNibS;
-        int R = std::max(1, std::min(kChunks, (kJTableWGs + G - 1) / G));
+        int R = std::max(1, std::min(128, (kJTableWGs + G - 1) / G));   // at most 128 parts for np_gen_kernel to XOR
         const int cpw = (kChunks + R - 1) / R;
         R = (kChunks + cpw - 1) / cpw;
         std::vector<uint32_t> nibs((size_t)kChunks * G * kNibW, 0u);
