@@ -302,7 +302,7 @@ int mppi_debug_nearest(mppi_ctx *ctx, const float *noise_dev, int K, int *slot_d
  * Euler as control.py:256-259) and reduces to the reference _F
  * (control.py:234-263) at n = 2 with I = l and J = b = 0.  The
  * cost is control.py:174-232 on (end-effector x, y, dq_1, dq_2).  Same
- * conventions as above; noise is [T][n][K_local] fp32, u and w_eps are T x n
+ * conventions as above; noise is [T][K_local][n] fp32, u and w_eps are T x n
  * row-major, x0 = [q(n), dq(n)].
  * ------------------------------------------------------------------------ */
 #define MPPI_CHAIN_MAX_DOF 8   /* array capacity; n in [2, 7] is supported */
@@ -381,7 +381,7 @@ int mppi_chain_optimal_traj_host(mppi_chain_ctx *ctx, const double *x0, const do
 /* control.py:129-145 analogue: out_dev[K][T][2n] fp32 (q, dq) */
 int mppi_chain_rollout_traj(mppi_chain_ctx *ctx, const double *base_u, const float *noise_dev, int K,
                             float *out_dev);
-/* N(0, Sigma) noise [T][n][K_local] from Philox4x32-10 (global sample index: shard-invariant) */
+/* N(0, Sigma) noise [T][K_local][n] from Philox4x32-10 (global sample index: shard-invariant) */
 int mppi_chain_noise_philox(mppi_chain_ctx *ctx, unsigned long long seed, unsigned long long step,
                             float *out_dev);
 int mppi_chain_sync(mppi_chain_ctx *ctx);

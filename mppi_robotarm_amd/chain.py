@@ -98,7 +98,7 @@ def _dptr(a: np.ndarray):
 
 
 class ChainEngine:
-    """Owns one ``mppi_chain_ctx`` (one device, one shard of samples); noise layout [T][n][K_local] fp32."""
+    """Owns one ``mppi_chain_ctx`` (one device, one shard of samples); noise layout [T][K_local][n] fp32."""
 
     def __init__(self, K_local: int, T: int, delta_t: float, param_lambda: float, param_alpha: float, sigma,
                  stage_cost_weight, terminal_cost_weight, param_exploration: float = 0.0,
@@ -175,13 +175,13 @@ class ChainEngine:
             N.check(self._lib.mppi_chain_set_stream(self._ctx, C.c_void_p(s.cuda_stream)), "mppi_chain_set_stream")
 
     def new_noise(self) -> torch.Tensor:
-        return torch.empty((self.T, self.n, self.K_local), dtype=torch.float32, device=self.device)
+        return torch.empty((self.T, self.K_local, self.n), dtype=torch.float32, device=self.device)
 
     def new_partial(self) -> torch.Tensor:
         return torch.empty(self.partial_len, dtype=torch.float64, device=self.device)
 
     def upload_noise(self, eps_ktn: np.ndarray, out: torch.Tensor | None = None) -> torch.Tensor:
-        """Reference-order noise (K_local, T, n) -> device [T][n][K_local] fp32."""
+        """Reference-order noise (K_local, T, n) -> device [T][K_local][n] fp32."""
         out = self.new_noise() if out is None else out
         # the fp64 draw as it is (one pageable copy, the host array free once it returns), then the transpose
         # and the fp64 -> fp32 rounding (to nearest, as NumPy's astype) in one device copy: the host transpose,
@@ -191,13 +191,13 @@ class ChainEngine:
         if stage is None or tuple(stage.shape) != eps.shape:
             stage = self._noise_stage = torch.empty(eps.shape, dtype=torch.float64, device=self.device)
         stage.copy_(torch.from_numpy(eps))
-        out.copy_(stage.permute(1, 2, 0))
+        out.copy_(stage.permute(1, 0, 2))
         return out
 
     def upload_std_noise(self, noise, z: torch.Tensor, out: torch.Tensor) -> torch.Event:
-        """As RolloutEngine.upload_std_noise, into the chain's [T][n][K_local] layout."""
+        """As RolloutEngine.upload_std_noise, into the chain's [T][K_local][n] layout."""
         from .engine import _upload_std
-        return _upload_std(self, noise, z, out, (1, 2, 0))
+        return _upload_std(self, noise, z, out, (1, 0, 2))
 
     def set_step_inputs(self, x0, window, u=None) -> None:
         self._sync_stream()
@@ -338,7 +338,7 @@ class ChainEngine:
         N.check(self._lib.mppi_chain_sync(self._ctx), "mppi_chain_sync")
 
     def _check_noise(self, noise: torch.Tensor) -> None:
-        shape = (self.T, self.n, self.K_local)
+        shape = (self.T, self.K_local, self.n)
         if (noise.dtype != torch.float32 or not noise.is_contiguous() or noise.device != self.device
                 or tuple(noise.shape) != shape):
             raise ValueError(f"noise must be a contiguous fp32 {shape} tensor on {self.device}")
@@ -551,7 +551,7 @@ class ChainMPPIController:
         eng._sync_stream()
         kl = eng.K_local
         self._npdev.draw(state, (int(self.K), int(self.T), self.dim_u), plan, self._noise_dev, eng.stream.cuda_stream,
-                         eng.k_offset, kl, (self.dim_u * kl, 1, kl))   # [T][n][K_local]
+                         eng.k_offset, kl, (self.dim_u * kl, self.dim_u, 1))   # [T][K_local][n]
         new = self._npdev.result()
         if new is None:
             return None

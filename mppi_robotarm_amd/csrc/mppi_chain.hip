@@ -11,7 +11,8 @@
 //    triangular solves -> joint accelerations -> semi-implicit Euler -> new
 //    sincos (shared with the next step and the end-effector kinematics) ->
 //    the window search of the 2-link engine -> stage + control cost.  Noise is
-//    [T][N][K] fp32: N coalesced 4-B-per-lane rows per step.  Same epilogue,
+//    [T][K][N] fp32 (like the 2-link engine's [T][K][2]): a sample's N values of
+//    a step contiguous, so a weighted sample's noise is T cache lines.  Same epilogue,
 //    in-launch merges and fused update as the 2-link engine (mppi_device.h),
 //    with T*N columns per partial row (MAXCH = 4 column chunks).
 //  * chain_traj_kernel<N, NOISE>, chain_philox_kernel: trajectory re-roll and
@@ -573,7 +574,7 @@ __device__ __forceinline__ double chain_horizon_f64(const ChainConst& c, const C
     double S = 0.0, ex = 0.0, ey = 0.0, e1 = 0.0, e2 = 0.0;
     float nx[N];
 #pragma unroll
-    for (int d = 0; d < N; ++d) nx[d] = noise[(size_t)d * K + k];
+    for (int d = 0; d < N; ++d) nx[d] = noise[(size_t)k * N + d];
     for (int t = 0; t < T; ++t) {
         double v[N], g = 0.0;
 #pragma unroll
@@ -583,7 +584,7 @@ __device__ __forceinline__ double chain_horizon_f64(const ChainConst& c, const C
         }
         const int tn = t + 1 < T ? t + 1 : t;
 #pragma unroll
-        for (int d = 0; d < N; ++d) nx[d] = noise[((size_t)tn * N + d) * K + k];
+        for (int d = 0; d < N; ++d) nx[d] = noise[((size_t)tn * K + k) * N + d];
         x.step(v, kd);
         double px, py;
         x.effector(kd, &px, &py);
@@ -739,9 +740,9 @@ __device__ __forceinline__ double chain_horizon_q4(const ChainConst& c, const Ch
         Sn = f32x2{__builtin_amdgcn_sinf(TH.x), __builtin_amdgcn_sinf(TH.y)};
     };
     angles();
-    // noise of links (a0, a1) at step t: rows (t N + d) K + k; pad links read link N - 1 (masked below);
+    // noise of links (a0, a1) at step t: floats (t K + k) N + d; pad links read link N - 1 (masked below);
     // the host keeps T N K 4 below 2^31 for this kernel (mppi_chain_ctx_create)
-    const unsigned o0 = (unsigned)(min(a0, N - 1) * K + k) * 4u, o1 = (unsigned)(min(a1, N - 1) * K + k) * 4u;
+    const unsigned o0 = (unsigned)(k * N + min(a0, N - 1)) * 4u, o1 = (unsigned)(k * N + min(a1, N - 1)) * 4u;
     const __amdgpu_buffer_rsrc_t nrs = rows_rsrc(noise, T * N * K * 4);
     const int rowb = N * K * 4;
     auto nrow = [&](int t) {
@@ -971,20 +972,20 @@ __global__ __launch_bounds__(kCT) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
     SearchLDS<true> sr{s_keys, st->ctr.x, st->ctr.y};
     ChainState<N> x;
     x.load(st->x0);
-    // noise row (t, d) of sample k: noise[(t N + d) K + k]; prefetches past the
-    // last step read row T - 1 again (never used)
-    // (uniform row base + a 32-bit lane byte offset: the saddr form of global_load)
-    const unsigned kb = (unsigned)k * 4u;
+    // noise (t, d) of sample k: noise[(t K + k) N + d] (a sample's N values of a step contiguous); prefetches
+    // past the last step read step T - 1 again (never used)
+    // (uniform step base + a 32-bit lane byte offset: the saddr form of global_load)
+    const unsigned kb = (unsigned)k * (unsigned)N * 4u;
 #ifdef MPPI_CHAIN_NOISE_BUFFER
     // row offset in the buffer instruction's scalar soffset: no 64-bit VALU address per load
     const __amdgpu_buffer_rsrc_t nrs = rows_rsrc(noise, T * N * K * 4);
     auto nrow = [&](int t, int d) {
-        const int so = __builtin_amdgcn_readfirstlane((min(t, T - 1) * N + d) * K * 4);
-        return __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(nrs, (int)kb, so, 0));
+        const int so = __builtin_amdgcn_readfirstlane(min(t, T - 1) * K * N * 4);
+        return __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(nrs, (int)kb + 4 * d, so, 0));
     };
 #else
     auto nrow = [&](int t, int d) {
-        const char* row = (const char*)(noise + ((size_t)min(t, T - 1) * N + d) * K);
+        const char* row = (const char*)(noise + (size_t)min(t, T - 1) * K * N + d);
         return *(const float*)(row + kb);
     };
 #endif
@@ -1156,10 +1157,11 @@ __global__ __launch_bounds__(kCT) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
             publish(blockIdx.x * stride + 4 + 2 * tid, s_e[tid]);
         }
     } else if (nl <= kSparseMax) {
-        // column (t, d) = t N + d of the noise is the row noise[col K : col K + K]
+        // column (t, d) = t N + d of the noise: sample k's value at noise[(t K + k) N + d]
         for (int col = tid; col < nval; col += kCT) {
-            const float* base = noise + (size_t)col * K;
-            publish(blockIdx.x * stride + 2 + col, gather_col(base, 1, s_k, s_e, nl));
+            const int tt = col / N;
+            const float* base = noise + (size_t)tt * K * N + (col - tt * N);
+            publish(blockIdx.x * stride + 2 + col, gather_col(base, N, s_k, s_e, nl));
         }
     } else {
         constexpr int PER = (NS + 63) / 64;
@@ -1181,7 +1183,10 @@ __global__ __launch_bounds__(kCT) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
             for (int r = 0; r < kRowBatch; ++r) {
                 const int cr = min(cb + r, nval - 1);
 #pragma unroll
-                for (int i = 0; i < PER; ++i) e[r][i] = noise[(size_t)cr * K + min(k0 + lane + 64 * i, K - 1)];
+                for (int i = 0; i < PER; ++i) {
+                    const int tt = cr / N;
+                    e[r][i] = noise[((size_t)tt * K + min(k0 + lane + 64 * i, K - 1)) * N + (cr - tt * N)];
+                }
             }
 #pragma unroll
             for (int r = 0; r < kRowBatch; ++r) {
@@ -1200,7 +1205,7 @@ __global__ __launch_bounds__(kCT) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
     if constexpr (POLL) {
         if ((int)blockIdx.x != g * kGroup) return;
         STAMP(3, NOW());
-        const ListSrc ls{noise, K};
+        const ListSrc ls{noise, K, N};
         if (ngroups == 1) {
             merge_rows_block<kCT, kCMaxCh, true, true, decltype(sm), kList>(slab_r, 0, gsz, geo, c.inv_lambda, sm,
                                                                             nullptr, 0, partial_out, w_eps_out, tag,
@@ -1297,7 +1302,7 @@ __global__ __launch_bounds__(kCT) void chain_traj_kernel(const ChainConst c, con
             const int t = min(t0 + j, T - 1);
             const int ti = t == 0 ? T - 1 : t - 1;
 #pragma unroll
-            for (int d = 0; d < N; ++d) e[j][d] = NOISE ? noise[((size_t)ti * N + d) * c.K_local + k] : 0.f;
+            for (int d = 0; d < N; ++d) e[j][d] = NOISE ? noise[((size_t)ti * c.K_local + k) * N + d] : 0.f;
         }
     };
     float cur[kChainTB][N];
@@ -1338,7 +1343,7 @@ __global__ __launch_bounds__(kCT) void chain_traj_kernel(const ChainConst c, con
     }
 }
 
-// eps[t][d][k] = (L z)_d, z ~ N(0, I) from Philox4x32-10 counters (global k, t,
+// eps[t][k][d] = (L z)_d, z ~ N(0, I) from Philox4x32-10 counters (global k, t,
 // call) + Box-Muller: a shard generates exactly its slice of the unsharded draw.
 // The factor travels by value (kernel argument, scalar loads) and the link count
 // is a template argument, so the matvec unrolls and z stays in registers (a
@@ -1367,13 +1372,13 @@ __global__ __launch_bounds__(kCT) void chain_philox_kernel(int K_local, int T, l
         z[4 * call + 2] = b.x;
         z[4 * call + 3] = b.y;
     }
-    float* row = out + (size_t)t * N * K_local + k;
+    float* row = out + ((size_t)t * K_local + k) * N;
 #pragma unroll
     for (int d = 0; d < N; ++d) {
         float e = 0.f;
 #pragma unroll
         for (int j = 0; j <= d; ++j) e = fmaf(Lc.L[d * kCMax + j], z[j], e);
-        row[(size_t)d * K_local] = e;
+        row[d] = e;
     }
 }
 

@@ -538,7 +538,7 @@ __device__ __forceinline__ void put_final(double rho, const double (&acc)[MAXCH]
 // merger that needs the row's columns gathers them from the noise itself with the row gather's operations in its
 // order (gather_col_n: fp64 fma over l from 0), so a list row merges to the same bits as the column row it
 // replaces, and only the rows that carry weight in some merge are ever gathered: a row's own gather cannot know
-// that, and read a cache line per value for every row (the chain's [T][n][K] noise).  Not the product: an A/B
+// that, and read a cache line per value for every row (the chain's noise: ~T lines per sample).  Not the product: an A/B
 // variant (MPPI_CHAIN_LIST in mppi_chain.hip; TRIED.md) that cut the c5 shard's traffic 1.14x -> 1.04x at +1.9 %
 // time.
 #ifndef MPPI_LIST_MAX
@@ -547,8 +547,8 @@ __device__ __forceinline__ void put_final(double rho, const double (&acc)[MAXCH]
 constexpr int kListMax = MPPI_LIST_MAX;
 constexpr unsigned kListHi = 0x7ff4c0deu;
 struct ListSrc {
-    const float* noise = nullptr;   // the row's column j (t n + d) of sample k at noise[j K + k]
-    int K = 0;
+    const float* noise = nullptr;   // the row's column j = t n + d of sample k at noise[(t K + k) n + d]
+    int K = 0, n = 1;
 };
 // A list-only row (its columns not published) says so in its rho granule: both tag words carry kListTagBit
 // (tags stay below it), so the merger knows from the rho poll which weighted rows it must gather itself, and a
@@ -607,11 +607,12 @@ __device__ __forceinline__ void list_entries(double (&x)[LB], int b0, int nb, in
     for (int j = 0; j < LB; ++j) {
         const int i = min(b0 + j / MAXCH, 63), col = tid + (j % MAXCH) * NT;
         const int nli = b0 + j / MAXCH < nb ? __builtin_amdgcn_readlane(nl_l, i) : 0;   // uniform
-        const size_t cb = (size_t)min(max(col - 1, 0), ncol - 2) * ls.K;
+        const int cc = min(max(col - 1, 0), ncol - 2), tt = cc / ls.n;
+        const size_t cb = (size_t)tt * ls.K * ls.n + (cc - tt * ls.n);
 #pragma unroll
         for (int l = 0; l < kListMax; ++l) {
             const int kk = __builtin_amdgcn_readlane(k_l[l], i);
-            e[j][l] = l < nli ? ls.noise[cb + kk] : 0.f;
+            e[j][l] = l < nli ? ls.noise[cb + (size_t)kk * ls.n] : 0.f;
         }
     }
 #pragma unroll

@@ -482,7 +482,7 @@ __global__ __launch_bounds__(kNT) void np_write_kernel(const uint32_t* __restric
     const long long s_lo = max(k_lo, (long long)sh.k_offset), s_hi = min(k_hi, (long long)sh.k_offset + sh.K_local - 1);
     if (s_hi < s_lo) return;
     const unsigned nk = (unsigned)(s_hi - s_lo + 1), du = sh.du;
-    const bool k_inner = sh.sk == 1;   // [T][n][K] (the chain): samples innermost; else (t, k, d) order
+    const bool k_inner = sh.sk == 1;   // a [T][du][K] layout: samples innermost; else (t, k, d) order
     const unsigned per_t = nk * du, total = per_t * (sh.per_k / du);
     for (unsigned e = threadIdx.x; e < total; e += kNT) {
         const unsigned t = e / per_t, rem = e - t * per_t;

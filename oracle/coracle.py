@@ -114,13 +114,17 @@ def _chain_strides(eps, layout):
     if layout == "KTN":
         K, T, n = eps.shape
         return K, T, n, T * n, n, 1
-    T, n, K = eps.shape                      # "TNK": device order [T][n][K]
+    if layout == "TKN":                      # the device order [T][K][n]
+        T, K, n = eps.shape
+        return K, T, n, n, K * n, 1
+    T, n, K = eps.shape                      # "TNK": [T][n][K]
     return K, T, n, 1, n * K, K
 
 
 def chain_rollout_costs(x0, u, eps, window, dt, lam, alpha, sigma, stage_w, term_w, P, k_exploit=None,
                         k_offset=0, layout="KTN", k_range=None, nthreads=0):
-    """S of the chain for samples ``k_range`` (default all); eps fp32 (K,T,n) "KTN" or (T,n,K) "TNK"."""
+    """S of the chain for samples ``k_range`` (default all); eps fp32 (K,T,n) "KTN", (T,K,n) "TKN" (the device's)
+    or (T,n,K) "TNK"."""
     eps = np.ascontiguousarray(eps, dtype=np.float32)
     K, T, n, sk, st, sd = _chain_strides(eps, layout)
     k0, k1 = (0, K) if k_range is None else k_range

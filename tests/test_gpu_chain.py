@@ -117,7 +117,7 @@ def test_chain_n7_against_c_oracle(K, T, lam, s99, lps, paths):
     eng.rollout(noise, S_out=S_dev)
     w = eng.weighted_noise()
     S = S_dev.cpu().numpy()
-    nz = noise.cpu().numpy()
+    nz = noise.cpu().numpy().transpose(0, 2, 1)   # device [T][K][n] -> (T, n, K)
     Sr = coracle.chain_rollout_costs(x0, u, nz, win, 0.006, lam, 0.98, sig, W, TW, CO.ChainParams(), layout="TNK")
     _, wr = coracle.chain_weighted_noise(Sr, nz, lam, layout="TNK")
     rel = np.abs(S - Sr) / np.abs(Sr)
@@ -224,7 +224,7 @@ def test_chain_shards_and_device_merge(paths):
         e = _engine(Kl, T, 1.0e7, K_total=K, k_offset=g * Kl)
         e.set_step_inputs(x0, paths["xydq_circle"][:30], u)
         nz = e.philox_noise(21, 4)
-        assert torch.equal(nz, noise[:, :, g * Kl:(g + 1) * Kl])
+        assert torch.equal(nz, noise[:, g * Kl:(g + 1) * Kl, :])
         e.rollout(nz, partial_out=parts[g * e.partial_len:(g + 1) * e.partial_len])
         engs.append(e)
     engs[0].merge(parts, G)
@@ -237,8 +237,8 @@ def test_chain_philox_noise_has_covariance_sigma():
     K, T = 65536, 4
     _, _, sig, _ = _c5()
     eng = _engine(K, T)
-    z = eng.philox_noise(3, 0).cpu().numpy()                    # (T, 7, K)
-    x = z.transpose(0, 2, 1).reshape(-1, 7).astype(np.float64)
+    z = eng.philox_noise(3, 0).cpu().numpy()                    # (T, K, 7)
+    x = z.reshape(-1, 7).astype(np.float64)
     assert np.max(np.abs(x.mean(0))) < 0.05
     cov = np.cov(x.T)
     np.testing.assert_allclose(cov, sig, atol=0.1 * np.sqrt(np.outer(np.diag(sig), np.diag(sig))).max() / 4)
@@ -253,7 +253,7 @@ def test_chain_trajectories_match_oracle(paths):
     eng.set_step_inputs(x0, paths["xydq_circle"][:30], u)
     noise = eng.philox_noise(2, 0)
     tr = eng.trajectories(base_u=u, noise=noise).double().cpu().numpy()
-    nz = noise.cpu().numpy()
+    nz = noise.cpu().numpy().transpose(0, 2, 1)   # device [T][K][n] -> (T, n, K)
     ctrl = np.roll(u[None] + nz.transpose(2, 0, 1), 1, axis=1)    # control(t) = u[t-1] + eps[t-1]
     ref = coracle.chain_traj(x0, ctrl, 0.006, CO.ChainParams())
     np.testing.assert_allclose(tr, ref, rtol=1e-4, atol=1e-4)
@@ -305,7 +305,7 @@ def _link_case(n, K, T, lam, paths, precision="f32", lps=1):
     eng.rollout(noise, S_out=S_dev)
     w = eng.weighted_noise()
     S = S_dev.cpu().numpy()
-    nz = noise.cpu().numpy()
+    nz = noise.cpu().numpy().transpose(0, 2, 1)   # device [T][K][n] -> (T, n, K)
     eng.close()
     Sr = coracle.chain_rollout_costs(x0, u, nz, win, 0.006, lam, 0.98, sig, W, TW, Po, layout="TNK")
     _, wr = coracle.chain_weighted_noise(Sr, nz, lam, layout="TNK")
@@ -366,7 +366,7 @@ def test_chain_c5_spread_weights(paths):
         eng.rollout(noise, S_out=S_dev)
         w = eng.weighted_noise()
         S = S_dev.cpu().numpy()
-        nz = noise.cpu().numpy()
+        nz = noise.cpu().numpy().transpose(0, 2, 1)   # device [T][K][n] -> (T, n, K)
         eng.close()
         if prec == "f64":
             Sr = coracle.chain_rollout_costs(x0, u, nz, win, 0.006, lam, 0.98, sig, W, TW, CO.ChainParams(),
@@ -462,7 +462,7 @@ def test_chain_short_horizons(T, precision, lps, paths):
     eng.rollout(noise, S_out=S_dev)
     w = eng.weighted_noise()
     S = S_dev.cpu().numpy()
-    nz = noise.cpu().numpy()
+    nz = noise.cpu().numpy().transpose(0, 2, 1)   # device [T][K][n] -> (T, n, K)
     eng.close()
     Sr = coracle.chain_rollout_costs(x0, u, nz, win, 0.006, lam, 0.98, sig, W, TW, CO.ChainParams(), layout="TNK")
     _, wr = coracle.chain_weighted_noise(Sr, nz, lam, layout="TNK")

@@ -51,7 +51,7 @@ def test_chain_noise_stream(K_local, T, k_offset, seed, step):
     from mppi_robotarm_amd.chain import CHAIN7_SIGMA, ChainEngine
     eng = ChainEngine(K_local, T, 0.006, 100.0, 0.98, CHAIN7_SIGMA, [0.5, 0.5, 5, 5], [5, 5, 50, 50],
                       K_total=k_offset + K_local, k_offset=k_offset, device=0)
-    dev = eng.philox_noise(seed, step).double().cpu().numpy()
+    dev = eng.philox_noise(seed, step).double().cpu().numpy().transpose(0, 2, 1)   # device [T][K][n] -> (T, n, K)
     ref = P.chain_noise(K_local, T, 7, k_offset, seed, step, CHAIN7_SIGMA)
     err = np.abs(dev - ref) / (1.0 + np.abs(ref))
     assert float(np.max(err)) < TOL, float(np.max(err))

@@ -33,7 +33,7 @@ for lam in lams:
     eng.rollout(noise, S_out=S_dev)
     w = eng.weighted_noise()
     S = S_dev.cpu().numpy()
-    nz = noise.cpu().numpy()
+    nz = noise.cpu().numpy().transpose(0, 2, 1)   # device [T][K][n] -> (T, n, K)
     Sr = coracle.chain_rollout_costs(CHAIN7_X0, u, nz, win, 0.006, lam, 0.98, CHAIN7_SIGMA, W, TW, CO.ChainParams(),
                                      layout="TNK")
     _, wr = coracle.chain_weighted_noise(Sr, nz, lam, layout="TNK")
@@ -60,7 +60,7 @@ eng = ChainEngine(K, T, 0.006, 100.0, 0.98, CHAIN7_SIGMA, W, TW, 0.0, ChainParam
 eng.set_step_inputs(CHAIN7_X0, win, u)
 noise = eng.philox_noise(11, 2)
 tr = eng.trajectories(u, noise, K=Kd).cpu().numpy().astype(np.float64)   # (Kd, T, 14)
-nz = noise.cpu().numpy()[:, :, :Kd].astype(np.float64)                  # (T, 7, Kd)
+nz = noise.cpu().numpy().transpose(0, 2, 1)[:, :, :Kd].astype(np.float64)   # device (T, K, 7) -> (T, 7, Kd)
 ti = (np.arange(T) - 1) % T
 ctrl = (u[ti][None] + nz[ti].transpose(2, 0, 1))                          # control(t) = u[t-1] + eps[t-1]
 ref = CO.chain_rollout_trajectory(CHAIN7_X0, ctrl, 0.006, CO.ChainParams())

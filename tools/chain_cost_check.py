@@ -25,7 +25,7 @@ for T in (1, 2, 4):
     S_dev = torch.empty(K, dtype=torch.float64, device="cuda")
     eng.rollout(noise, S_out=S_dev)
     S = S_dev.cpu().numpy()
-    nz = noise.cpu().numpy()
+    nz = noise.cpu().numpy().transpose(0, 2, 1)   # device [T][K][n] -> (T, n, K)
     Sr = coracle.chain_rollout_costs(CHAIN7_X0, u, nz, win, 0.006, 100.0, 0.98, CHAIN7_SIGMA, W, TW, Po, layout="TNK")
     rel = np.abs(S - Sr) / np.abs(Sr)
     k = int(np.argmax(rel))
