@@ -36,8 +36,9 @@ extern "C" {
                                 step; every rank of the step reports it and none applied the
                                 update (the nominal is the one before the step)              */
 #define MPPI_E_RETRY -6      /* mppi_np_draw_result: the draw generated fewer accepted   */
-                             /* polar attempts than it needed; nothing was written and   */
-                             /* the state is the caller's (draw on the host instead)     */
+                             /* polar attempts than it needed (or its look-back gave up);*/
+                             /* the output is incomplete and the state is the caller's   */
+                             /* (draw on the host instead)                               */
 #define MPPI_E_PATH_END -4   /* mppi_dropin_tick: the updated waypoint index reached   */
                              /* the end of the path (control.py:76-78: the reference   */
                              /* prints "[ERROR] ..." and raises IndexError)           */
@@ -452,7 +453,7 @@ int mppi_np_plan(const mppi_np_ctx *ctx, long long n, int pos, int has_gauss, in
 int mppi_np_set_jumps(mppi_np_ctx *ctx, int block_stride, int streams, const unsigned long long *polys, int words);
 /* Queue the draw of n normals from state *st on `stream` (a hipStream_t) into tgt;
  * asynchronous: mppi_np_draw_result waits for it and returns the state the
- * draw leaves (MPPI_E_RETRY: nothing written, the state untouched). */
+ * draw leaves (MPPI_E_RETRY: the output incomplete, the state untouched). */
 int mppi_np_draw(mppi_np_ctx *ctx, void *stream, const mppi_np_state *st, long long n, const mppi_np_target *tgt);
 int mppi_np_draw_result(mppi_np_ctx *ctx, mppi_np_state *st_out);
 

@@ -16,9 +16,9 @@
 //   np_gen_kernel    one workgroup per stream twists its range of blocks; a block's 624 words are each a
 //                    function of the previous block alone (the twist's in-block dependencies unrolled: up to
 //                    three tempering-free mix terms per word), so one barrier per block.
-//   np_count_kernel  accepted attempts per workgroup (2048 consecutive attempts each).
-//   np_scan_kernel   their exclusive prefix: the index of each workgroup's first pair.
-//   np_write_kernel  the accepted attempts again, each pair's place from the prefix; f with glibc's log
+//   np_write_kernel  the attempts, 2048 consecutive ones per workgroup; the index of the workgroup's first pair
+//                    by look-back over its predecessors' published counts (one pass, no separate count and
+//                    scan); each accepted pair's place from it; f with glibc's log
 //                    reproduced (np_glibc_log.h), IEEE division and square root; the transform of the drop-in
 //                    (a scaled column permutation, hostrng.monomial_transform) and the rounding to fp32, into
 //                    the engine's noise layout for this rank's samples.
@@ -76,10 +76,12 @@ constexpr int kNibW = kNibS / 8;                      // their nibbles of one ch
 constexpr int kChunks = (kDeg + 3) / 4;               // 4-bit chunks of a jump polynomial
 constexpr int kJNT = 640;                             // table jump threads: output word i per lane (< 624)
 constexpr int kJTableWGs = MPPI_NP_JUMP_WGS;                       // table jump: chunk ranges x stream groups, about
-constexpr int kAttRounds = 8;                         // attempts per thread, interleaved: attempt a0 + 256 r + t
+#ifndef MPPI_NP_ATT_ROUNDS
+#define MPPI_NP_ATT_ROUNDS 8
+#endif
+constexpr int kAttRounds = MPPI_NP_ATT_ROUNDS;                         // attempts per thread, interleaved: attempt a0 + 256 r + t
 constexpr int kAttPerWG = kNT * kAttRounds;
 constexpr size_t kJumpLds = (kSeqPad + 2 * kJHalf + kJPart) * sizeof(uint32_t);   // 107 KB
-constexpr int kScanT = 1024;
 
 __device__ __forceinline__ uint32_t mt_mix(uint32_t a, uint32_t b) {
     const uint32_t y = (a & kUp) | (b & kLo);
@@ -313,11 +315,17 @@ __global__ __launch_bounds__(kJNT) void np_jumpn_kernel(const uint32_t* __restri
 
 // stream s: blocks [1 + P s, min(1 + P (s + 1), nblk)); stream 0 also writes block 0 (the state's key array)
 __global__ __launch_bounds__(kTT) void np_gen_kernel(const uint32_t* __restrict__ key, const uint32_t* __restrict__ parts,
-                                                     uint32_t* __restrict__ words, int P, int nblk, int nparts) {
+                                                     uint32_t* __restrict__ words, int P, int nblk, int nparts,
+                                                     NpResult* res) {
     __shared__ uint32_t buf[2][kN];
     const int s = blockIdx.x, i = twist_slot(threadIdx.x);
     const int b0 = 1 + P * s, b1 = min(1 + P * (s + 1), nblk);
     if (s == 0) {
+        if (threadIdx.x == 0) {   // the draw's result, before np_write_kernel fills it
+            res->last_attempt = -1;
+            res->total = 0;
+            res->status = 0;
+        }
         if (i >= 0) {
             const uint32_t v = key[i];
             buf[0][i] = v;
@@ -356,77 +364,66 @@ __global__ __launch_bounds__(kTT) void np_gen_kernel(const uint32_t* __restrict_
 }
 
 // ------------------------------------------------------------------ the polar method
-__device__ __forceinline__ int block_sum(int v, int* s_tmp) {
-    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
-    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-    if (lane == 0) s_tmp[wave] = v;
-    __syncthreads();
-    int t = 0;
-    for (int w = 0; w < (int)(blockDim.x >> 6); ++w) t += s_tmp[w];
-    return t;
+// Workgroup look-back (single-pass prefix): workgroup w publishes its accepted-attempt count (kLookAgg) as soon
+// as its attempts are in, then its inclusive prefix (kLookIncl) once wave 0 has summed the predecessors' counts
+// back to the nearest published prefix, 64 workgroups per poll (kLookVoid: a predecessor gave up, and so does
+// this workgroup).  A word: [epoch 24 | status 2 | value 38]; the
+// draw's epoch tells this draw's words from an earlier draw's, so the array is not reset between draws.
+// Workgroups are dispatched in order, so every predecessor a workgroup waits for is resident or done.
+constexpr int kLookShift = 38;
+constexpr unsigned long long kLookVal = (1ull << kLookShift) - 1ull;
+constexpr unsigned long long kLookAgg = 1ull << kLookShift, kLookIncl = 2ull << kLookShift;
+constexpr unsigned long long kLookVoid = 3ull << kLookShift, kLookStat = 3ull << kLookShift;
+constexpr unsigned long long kLookEpoch = ~0ull << (kLookShift + 2);
+constexpr int kLookPolls = 1 << 20;   // give up (status 2, the host draws again) rather than spin for ever
+
+__device__ __forceinline__ void look_publish(unsigned long long* look, long long w, unsigned long long word) {
+    __hip_atomic_store(look + w, word, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
-// attempt a0 + 256 r + t for round r of thread t: each round's loads are one coalesced 4 KB run
-__global__ __launch_bounds__(kNT) void np_count_kernel(const uint32_t* __restrict__ words, long long base,
-                                                       long long A, int* __restrict__ counts) {
-    __shared__ int s_tmp[kNT / 64];
-    const long long a0 = (long long)blockIdx.x * kAttPerWG + threadIdx.x;
-    int c = 0;
-#pragma unroll
-    for (int r = 0; r < kAttRounds; ++r) {
-        const long long a = a0 + (long long)r * kNT;
-        if (a < A) {
-            double x1, x2, r2;
-            attempt(words, base, a, x1, x2, r2);
-            c += accepted(r2);
+// wave 0 of workgroup w > 0: the exclusive prefix of its count (every lane returns it); -1 after kLookPolls polls
+__device__ long long look_back(unsigned long long* look, long long w, unsigned long long epoch) {
+    const int lane = threadIdx.x & 63;
+    long long excl = 0, j = w - 1;
+    for (int polls = 0; polls < kLookPolls; ++polls) {
+        const long long idx = j - lane;
+        unsigned long long v = idx >= 0 ? __hip_atomic_load(look + idx, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
+                                        : (epoch | kLookIncl);
+        if ((v & kLookEpoch) != epoch) v = 0;   // an earlier draw's word: not published yet
+        const unsigned long long incl = __ballot((v & kLookStat) == kLookIncl);
+        const unsigned long long none = __ballot((v & kLookStat) == 0);
+        const unsigned long long gone = __ballot((v & kLookStat) == kLookVoid);
+        // lanes 0 .. the first inclusive prefix (or all 64) must be published
+        const unsigned long long need = incl ? (2ull << (__builtin_ctzll(incl))) - 1ull : ~0ull;
+        if (gone & need) return -1;
+        if (none & need) {
+            __builtin_amdgcn_s_sleep(1);
+            continue;
         }
+        long long part = ((1ull << lane) & need) ? (long long)(v & kLookVal) : 0;
+        for (int o = 32; o > 0; o >>= 1) part += __shfl_xor(part, o);
+        excl += part;
+        if (incl) return excl;
+        j -= 64;
     }
-    c = block_sum(c, s_tmp);
-    if (threadIdx.x == 0) counts[blockIdx.x] = c;
+    return -1;
 }
 
-// exclusive prefix of the workgroup counts (one workgroup); the total and the sufficiency check
-__global__ __launch_bounds__(kScanT) void np_scan_kernel(const int* __restrict__ counts, long long* __restrict__ offsets,
-                                                         int nwg, long long pairs, NpResult* res) {
-    __shared__ long long s_part[kScanT];
-    const int per = (nwg + kScanT - 1) / kScanT;
-    const int i0 = threadIdx.x * per, i1 = min(i0 + per, nwg);
-    long long sum = 0;
-    for (int i = i0; i < i1; ++i) sum += counts[i];
-    s_part[threadIdx.x] = sum;
-    __syncthreads();
-    for (int o = 1; o < kScanT; o <<= 1) {   // inclusive scan of the per-thread sums
-        const long long v = threadIdx.x >= (unsigned)o ? s_part[threadIdx.x - o] : 0;
-        __syncthreads();
-        s_part[threadIdx.x] += v;
-        __syncthreads();
-    }
-    long long run = s_part[threadIdx.x] - sum;
-    for (int i = i0; i < i1; ++i) {
-        offsets[i] = run;
-        run += counts[i];
-    }
-    if (threadIdx.x == kScanT - 1) {
-        res->total = s_part[kScanT - 1];
-        res->status = s_part[kScanT - 1] < pairs ? 1 : 0;
-        res->last_attempt = -1;
-    }
-}
-
-// The accepted attempts again: each pair's place from the prefix, f with glibc's log reproduced (np_glibc_log.h),
-// IEEE division and square root.  The workgroup's normals m in [m0, m1) (NumPy's (K, T, du) order) are staged in
+// The attempts, their workgroup's count published and f computed (glibc's log reproduced, np_glibc_log.h; IEEE
+// division and square root) while the look-back finds the workgroup's first pair.  The workgroup's normals m in [m0, m1) (NumPy's (K, T, du) order) are staged in
 // LDS, then written through the transform in the engine's layout row by row: for each step t, the workgroup's
 // samples are contiguous there, so consecutive threads write consecutive addresses (written straight from the
 // attempts, every lane of a wave hit its own row: one cache line per 8 bytes).
 __global__ __launch_bounds__(kNT) void np_write_kernel(const uint32_t* __restrict__ words, long long base, long long A,
-                                                       const long long* __restrict__ offsets,
-                                                       const double* __restrict__ logd, NpShape sh, long long pairs,
-                                                       long long n, int o, double cached, NpResult* res) {
+                                                       unsigned long long* __restrict__ look,
+                                                       unsigned long long epoch, const double* __restrict__ logd,
+                                                       NpShape sh, long long pairs, long long n, int o, double cached,
+                                                       NpResult* res) {
     __shared__ double s_log[NPLOG_NDATA];
     __shared__ int s_cnt[kAttRounds][kNT / 64];
+    __shared__ long long s_qw;
     __shared__ double s_z[2 * kAttPerWG];
     for (int i = threadIdx.x; i < NPLOG_NDATA; i += kNT) s_log[i] = logd[i];
-    if (res->status) return;   // uniform: every thread returns
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     const long long a0 = (long long)blockIdx.x * kAttPerWG + threadIdx.x;
     double x1[kAttRounds], x2[kAttRounds], r2[kAttRounds];
@@ -442,37 +439,66 @@ __global__ __launch_bounds__(kNT) void np_write_kernel(const uint32_t* __restric
         if (lane == 0) s_cnt[r][wave] = __popcll(bal);
     }
     __syncthreads();   // also publishes s_log
-    // pair index of this thread's attempt in round r: the workgroup's offset, all accepted attempts of the
-    // rounds before r, those of round r in earlier waves, and those of earlier lanes of this wave
-    const long long qw = offsets[blockIdx.x];
-    long long q0 = qw;
+    const long long w = blockIdx.x;
+    int agg = 0;   // the workgroup's accepted attempts
+    for (int r = 0; r < kAttRounds; ++r)
+        for (int v = 0; v < kNT / 64; ++v) agg += s_cnt[r][v];
+    if (threadIdx.x == 0) look_publish(look, w, epoch | (w == 0 ? kLookIncl : kLookAgg) | (unsigned long long)agg);
+    // local pair index of this thread's attempt in round r: all accepted attempts of the rounds before r, those of
+    // round r in earlier waves, and those of earlier lanes of this wave; f while the predecessors publish
+    int lq0 = 0, lqr[kAttRounds];
     const unsigned long long lt = (1ull << lane) - 1ull;
 #pragma unroll
     for (int r = 0; r < kAttRounds; ++r) {
         const bool acc = (mask >> r) & 1u;
         const unsigned long long bal = __ballot(acc);
-        long long q = q0 + __popcll(bal & lt);
         int before = 0, round = 0;
-        for (int w = 0; w < kNT / 64; ++w) {
-            const int cw = s_cnt[r][w];
-            before += w < wave ? cw : 0;
+        for (int v = 0; v < kNT / 64; ++v) {
+            const int cw = s_cnt[r][v];
+            before += v < wave ? cw : 0;
             round += cw;
         }
-        q += before;
-        if (acc && q < pairs) {
+        const int lq = lq0 + before + __popcll(bal & lt);
+        lqr[r] = acc ? lq : -1;
+        if (acc && lq < pairs) {
             const double f = sqrt(-2.0 * np_glibc_log(s_log, r2[r]) / r2[r]);
-            const double g1 = f * x1[r], g2 = f * x2[r];   // legacy_gauss returns f x2 and caches f x1
-            const int lq = (int)(q - qw);
-            s_z[2 * lq] = g2;       // normal o + 2 q
-            s_z[2 * lq + 1] = g1;   // o + 2 q + 1
-            if (q == pairs - 1) {
-                res->last_attempt = a0 + (long long)r * kNT;
-                res->last_fx1 = g1;
+            s_z[2 * lq] = f * x2[r];       // normal o + 2 q: legacy_gauss returns f x2
+            s_z[2 * lq + 1] = f * x1[r];   // o + 2 q + 1: and caches f x1
+        }
+        lq0 += round;
+    }
+    if (wave == 0) {   // the workgroup's first pair: the look-back
+        if (w == 0) {
+            if (lane == 0) s_qw = 0;
+        } else {
+            const long long ex = look_back(look, w, epoch);
+            if (lane == 0) {
+                if (ex >= 0) {
+                    look_publish(look, w, epoch | kLookIncl | (unsigned long long)(ex + agg));
+                } else {   // the look-back gave up: the draw is void, and the successors see it
+                    look_publish(look, w, epoch | kLookVoid);
+                    res->status = 2;
+                }
+                s_qw = ex;
             }
         }
-        q0 += round;
+        if (w == (long long)gridDim.x - 1 && lane == 0 && s_qw >= 0) {   // the last workgroup: the total
+            res->total = s_qw + agg;
+            if (s_qw + agg < pairs) res->status = 1;
+        }
     }
-    __syncthreads();
+    __syncthreads();   // s_qw and s_z
+    const long long qw = s_qw;
+    if (qw < 0) return;   // uniform
+    const long long q0 = qw + agg;
+    if (qw <= pairs - 1 && pairs - 1 < q0) {   // the last wanted pair is here: its attempt and f x1
+#pragma unroll
+        for (int r = 0; r < kAttRounds; ++r)
+            if (lqr[r] == (int)(pairs - 1 - qw)) {
+                res->last_attempt = a0 + (long long)r * kNT;
+                res->last_fx1 = s_z[2 * lqr[r] + 1];
+            }
+    }
     // normals [m0, m1) of this workgroup: pairs [qw, q0) below `pairs`; the cached Gaussian (m = 0) comes first
     const long long zb = o + 2 * qw;   // normal of s_z[0]
     const long long m0 = blockIdx.x == 0 ? 0 : zb;
@@ -481,25 +507,32 @@ __global__ __launch_bounds__(kNT) void np_write_kernel(const uint32_t* __restric
     const long long k_lo = m0 / sh.per_k, k_hi = (m1 - 1) / sh.per_k;
     const long long s_lo = max(k_lo, (long long)sh.k_offset), s_hi = min(k_hi, (long long)sh.k_offset + sh.K_local - 1);
     if (s_hi < s_lo) return;
-    const unsigned nk = (unsigned)(s_hi - s_lo + 1), du = sh.du;
-    const bool k_inner = sh.sk == 1;   // a [T][du][K] layout: samples innermost; else (t, k, d) order
-    const unsigned per_t = nk * du, total = per_t * (sh.per_k / du);
-    for (unsigned e = threadIdx.x; e < total; e += kNT) {
-        const unsigned t = e / per_t, rem = e - t * per_t;
+    const unsigned nk = (unsigned)(s_hi - s_lo + 1), du = sh.du, nt = sh.per_k / du;
+    const bool k_inner = sh.sk == 1;   // a [T][du][K] layout: samples innermost; else (k, d) order within a step
+    // element j of a step's nk du (one division each), then down the steps, G steps apart: G groups of per_t
+    // threads when a step's elements fill less than the workgroup; for a fixed step the threads' addresses are
+    // consecutive
+    const unsigned per_t = nk * du, G = max(1u, (unsigned)kNT / per_t), g0 = threadIdx.x / per_t;
+    if (g0 >= G) return;
+    for (unsigned j = threadIdx.x - g0 * per_t; j < per_t; j += G == 1 ? kNT : per_t) {
         unsigned kk, d;
         if (k_inner) {
-            d = rem / nk;
-            kk = rem - d * nk;
+            d = j / nk;
+            kk = j - d * nk;
         } else {
-            kk = rem / du;
-            d = rem - kk * du;
+            kk = j / du;
+            d = j - kk * du;
         }
         const long long k = s_lo + kk;
-        const long long m = k * sh.per_k + (long long)t * du + sh.src[d];
-        if (m < m0 || m >= m1) continue;
-        const double z = m < zb ? cached : s_z[m - zb];
-        sh.out[(long long)t * sh.st + (k - sh.k_offset) * sh.sk + (long long)d * sh.sd] =
-            (float)(z * sh.scale[d] + sh.mean[d]);
+        long long m = k * sh.per_k + sh.src[d] + (long long)g0 * du;
+        float* op = sh.out + (k - sh.k_offset) * sh.sk + (long long)d * sh.sd + (long long)g0 * sh.st;
+        const double sc = sh.scale[d], mu = sh.mean[d];
+        const long long dm = (long long)G * du, dop = (long long)G * sh.st;
+        for (unsigned t = g0; t < nt; t += G, m += dm, op += dop) {
+            if (m < m0 || m >= m1) continue;
+            const double z = m < zb ? cached : s_z[m - zb];
+            *op = (float)(z * sc + mu);
+        }
     }
 }
 
@@ -538,9 +571,9 @@ struct mppi_np_ctx {
     uint32_t* d_jumped = nullptr;
     uint32_t* d_words = nullptr;
     size_t words_cap = 0;           // words
-    int* d_counts = nullptr;
-    long long* d_offsets = nullptr;
-    size_t counts_cap = 0;          // workgroups
+    unsigned long long* d_look = nullptr;   // np_write_kernel's look-back words, one per workgroup
+    size_t look_cap = 0;            // workgroups
+    unsigned long long epoch = 0;   // the last draw's epoch (24 bits; the words are cleared when it wraps)
     NpResult* d_res = nullptr;
     mppi_np_state* d_state = nullptr;
     NpHostOut* h_out = nullptr;     // page-locked: the draw's state and status read-back
@@ -637,8 +670,7 @@ void mppi_np_ctx_destroy(mppi_np_ctx* c) {
     (void)hipFree(c->d_nibs);
     (void)hipFree(c->d_jumped);
     (void)hipFree(c->d_words);
-    (void)hipFree(c->d_counts);
-    (void)hipFree(c->d_offsets);
+    (void)hipFree(c->d_look);
     (void)hipFree(c->d_res);
     (void)hipFree(c->d_state);
     if (c->h_out) (void)hipHostFree(c->h_out);
@@ -748,15 +780,17 @@ int mppi_np_draw(mppi_np_ctx* c, void* stream, const mppi_np_state* st, long lon
         c->words_cap = words;
     }
     const long long nwg = (p.A + kAttPerWG - 1) / kAttPerWG;
-    if ((size_t)nwg > c->counts_cap) {
-        (void)hipFree(c->d_counts);
-        (void)hipFree(c->d_offsets);
-        c->d_counts = nullptr;
-        c->d_offsets = nullptr;
-        c->counts_cap = 0;
-        NP_CHECK(hipMalloc(&c->d_counts, nwg * sizeof(int)));
-        NP_CHECK(hipMalloc(&c->d_offsets, nwg * sizeof(long long)));
-        c->counts_cap = (size_t)nwg;
+    if ((size_t)nwg > c->look_cap) {
+        (void)hipFree(c->d_look);
+        c->d_look = nullptr;
+        c->look_cap = 0;
+        NP_CHECK(hipMalloc(&c->d_look, nwg * sizeof(unsigned long long)));
+        c->look_cap = (size_t)nwg;
+        c->epoch = 0;   // cleared below
+    }
+    if (++c->epoch >= (1ull << (64 - kLookShift - 2)) || c->epoch == 1) {
+        c->epoch = 1;
+        NP_CHECK(hipMemsetAsync(c->d_look, 0, c->look_cap * sizeof(unsigned long long), s));
     }
     memcpy(c->h_key, st->key, kN * sizeof(uint32_t));
     NP_CHECK(hipMemcpyAsync(c->d_key, c->h_key, kN * sizeof(uint32_t), hipMemcpyHostToDevice, s));
@@ -771,11 +805,7 @@ int mppi_np_draw(mppi_np_ctx* c, void* stream, const mppi_np_state* st, long lon
                                c->d_nbits, c->d_jumped);
     }
     hipLaunchKernelGGL(np_gen_kernel, dim3(p.streams), dim3(kTT), 0, s, c->d_key, c->d_jumped, c->d_words, p.P,
-                       (int)p.nblk, c->jparts);
-    hipLaunchKernelGGL(np_count_kernel, dim3((unsigned)nwg), dim3(kNT), 0, s, c->d_words, (long long)st->pos, p.A,
-                       c->d_counts);
-    hipLaunchKernelGGL(np_scan_kernel, dim3(1), dim3(kScanT), 0, s, c->d_counts, c->d_offsets, (int)nwg, p.pairs,
-                       c->d_res);
+                       (int)p.nblk, c->jparts, c->d_res);
     NpShape sh;
     sh.out = (float*)tgt->out_dev;
     sh.per_k = (unsigned)(tgt->T * tgt->du);
@@ -791,7 +821,8 @@ int mppi_np_draw(mppi_np_ctx* c, void* stream, const mppi_np_state* st, long lon
         sh.mean[d] = d < tgt->du ? tgt->mean[d] : 0.0;
     }
     hipLaunchKernelGGL(np_write_kernel, dim3((unsigned)nwg), dim3(kNT), 0, s, c->d_words, (long long)st->pos, p.A,
-                       c->d_offsets, c->d_log, sh, p.pairs, n, st->has_gauss ? 1 : 0, st->gauss, c->d_res);
+                       c->d_look, c->epoch << (kLookShift + 2), c->d_log, sh, p.pairs, n, st->has_gauss ? 1 : 0,
+                       st->gauss, c->d_res);
     hipLaunchKernelGGL(np_state_kernel, dim3(1), dim3(kNT), 0, s, c->d_words, (long long)st->pos, c->d_res, p.need,
                        c->d_state);
     NP_CHECK(hipGetLastError());
@@ -808,7 +839,7 @@ int mppi_np_draw_result(mppi_np_ctx* c, mppi_np_state* st_out) {
     c->pending = false;
     NP_CHECK(hipEventSynchronize(c->done));
     if (c->h_out->status != 0)
-        return fail(MPPI_E_RETRY, "mppi_np_draw: fewer accepted attempts than pairs wanted (nothing written)");
+        return fail(MPPI_E_RETRY, "mppi_np_draw: fewer accepted attempts than pairs wanted, or the look-back gave up (output incomplete)");
     *st_out = c->h_out->st;
     return MPPI_OK;
 }

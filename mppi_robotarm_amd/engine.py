@@ -477,11 +477,11 @@ class NpDeviceStream:
 
     def result(self):
         """The state the last draw leaves, as np.random.get_state()'s tuple (waits for the draw), or None when
-        the draw could not complete (nothing written)."""
+        the draw could not complete (the output incomplete: draw it on the host)."""
         st = self._st
         rc = self._lib.mppi_np_draw_result(self._ctx, C.byref(st))
         if rc == N.MPPI_E_RETRY:
-            return None   # too few accepted attempts (never seen): nothing written, np.random untouched
+            return None   # too few accepted attempts (never seen): np.random untouched
         N.check(rc, "mppi_np_draw_result")
         key = np.frombuffer(st.key, dtype=np.uint32).copy()
         return ("MT19937", key, st.pos, st.has_gauss, st.gauss)
