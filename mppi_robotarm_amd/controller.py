@@ -236,6 +236,14 @@ class MPPIControllerForPathTracking:
         self._fast = None              # what the last bound tick checked (calc_control_input's fast test)
         self.numpy_noise_on_device = numpy_noise_on_device   # noise="numpy": the same stream drawn on the device
         self._npdev = None             # its engine.NpDeviceStream (False: unavailable here)
+        self._npre = None              # (start state, spec) of the next call's draw, queued at the end of a call
+        self._np_spec = None           # (spec, plan) of this call's device draw
+        self._npre_used = 0            # calls that used the queued draw
+        self._np_plan = None           # (Sigma bytes, dtype, hostrng.monomial_plan) of the last draw
+        self._np_left = None           # the state this call's draw left np.random in
+        self._noise_alt = None         # the second noise buffer: the queued draw writes it while a step reads the other
+        self._np_stream = None         # the stream of the queued draws (concurrent with the step)
+        self._np_ev = None
 
     @property
     def host_update(self) -> bool:
@@ -283,6 +291,7 @@ class MPPIControllerForPathTracking:
                 param_gamma=self.param_gamma)
             self._engine_built_for = key
             self._noise_dev = self._engine.new_noise()
+            self._noise_alt = None
             self._partial = self._engine.new_partial()
             self._S_dev = torch.empty(K_local, dtype=torch.float64, device=self._engine.device)
             self._traj_dev = torch.empty((self.T, self.dim_x), dtype=torch.float32, device=self._engine.device)
@@ -362,6 +371,8 @@ class MPPIControllerForPathTracking:
         self._noise_ready = None
 
     def _calc_control_input(self, observed_x: np.ndarray) -> Tuple[float, np.ndarray]:
+        if self._npre is not None and self.noise_source != "numpy":
+            self._settle_predraw()                         # (the NumPy path settles it after its checks)
         f = self._fast
         if (f is not None and f[0] is self.ref_path and f[1] is self.u_prev and f[2] is self.Sigma
                 and f[3] is self.stage_cost_weight and f[4] is self.terminal_cost_weight and f[5] is self._engine
@@ -407,6 +418,8 @@ class MPPIControllerForPathTracking:
         window = self.ref_path[self.prev_waypoints_idx:(self.prev_waypoints_idx + SEARCH_IDX_LEN)]
         world, _ = self._shard()
         if not self.host_update and world == 1 and not self.visualze_sampled_trajs:
+            if isinstance(epsilon, DeviceDrawn):
+                self._queue_predraw(eng)                   # the next call's draw, beside this step
             return self._dropin_step(eng, x0, window, u)
         eng.set_step_inputs(np.asarray(x0, dtype=np.float64), window, u)
         if world > 1 and self._xmode is None:
@@ -480,7 +493,8 @@ class MPPIControllerForPathTracking:
         if self._engine is None or key != self._engine_built_for:
             return None                                    # (re)build on the general path (LinAlgError order kept)
         eng = self._engine
-        bkey = (eng, path, u, self.keep_costs, self.visualize_optimal_traj, self.seed, self.l1, self.l2)
+        bkey = (eng, path, u, self.keep_costs, self.visualize_optimal_traj, self.seed, self.l1, self.l2,
+                self._noise_dev)                           # (a NumPy-noise run swaps the noise buffers)
         if self._bound is None or any(a is not b for a, b in zip(bkey, self._bound)):
             self._x_buf = np.zeros(4)
             self._idx_buf = np.zeros(2, dtype=np.int64)
@@ -616,32 +630,77 @@ class MPPIControllerForPathTracking:
                                               self._zbuf_numpy(self.K * self.T * self.dim_u))
         return std if std is not None else self._calc_epsilon(self.Sigma, self.K, self.T, self.dim_u)
 
+    def _drop_predraw(self):
+        """Wait for a queued draw this call does not use (its buffer may be rewritten or freed next); None."""
+        if self._npre is not None:
+            self._settle_predraw()
+        return None
+
+    def _settle_predraw(self):
+        """Wait for the draw queued by the last call: (the state it started from, its spec, its buffer, the state
+        it leaves), or None.  Settled before anything may rewrite or free its buffer."""
+        pre, self._npre = self._npre, None
+        new = self._npdev.result()
+        return None if new is None else (pre[0], pre[1], pre[2], new)
+
+    def _queue_predraw(self, eng: RolloutEngine) -> None:
+        """The next call's draw, queued before this call's step from the state this call's draw left, into the
+        second noise buffer on a stream of its own: it runs beside the step and while the caller works between
+        calls.  Its stream first waits for the work already queued on the engine's stream (the last step, which
+        read that buffer).  The next call uses it only if NumPy's state is still that one and nothing the draw
+        depends on has changed (_device_reference_noise); otherwise it draws again, so the values and state are
+        NumPy's either way."""
+        spec, plan = self._np_spec
+        state = self._np_left                              # np.random's state now: this call set it last
+        eng._sync_stream()
+        if self._noise_alt is None:
+            self._noise_alt = eng.new_noise()
+        if self._np_stream is None:
+            self._np_stream = torch.cuda.Stream(device=eng.device)
+            self._np_ev = torch.cuda.Event()
+        self._np_ev.record(eng.stream)
+        self._np_stream.wait_event(self._np_ev)
+        self._npdev.draw(state, (int(self.K), int(self.T), self.dim_u), plan, self._noise_alt,
+                         self._np_stream.cuda_stream, eng.k_offset, eng.K_local,
+                         (eng.K_local * self.dim_u, self.dim_u, 1))
+        self._npre = (state, spec, self._noise_alt)
+
+    @staticmethod
+    def _same_np_state(a, b) -> bool:
+        return (a[0] == b[0] and a[2] == b[2] and a[3] == b[3] and a[4] == b[4]
+                and np.array_equal(a[1], b[1]))
+
     def _device_reference_noise(self):
         """control.py:84 on the device: the reference's own stream (np.random.multivariate_normal on the legacy
         global RNG, NumPy's values and the state it leaves) drawn straight into the engine's noise buffer
         (engine.NpDeviceStream, include/mppi_rocm.h mppi_np_*), when _calc_epsilon is the reference's and Sigma's
         transform is a scaled column permutation (run.py's 20 I).  None: not applicable here (the host path
         draws then; nothing was drawn).  A singular Sigma takes the host path too, which draws before
-        np.linalg.inv raises, as control.py:84,106 do."""
+        np.linalg.inv raises, as control.py:84,106 do.  The draw the last call queued is waited for only after
+        these checks (they run while it does), and used when it started from NumPy's current state."""
         if not self.numpy_noise_on_device or self._npdev is False:
-            return None
+            return self._drop_predraw()
         cls = MPPIControllerForPathTracking
         if "_calc_epsilon" in self.__dict__ or type(self)._calc_epsilon is not cls._calc_epsilon:
-            return None
+            return self._drop_predraw()
         sig = self.Sigma
         if not (isinstance(sig, np.ndarray) and sig.shape == (self.dim_u, self.dim_u)):
-            return None                                    # the host path prints and raises as the reference
+            return self._drop_predraw()                    # the host path prints and raises as the reference
         n = int(self.K) * int(self.T) * self.dim_u
         if n < hostrng._MIN_NORMALS or n >= 2 ** 31:
-            return None
+            return self._drop_predraw()
         state = np.random.get_state()
         if state[0] != "MT19937":
-            return None
-        plan = hostrng.monomial_plan(np.full((self.dim_u), 0.0), sig)
+            return self._drop_predraw()
+        sb = sig.tobytes()
+        if self._np_plan is None or self._np_plan[0] != sb or self._np_plan[1] != sig.dtype:
+            self._np_plan = (sb, sig.dtype, hostrng.monomial_plan(np.full((self.dim_u), 0.0), sig))
+        plan = self._np_plan[2]
         if plan is None:
-            return None
+            return self._drop_predraw()
         key = self._engine_key()
         if key != self._engine_built_for:
+            self._drop_predraw()                           # the engine and its buffer may be rebuilt below
             try:
                 np.linalg.inv(sig)
             except np.linalg.LinAlgError:
@@ -657,13 +716,25 @@ class MPPIControllerForPathTracking:
         if not plan[3]:
             import warnings
             warnings.warn("covariance is not symmetric positive-semidefinite.", RuntimeWarning)   # NumPy's
-        eng._sync_stream()
-        self._npdev.draw(state, (int(self.K), int(self.T), self.dim_u), plan, self._noise_dev, eng.stream.cuda_stream,
-                         eng.k_offset, eng.K_local, (eng.K_local * self.dim_u, self.dim_u, 1))
-        new = self._npdev.result()
+        spec = (int(self.K), int(self.T), self.dim_u, eng, eng.k_offset, eng.K_local, sb)
+        self._np_spec = (spec, plan)
+        new = None
+        if self._npre is not None:
+            pre = self._settle_predraw()
+            if (pre is not None and pre[1] == spec and pre[2] is self._noise_alt
+                    and self._same_np_state(pre[0], state)):
+                new = pre[3]                               # drawn beside the last step: NumPy's values
+                self._noise_dev, self._noise_alt = self._noise_alt, self._noise_dev
+                self._npre_used += 1
+        if new is None:
+            eng._sync_stream()
+            self._npdev.draw(state, (int(self.K), int(self.T), self.dim_u), plan, self._noise_dev,
+                             eng.stream.cuda_stream, eng.k_offset, eng.K_local, (eng.K_local * self.dim_u, self.dim_u, 1))
+            new = self._npdev.result()
         if new is None:
             return None
         np.random.set_state(new)
+        self._np_left = new
         return DeviceDrawn(float(np.sum(new[1][:16], dtype=np.float64)) + new[2])
 
     def _zbuf_numpy(self, n: int) -> np.ndarray:
@@ -715,6 +786,8 @@ class MPPIControllerForPathTracking:
         return out
 
     def close(self):
+        if self._npre is not None:
+            self._settle_predraw()                         # its buffer outlives it
         if self._engine is not None:
             self._engine.close()
             self._engine = None

@@ -102,7 +102,7 @@ def test_rank_slices_are_slices_of_the_whole_draw(nd):
         assert _same_state(st_part, st_full)   # every rank leaves the same state
 
 
-def _loop(device_draw: bool, ticks=4, K=4096, T=32):
+def _loop(device_draw: bool, ticks=4, K=4096, T=32, between=None):
     from mppi_robotarm_amd.controller import MPPIControllerForPathTracking
     from mppi_robotarm_amd.params import X0_RUNPY, runpy_config
     from conftest import load_paths
@@ -113,20 +113,45 @@ def _loop(device_draw: bool, ticks=4, K=4096, T=32):
     np.random.seed(21)
     x, out = X0_RUNPY.copy(), []
     for i in range(ticks):
+        if between is not None:
+            between(i, c)
         u0, u_seq, opt, _ = c.calc_control_input(x)
         out.append((u_seq.copy(), opt.copy()))
         x = x + 0.002 * (i + 1)
     used = c._npdev
+    hits = c._npre_used
     c.close()
-    return out, np.random.get_state(), used
+    return out, np.random.get_state(), used, hits
 
 
 def test_controller_device_draw_equals_host_draw():
     """The drop-in with its default noise: the device draw gives the host draw's steps bit for bit and leaves
     np.random where the host draw (NumPy's values and state, tests/test_hostrng.py) leaves it."""
-    a, st_a, used = _loop(True)
-    b, st_b, _ = _loop(False)
+    a, st_a, used, hits = _loop(True)
+    b, st_b, _, _ = _loop(False)
     assert used, "the controller did not take the device draw"
+    assert hits == 3, "calls 2-4 use the draw queued by the call before"
+    for (ua, oa), (ub, ob) in zip(a, b):
+        np.testing.assert_array_equal(ua, ub)
+        np.testing.assert_array_equal(oa, ob)
+    assert _same_state(st_a, st_b)
+
+
+def test_queued_draw_is_dropped_when_numpy_state_or_sigma_changes():
+    """The draw queued for the next call is used only when np.random is still where the last call left it and
+    Sigma's transform is unchanged: the caller's own draws, a reseed and a new Sigma between calls give the host
+    draw's steps and state bit for bit."""
+    def between(i, c):
+        if i == 1:
+            np.random.rand(3)                               # the caller consumes the stream
+        elif i == 3:
+            np.random.seed(7)
+        elif i == 5:
+            c.Sigma = np.eye(2) * 10.0                      # another plan
+    a, st_a, used, hits = _loop(True, ticks=7, between=between)
+    b, st_b, _, _ = _loop(False, ticks=7, between=between)
+    assert used
+    assert hits == 3, "used at calls 3, 5 and 7 only"
     for (ua, oa), (ub, ob) in zip(a, b):
         np.testing.assert_array_equal(ua, ub)
         np.testing.assert_array_equal(oa, ob)
