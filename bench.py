@@ -608,7 +608,8 @@ def main():
                 "visualze_sampled_trajs=True, i.e. also the (K, T, 4) fp64 sampled_traj_list (134 MB at K = "
                 "65536) re-rolled on the device and read back every call; numpy_noise: back to back with the "
                 "drop-in's default noise='numpy', the reference's own np.random.multivariate_normal stream "
-                "(NumPy's values and RNG state) drawn on the device every call (mppi_np_*). "
+                "(NumPy's values and RNG state) drawn on the device every call (mppi_np_*): each call queues the "
+                "next call's draw beside its step, used when np.random is still where the call left it. "
                 "ms_per_step is the device-resident loop")
         if world == 1 and c5:
             out["control_step_latency_back_to_back_ms"] = chain_dropin_latency(K, T, local_rank, args.precision)
@@ -623,7 +624,7 @@ def main():
                 "the launch (each call then also waits for the previous draw). 40 calls after 10 uncounted. "
                 "numpy_noise: the same with the drop-in's default noise='numpy', the reference's own "
                 "np.random.multivariate_normal stream (NumPy's values and RNG state) drawn on the device every "
-                "call (10 calls after 3). ms_per_step is the device-resident loop")
+                "call, the next call's beside the step (10 calls after 3). ms_per_step is the device-resident loop")
         if world == 1 and args.cpu_seconds > 0:
             progress("CPU baseline")
             out["cpu_baseline"] = (cpu_baseline_c5(args, window, x0, u, K, T) if c5

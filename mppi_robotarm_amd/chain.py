@@ -406,10 +406,17 @@ class ChainMPPIController:
         self.last_S = None
         self.numpy_noise_on_device = numpy_noise_on_device   # noise="numpy": the same stream drawn on the device
         self._npdev = None             # its engine.NpDeviceStream (False: unavailable here)
+        self._npre = None              # (start state, spec, buffer) of the next call's draw, queued beside a step
+        self._np_spec = None           # (spec, plan) of this call's device draw
+        self._np_left = None           # the state it left np.random in
+        self._np_plan = None           # (Sigma bytes, dtype, hostrng.monomial_plan) of the last draw
+        self._npre_used = 0            # calls that used the queued draw
+        self._np_stream = None         # the stream of the queued draws
+        self._np_ev = None
 
     # the per-engine fields: the active engine's live here, the others' are parked in _slots
-    _SLOT = ("_engine", "_engine_built_for", "_xmode", "_noise_ready", "_noise_dev", "_partial", "_S_dev",
-             "_gathered")
+    _SLOT = ("_engine", "_engine_built_for", "_xmode", "_noise_ready", "_noise_dev", "_noise_alt", "_partial",
+             "_S_dev", "_gathered")
 
     def _activate(self, precision: str) -> None:
         """Make the engine of `precision` (built on first use) the one the fields above refer to."""
@@ -452,6 +459,7 @@ class ChainMPPIController:
                                        self.chain, K_total=self.K, k_offset=k_offset, device=device,
                                        precision=self._active, param_gamma=self.param_gamma)
             self._noise_dev = self._engine.new_noise()
+            self._noise_alt = None                         # the queued draw's buffer, made on first use
             self._partial = self._engine.new_partial()
             self._S_dev = torch.empty(K_local, dtype=torch.float64, device=self._engine.device)
             if world > 1:
@@ -509,30 +517,68 @@ class ChainMPPIController:
         std = hostrng.multivariate_normal_std(np.zeros(self.dim_u), sigma, (self.K, self.T), self._zbuf.numpy())
         return std if std is not None else self._calc_epsilon(sigma, self.K, self.T, self.dim_u)
 
+    def _drop_predraw(self):
+        """Wait for a queued draw this call does not use (its buffer may be rewritten or freed next); None."""
+        if self._npre is not None:
+            self._settle_predraw()
+        return None
+
+    def _settle_predraw(self):
+        """As MPPIControllerForPathTracking._settle_predraw."""
+        pre, self._npre = self._npre, None
+        new = self._npdev.result()
+        return None if new is None else (pre[0], pre[1], pre[2], new)
+
+    def _queue_predraw(self, eng: ChainEngine) -> None:
+        """As MPPIControllerForPathTracking._queue_predraw: the next call's draw from the state this call's draw
+        left, into this engine's second noise buffer on a stream of its own, beside this call's step (its stream
+        first waits for the work already queued on the engine's, the last reader of that buffer).  The next call
+        uses it when np.random is still in that state and it runs on the same engine (precision="auto" may
+        switch engines: then it draws again)."""
+        spec, plan = self._np_spec
+        state = self._np_left
+        eng._sync_stream()
+        if self._noise_alt is None:
+            self._noise_alt = eng.new_noise()
+        if self._np_stream is None:
+            self._np_stream = torch.cuda.Stream(device=eng.device)
+            self._np_ev = torch.cuda.Event()
+        self._np_ev.record(eng.stream)
+        self._np_stream.wait_event(self._np_ev)
+        kl = eng.K_local
+        self._npdev.draw(state, (int(self.K), int(self.T), self.dim_u), plan, self._noise_alt,
+                         self._np_stream.cuda_stream, eng.k_offset, kl, (self.dim_u * kl, self.dim_u, 1))
+        self._npre = (state, spec, self._noise_alt)
+
     def _device_reference_noise(self, prec: str):
         """control.py:84 on the device, as MPPIControllerForPathTracking._device_reference_noise: NumPy's stream
         (values and RNG state) drawn into the noise buffer of the `prec` engine, the one the step runs on first
-        (a step re-run in the other precision copies it over).  None: the host path draws."""
-        from .controller import DeviceDrawn
+        (a step re-run in the other precision copies it over), or taken from the draw the last call queued when
+        it started from NumPy's current state on this engine.  None: the host path draws."""
+        from .controller import DeviceDrawn, MPPIControllerForPathTracking as _C
         if not self.numpy_noise_on_device or self._npdev is False:
-            return None
+            return self._drop_predraw()
         if "_calc_epsilon" in self.__dict__ or type(self)._calc_epsilon is not ChainMPPIController._calc_epsilon:
-            return None
+            return self._drop_predraw()
         sig = self.Sigma
         if not (isinstance(sig, np.ndarray) and sig.shape == (self.dim_u, self.dim_u)):
-            return None
+            return self._drop_predraw()
         n = int(self.K) * int(self.T) * self.dim_u
         if n < hostrng._MIN_NORMALS or n >= 2 ** 31:
-            return None
+            return self._drop_predraw()
         state = np.random.get_state()
         if state[0] != "MT19937":
-            return None
-        plan = hostrng.monomial_plan(np.zeros(self.dim_u), sig)
+            return self._drop_predraw()
+        sb = sig.tobytes()
+        if self._np_plan is None or self._np_plan[0] != sb or self._np_plan[1] != sig.dtype:
+            self._np_plan = (sb, sig.dtype, hostrng.monomial_plan(np.zeros(self.dim_u), sig))
+        plan = self._np_plan[2]
         if plan is None:
-            return None
+            return self._drop_predraw()
         self._activate(prec)
         key = self._engine_key()
         if key != self._engine_built_for:
+            self._drop_predraw()                           # the engine and its buffers may be rebuilt below
             try:
                 np.linalg.inv(sig)
             except np.linalg.LinAlgError:
@@ -548,14 +594,26 @@ class ChainMPPIController:
         if not plan[3]:
             import warnings
             warnings.warn("covariance is not symmetric positive-semidefinite.", RuntimeWarning)   # NumPy's
-        eng._sync_stream()
         kl = eng.K_local
-        self._npdev.draw(state, (int(self.K), int(self.T), self.dim_u), plan, self._noise_dev, eng.stream.cuda_stream,
-                         eng.k_offset, kl, (self.dim_u * kl, self.dim_u, 1))   # [T][K_local][n]
-        new = self._npdev.result()
+        spec = (int(self.K), int(self.T), self.dim_u, eng, eng.k_offset, kl, sb)
+        self._np_spec = (spec, plan)
+        new = None
+        if self._npre is not None:
+            pre = self._settle_predraw()
+            if (pre is not None and pre[1] == spec and pre[2] is self._noise_alt
+                    and _C._same_np_state(pre[0], state)):
+                new = pre[3]                               # drawn beside the last step: NumPy's values
+                self._noise_dev, self._noise_alt = self._noise_alt, self._noise_dev
+                self._npre_used += 1
+        if new is None:
+            eng._sync_stream()
+            self._npdev.draw(state, (int(self.K), int(self.T), self.dim_u), plan, self._noise_dev,
+                             eng.stream.cuda_stream, eng.k_offset, kl, (self.dim_u * kl, self.dim_u, 1))  # [T][K_local][n]
+            new = self._npdev.result()
         if new is None:
             return None
         np.random.set_state(new)
+        self._np_left = new
         d = DeviceDrawn(float(np.sum(new[1][:16], dtype=np.float64)) + new[2])
         d.buf = self._noise_dev
         return d
@@ -568,6 +626,8 @@ class ChainMPPIController:
         return hostrng.multivariate_normal(np.zeros(size_dim_u), sigma, (size_sample, size_time_step))
 
     def calc_control_input(self, observed_x):
+        if self._npre is not None and self.noise_source != "numpy":
+            self._settle_predraw()                         # (the NumPy path settles it after its checks)
         u = self.u_prev
         x0 = np.asarray(observed_x, dtype=np.float64)
         self._get_nearest_waypoint(*self._effector(x0[:self.dim_u]), update_prev_idx=True)
@@ -580,6 +640,8 @@ class ChainMPPIController:
             epsilon = self._device_reference_noise(prec)
             if epsilon is None:
                 epsilon = self._reference_noise()
+            elif self.T >= 5 and not self.visualze_sampled_trajs and self.process_group is None:
+                self._queue_predraw(self._engine)          # the next call's draw, beside this step
         else:
             epsilon = None
         step = self._step_count
@@ -710,6 +772,8 @@ class ChainMPPIController:
         self._xmode = None
 
     def close(self):
+        if self._npre is not None:
+            self._settle_predraw()                         # its buffer outlives it
         if self._npdev:
             self._npdev.close()
         self._npdev = None

@@ -170,9 +170,9 @@ def _chain_loop(device_draw: bool, lam: float, ticks=3, K=4096, T=16):
         u0, u_seq, opt, _ = c.calc_control_input(CHAIN7_X0)
         out.append((u_seq.copy(), opt.copy()))
         precs.append(c.last_precision)
-    used = c._npdev
+    used, hits = c._npdev, c._npre_used
     c.close()
-    return out, np.random.get_state(), used, precs
+    return out, np.random.get_state(), used, precs, hits
 
 
 @pytest.mark.parametrize("lam", [100.0, 3.0e5])
@@ -180,9 +180,10 @@ def test_chain_controller_device_draw_equals_host_draw(lam):
     """The 7-link drop-in's default noise on the device: the host draw's steps bit for bit; at lambda = 3e5 the
     weights spread and precision="auto" re-runs each step in fp64 on the other engine (the draw copied into its
     noise buffer)."""
-    a, st_a, used, precs = _chain_loop(True, lam)
-    b, st_b, _, precs_b = _chain_loop(False, lam)
+    a, st_a, used, precs, hits = _chain_loop(True, lam)
+    b, st_b, _, precs_b, _ = _chain_loop(False, lam)
     assert used, "the chain controller did not take the device draw"
+    assert hits >= 1, "a call used the draw queued beside the step before (same engine: same precision)"
     assert precs == precs_b
     assert lam < 1e4 or "f64" in precs
     for (ua, oa), (ub, ob) in zip(a, b):
