@@ -414,7 +414,11 @@ __device__ long long look_back(unsigned long long* look, long long w, unsigned l
 // LDS, then written through the transform in the engine's layout row by row: for each step t, the workgroup's
 // samples are contiguous there, so consecutive threads write consecutive addresses (written straight from the
 // attempts, every lane of a wave hit its own row: one cache line per 8 bytes).
-__global__ __launch_bounds__(kNT) void np_write_kernel(const uint32_t* __restrict__ words, long long base, long long A,
+#ifndef MPPI_NP_WRITE_WAVES
+#define MPPI_NP_WRITE_WAVES 4
+#endif
+// at most 128 VGPRs: four waves per SIMD (130 gave three)
+__global__ __launch_bounds__(kNT) __attribute__((amdgpu_waves_per_eu(MPPI_NP_WRITE_WAVES))) void np_write_kernel(const uint32_t* __restrict__ words, long long base, long long A,
                                                        unsigned long long* __restrict__ look,
                                                        unsigned long long epoch, const double* __restrict__ logd,
                                                        NpShape sh, long long pairs, long long n, int o, double cached,
@@ -426,14 +430,14 @@ __global__ __launch_bounds__(kNT) void np_write_kernel(const uint32_t* __restric
     for (int i = threadIdx.x; i < NPLOG_NDATA; i += kNT) s_log[i] = logd[i];
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     const long long a0 = (long long)blockIdx.x * kAttPerWG + threadIdx.x;
-    double x1[kAttRounds], x2[kAttRounds], r2[kAttRounds];
+    double x1[kAttRounds], x2[kAttRounds];   // r2 recomputed where f needs it (the same rounded operations)
     unsigned mask = 0;
 #pragma unroll
     for (int r = 0; r < kAttRounds; ++r) {
         const long long a = a0 + (long long)r * kNT;
-        r2[r] = 2.0;
-        if (a < A) attempt(words, base, a, x1[r], x2[r], r2[r]);
-        const bool acc = accepted(r2[r]);
+        double r2 = 2.0;
+        if (a < A) attempt(words, base, a, x1[r], x2[r], r2);
+        const bool acc = accepted(r2);
         mask |= (unsigned)acc << r;
         const unsigned long long bal = __ballot(acc);
         if (lane == 0) s_cnt[r][wave] = __popcll(bal);
@@ -446,7 +450,7 @@ __global__ __launch_bounds__(kNT) void np_write_kernel(const uint32_t* __restric
     if (threadIdx.x == 0) look_publish(look, w, epoch | (w == 0 ? kLookIncl : kLookAgg) | (unsigned long long)agg);
     // local pair index of this thread's attempt in round r: all accepted attempts of the rounds before r, those of
     // round r in earlier waves, and those of earlier lanes of this wave; f while the predecessors publish
-    int lq0 = 0, lqr[kAttRounds];
+    int lq0 = 0;
     const unsigned long long lt = (1ull << lane) - 1ull;
 #pragma unroll
     for (int r = 0; r < kAttRounds; ++r) {
@@ -459,9 +463,9 @@ __global__ __launch_bounds__(kNT) void np_write_kernel(const uint32_t* __restric
             round += cw;
         }
         const int lq = lq0 + before + __popcll(bal & lt);
-        lqr[r] = acc ? lq : -1;
         if (acc && lq < pairs) {
-            const double f = sqrt(-2.0 * np_glibc_log(s_log, r2[r]) / r2[r]);
+            const double r2 = x1[r] * x1[r] + x2[r] * x2[r];   // as attempt()
+            const double f = sqrt(-2.0 * np_glibc_log(s_log, r2) / r2);
             s_z[2 * lq] = f * x2[r];       // normal o + 2 q: legacy_gauss returns f x2
             s_z[2 * lq + 1] = f * x1[r];   // o + 2 q + 1: and caches f x1
         }
@@ -491,13 +495,24 @@ __global__ __launch_bounds__(kNT) void np_write_kernel(const uint32_t* __restric
     const long long qw = s_qw;
     if (qw < 0) return;   // uniform
     const long long q0 = qw + agg;
-    if (qw <= pairs - 1 && pairs - 1 < q0) {   // the last wanted pair is here: its attempt and f x1
-#pragma unroll
-        for (int r = 0; r < kAttRounds; ++r)
-            if (lqr[r] == (int)(pairs - 1 - qw)) {
-                res->last_attempt = a0 + (long long)r * kNT;
-                res->last_fx1 = s_z[2 * lqr[r] + 1];
+    if (qw <= pairs - 1 && pairs - 1 < q0) {   // the last wanted pair is here (uniform): its attempt and f x1
+        const int want = (int)(pairs - 1 - qw);
+        int l0 = 0;
+        for (int r = 0; r < kAttRounds; ++r) {   // the local indices again, as above
+            const bool acc = (mask >> r) & 1u;
+            const unsigned long long bal = __ballot(acc);
+            int before = 0, round = 0;
+            for (int v = 0; v < kNT / 64; ++v) {
+                const int cw = s_cnt[r][v];
+                before += v < wave ? cw : 0;
+                round += cw;
             }
+            if (acc && l0 + before + __popcll(bal & lt) == want) {
+                res->last_attempt = a0 + (long long)r * kNT;
+                res->last_fx1 = s_z[2 * want + 1];
+            }
+            l0 += round;
+        }
     }
     // normals [m0, m1) of this workgroup: pairs [qw, q0) below `pairs`; the cached Gaussian (m = 0) comes first
     const long long zb = o + 2 * qw;   // normal of s_z[0]
