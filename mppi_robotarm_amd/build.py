@@ -55,7 +55,9 @@ def build_native(force: bool = False, extra_flags: list[str] | None = None, out:
 
 def build_host_rng(force: bool = False) -> str:
     """csrc/np_legacy_gauss.c -> _lib/libmppi_hostrng.so: host C, no contraction, so its values equal NumPy's."""
-    if not force and os.path.exists(HOST_RNG_OUT) and os.path.getmtime(HOST_RNG_OUT) >= os.path.getmtime(HOST_RNG_SRC):
+    deps = (HOST_RNG_SRC, os.path.join(CSRC, "np_glibc_log.h"))
+    if not force and os.path.exists(HOST_RNG_OUT) and all(os.path.getmtime(HOST_RNG_OUT) >= os.path.getmtime(d)
+                                                          for d in deps):
         return HOST_RNG_OUT
     os.makedirs(os.path.dirname(HOST_RNG_OUT), exist_ok=True)
     subprocess.run(["gcc", "-O3", "-fPIC", "-shared", "-ffp-contract=off", "-fno-fast-math", "-pthread", "-o",
