@@ -295,6 +295,20 @@ def numpy_noise_latency(K, T, device, calls=20, warm=5):
     return float(np.median(ts[warm:])) * 1e3
 
 
+def numpy_noise_closed_loop(K, T, device, ticks=100, warm=30):
+    """The drop-in with its default noise="numpy" in run.py's closed loop (mppi_robotarm_amd.harness, the plant
+    stepped on the host between ticks): median calc_control_input wall time (ms) after a first loop of `warm`
+    ticks; the next call's draw runs beside the step and under the plant step."""
+    from mppi_robotarm_amd.harness import run_closed_loop
+    path = np.load(os.path.join(ROOT, "tests", "golden", "paths.npz"))["xydq_circle"][:, :4]
+    np.random.seed(0)
+    for n in (warm, ticks):
+        rec = run_closed_loop(path, ticks=n, number_of_samples_K=K, horizon_step_T=T, noise="numpy",
+                              verbose=False, visualze_sampled_trajs=False, device=device)
+        rec["controller"].close()
+    return float(np.median(rec["latency_s"][3:] * 1e3))
+
+
 def chain_dropin_latency(K, T, device, precision="f32", calls=40, warm=10, noise="device"):
     """The chain drop-in's calc_control_input back to back (ms, median) from the config-5 start state, the
     start nominal re-staged before each call (the bench loop's reset: no plant between calls).  noise="numpy":
@@ -597,6 +611,7 @@ def main():
             out["control_step_latency_sampled_trajs_ms"] = sampled_latency(K, T, local_rank)
             progress("NumPy-noise leg")
             out["control_step_latency_numpy_noise_ms"] = numpy_noise_latency(K, T, local_rank)
+            out["control_step_latency_numpy_noise_closed_loop_ms"] = numpy_noise_closed_loop(K, T, local_rank)
             out["control_step_latency_def"] = (
                 "median wall time of MPPIControllerForPathTracking.calc_control_input (drop-in, noise='device') "
                 "in run.py's closed loop at this K, T: stage inputs, one fused launch (rollouts, soft-min, "
@@ -609,7 +624,8 @@ def main():
                 "65536) re-rolled on the device and read back every call; numpy_noise: back to back with the "
                 "drop-in's default noise='numpy', the reference's own np.random.multivariate_normal stream "
                 "(NumPy's values and RNG state) drawn on the device every call (mppi_np_*): each call queues the "
-                "next call's draw beside its step, used when np.random is still where the call left it. "
+                "next call's draw beside its step, used when np.random is still where the call left it; "
+                "numpy_noise_closed_loop: the same in run.py's closed loop (100 ticks after 30). "
                 "ms_per_step is the device-resident loop")
         if world == 1 and c5:
             out["control_step_latency_back_to_back_ms"] = chain_dropin_latency(K, T, local_rank, args.precision)
