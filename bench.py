@@ -254,15 +254,19 @@ def dropin_latency(K, T, device, ticks=200, warm=100):
     return float(np.median(lat)), float(np.percentile(lat, 90)), float(np.median(b2b))
 
 
-def sampled_latency(K, T, device, calls=20, warm=5):
+def sampled_latency(K, T, device, calls=20, warm=5, noise="device"):
     """calc_control_input back to back (ms, median) with run.py's visualze_sampled_trajs=True: the K x T
-    re-roll of control.py:135-145 on the device and its fp64 sampled_traj_list read back every call."""
+    re-roll of control.py:135-145 on the device and its fp64 sampled_traj_list read back every call (fp32 DMA,
+    widened on host threads: controller.SampledReadback).  noise="numpy": run.py's exact flags together (the
+    drop-in's default noise, the reference's np.random stream drawn on the device, the next call's draw queued
+    behind the re-roll).  Returns (median ms, detail dict)."""
     from mppi_robotarm_amd.controller import MPPIControllerForPathTracking
     from mppi_robotarm_amd.params import runpy_config
     path = np.load(os.path.join(ROOT, "tests", "golden", "paths.npz"))["xydq_circle"][:, :4]
     kw = runpy_config()
     kw.update(number_of_samples_K=K, horizon_step_T=T, visualze_sampled_trajs=True)
-    c = MPPIControllerForPathTracking(ref_path=path, noise="device", seed=0, verbose=False, device=device, **kw)
+    c = MPPIControllerForPathTracking(ref_path=path, noise=noise, seed=0, verbose=False, device=device, **kw)
+    np.random.seed(0)
     ts = []
     for i in range(warm + calls):
         c.prev_waypoints_idx = 0
@@ -270,8 +274,27 @@ def sampled_latency(K, T, device, calls=20, warm=5):
         out = c.calc_control_input(X0_RUNPY)
         ts.append(time.perf_counter() - t0)
         del out
+    detail = {"calls": calls, "warm": warm}
+    if noise == "numpy":
+        detail["queued_draws_used"] = c._npre_used
+        detail["device_draws"] = c._npdev.draws if c._npdev else 0
+        detail["device_draw_retries"] = c._npdev.retries if c._npdev else None
+    rb = c._sampled_pool._rb
+    if rb is not None:
+        # the read-back alone on a tensor of the same shape: the floor under the sampled leg
+        tr = torch.randn((K, T, 4), device=f"cuda:{device}", dtype=torch.float32)
+        dst = np.empty((K, T, 4))
+        rt = []
+        for i in range(12):
+            torch.cuda.synchronize()
+            t0 = time.perf_counter()
+            rb.run(tr, dst)
+            rt.append(time.perf_counter() - t0)
+        detail["readback_only_ms"] = float(np.median(rt[2:])) * 1e3
+        detail["readback_workers"] = rb.workers
+        detail["readback_bytes_over_link"] = int(tr.numel() * 4)
     c.close()
-    return float(np.median(ts[warm:])) * 1e3
+    return float(np.median(ts[warm:])) * 1e3, detail
 
 
 def numpy_noise_latency(K, T, device, calls=20, warm=5):
@@ -291,8 +314,11 @@ def numpy_noise_latency(K, T, device, calls=20, warm=5):
         t0 = time.perf_counter()
         c.calc_control_input(X0_RUNPY)
         ts.append(time.perf_counter() - t0)
+    detail = {"calls": calls, "warm": warm, "queued_draws_used": c._npre_used,
+              "device_draws": c._npdev.draws if c._npdev else 0,
+              "device_draw_retries": c._npdev.retries if c._npdev else None}
     c.close()
-    return float(np.median(ts[warm:])) * 1e3
+    return float(np.median(ts[warm:])) * 1e3, detail
 
 
 def numpy_noise_closed_loop(K, T, device, ticks=100, warm=30):
@@ -608,9 +634,14 @@ def main():
             out["control_step_latency_p90_ms"] = p90
             out["control_step_latency_back_to_back_ms"] = b2b
             progress("sampled-trajectories leg")
-            out["control_step_latency_sampled_trajs_ms"] = sampled_latency(K, T, local_rank)
+            out["control_step_latency_sampled_trajs_ms"], out["sampled_trajs_detail"] = sampled_latency(
+                K, T, local_rank)
+            progress("run.py-flags leg (NumPy noise + sampled trajectories)")
+            out["control_step_latency_runpy_flags_ms"], out["runpy_flags_detail"] = sampled_latency(
+                K, T, local_rank, noise="numpy")
             progress("NumPy-noise leg")
-            out["control_step_latency_numpy_noise_ms"] = numpy_noise_latency(K, T, local_rank)
+            out["control_step_latency_numpy_noise_ms"], out["numpy_noise_detail"] = numpy_noise_latency(
+                K, T, local_rank)
             out["control_step_latency_numpy_noise_closed_loop_ms"] = numpy_noise_closed_loop(K, T, local_rank)
             out["control_step_latency_def"] = (
                 "median wall time of MPPIControllerForPathTracking.calc_control_input (drop-in, noise='device') "
@@ -621,7 +652,9 @@ def main():
                 "also waits for the previous draw). Steady state: 200 ticks each, after 100 uncounted. These "
                 "two run with visualze_sampled_trajs=False; sampled_trajs: back to back with run.py's own "
                 "visualze_sampled_trajs=True, i.e. also the (K, T, 4) fp64 sampled_traj_list (134 MB at K = "
-                "65536) re-rolled on the device and read back every call; numpy_noise: back to back with the "
+                "65536) re-rolled on the device, its fp32 states DMA'd in chunks and widened to fp64 by host threads "
+                "every call (sampled_trajs_detail.readback_only_ms: that read-back alone); runpy_flags: run.py's "
+                "exact flags together, noise='numpy' (the default) and visualze_sampled_trajs=True; numpy_noise: back to back with the "
                 "drop-in's default noise='numpy', the reference's own np.random.multivariate_normal stream "
                 "(NumPy's values and RNG state) drawn on the device every call (mppi_np_*): each call queues the "
                 "next call's draw beside its step, used when np.random is still where the call left it; "

@@ -167,6 +167,22 @@ int mppi_get_nominal(mppi_ctx *ctx, double *u_host /* [T][2] */);
 int mppi_rollout_traj(mppi_ctx *ctx, const double *base_u, const float *noise_dev, int K,
                       float *out_dev);
 
+/* sampled_traj_list's host read-back (control.py:135-145 returns fp64; the
+ * re-roll writes fp32).  fp32 -> fp64 is exact, so the widening runs on the
+ * host: n fp32 values at src_dev are copied chunk by chunk (chunk_floats each,
+ * the last three a half, a quarter and an eighth of it) after the work queued
+ * on `stream` (the kernel that wrote them), alternating over copy_streams
+ * streams of the object's own (0: on `stream` itself), into a page-locked ring
+ * of `slots` chunks, and `workers` host threads widen each landed chunk into
+ * dst_host (n fp64, any host memory) while the next chunks are in flight.
+ * Half the bytes of a device-side widening cross the host link, and the
+ * values are the same.  mppi_readback_run returns when dst_host is written. */
+typedef struct mppi_readback mppi_readback;
+int mppi_readback_create(int device, int workers, int slots, long long chunk_floats, int copy_streams,
+                         mppi_readback **out);
+void mppi_readback_destroy(mppi_readback *rb);
+int mppi_readback_run(mppi_readback *rb, void *stream, const float *src_dev, double *dst_host, long long n);
+
 /* The optimal trajectory of control.py:129-134 (the updated controls u_new
  * before the shift of :148-149, off-by-one u_new[t-1]) after a launch with
  * MPPI_FLAG_FUSED_UPDATE: fp32 states out_dev[T][4] of one re-roll from x0,

@@ -47,7 +47,7 @@ EXPORTS = (
     "mppi_chain_wait_outputs", "mppi_chain_optimal_traj_host", "mppi_chain_last_eta",
     "mppi_config_init", "mppi_chain_config_init",
     "mppi_np_ctx_create", "mppi_np_ctx_destroy", "mppi_np_plan", "mppi_np_set_jumps", "mppi_np_draw",
-    "mppi_np_draw_result",
+    "mppi_np_draw_result", "mppi_readback_create", "mppi_readback_destroy", "mppi_readback_run",
 )
 
 
@@ -195,6 +195,9 @@ def open_library(path: str):
         "mppi_np_draw": ([vp, vp, C.POINTER(NpStateC), C.c_longlong, C.POINTER(NpTargetC)], C.c_int),
         "mppi_np_draw_result": ([vp, C.POINTER(NpStateC)], C.c_int),
         "mppi_chain_config_init": ([C.POINTER(ChainConfigC)], None),
+        "mppi_readback_create": ([C.c_int, C.c_int, C.c_int, C.c_longlong, C.c_int, C.POINTER(vp)], C.c_int),
+        "mppi_readback_destroy": ([vp], None),
+        "mppi_readback_run": ([vp, vp, vp, vp, C.c_longlong], C.c_int),
     }
     for name, (args, res) in sig.items():
         if not hasattr(L, name):   # an older diagnostic build (tools/ab.py); load() checks the product's exports

@@ -1,8 +1,9 @@
 """In-tree build of the HIP library for gfx950 (``hipcc`` cross-compiles without a GPU).
 
-Three translation units — ``csrc/mppi_rocm.hip`` (the reference's 2-link arm),
-``csrc/mppi_chain.hip`` (the n-link chain of config 5) and
-``csrc/mppi_npgauss.hip`` (the reference's NumPy noise stream on the device) —
+Four translation units — ``csrc/mppi_rocm.hip`` (the reference's 2-link arm),
+``csrc/mppi_chain.hip`` (the n-link chain of config 5),
+``csrc/mppi_npgauss.hip`` (the reference's NumPy noise stream on the device)
+and ``csrc/mppi_readback.hip`` (the sampled trajectories' host read-back) —
 are compiled in parallel and linked into ``_lib/libmppi_rocm.so``.
 """
 from __future__ import annotations
@@ -14,7 +15,8 @@ import subprocess
 HERE = os.path.dirname(os.path.abspath(__file__))
 ROOT = os.path.dirname(HERE)
 CSRC = os.path.join(HERE, "csrc")
-SRCS = [os.path.join(CSRC, "mppi_rocm.hip"), os.path.join(CSRC, "mppi_chain.hip"), os.path.join(CSRC, "mppi_npgauss.hip")]
+SRCS = [os.path.join(CSRC, "mppi_rocm.hip"), os.path.join(CSRC, "mppi_chain.hip"), os.path.join(CSRC, "mppi_npgauss.hip"),
+        os.path.join(CSRC, "mppi_readback.hip")]
 OUT = os.path.join(HERE, "_lib", "libmppi_rocm.so")
 HOST_RNG_SRC = os.path.join(CSRC, "np_legacy_gauss.c")
 HOST_RNG_OUT = os.path.join(HERE, "_lib", "libmppi_hostrng.so")

@@ -24,7 +24,7 @@ from scipy.ndimage import median_filter
 
 from . import _native as N
 from . import hostrng
-from .controller import PinnedReadback, _noise_check, _pinned_zbuf, first_min_index
+from .controller import SampledReadback, _noise_check, _pinned_zbuf, first_min_index
 from .distributed import attach_exchange, check_exchange, exchange_partials, same_on_all_ranks, shard_geometry
 
 SEARCH_IDX_LEN = 30  # control.py:203
@@ -400,7 +400,7 @@ class ChainMPPIController:
         self.last_precision = None     # the rollout precision of the last step's result
         self.last_eta = None           # and the spread of its weights (eta, mppi_chain_last_eta)
         self._last_sampled = None      # the previous call's sampled_traj_list (_fresh_sampled)
-        self._sampled_pool = PinnedReadback()   # sampled_traj_list's read-back buffers
+        self._sampled_pool = SampledReadback()   # sampled_traj_list's read-back buffers
         self._step_count = 0
         self.keep_costs = False
         self.last_S = None
@@ -545,6 +545,7 @@ class ChainMPPIController:
             self._np_ev = torch.cuda.Event()
         self._np_ev.record(eng.stream)
         self._np_stream.wait_event(self._np_ev)
+        self._noise_alt.record_stream(self._np_stream)    # its block is not reused before the draw has run
         kl = eng.K_local
         self._npdev.draw(state, (int(self.K), int(self.T), self.dim_u), plan, self._noise_alt,
                          self._np_stream.cuda_stream, eng.k_offset, kl, (self.dim_u * kl, self.dim_u, 1))
@@ -742,7 +743,7 @@ class ChainMPPIController:
                 sampled = np.zeros((self.K, self.T, self.dim_x))
                 gather_trajectories(tr, self.K, sampled, self.process_group)
             else:
-                sampled = self._sampled_pool(tr)   # the caller's alone, as a fresh array (PinnedReadback)
+                sampled = self._sampled_pool(tr)   # the caller's alone, as a fresh array (SampledReadback)
         else:
             sampled = np.zeros((self.K, self.T, self.dim_x))
         self._prefetch_noise(eng)
@@ -770,6 +771,13 @@ class ChainMPPIController:
         self._engine_built_for = None
         self._noise_ready = None       # a new engine's noise buffer is fresh: draw again
         self._xmode = None
+
+    def __del__(self):  # pragma: no cover - best effort
+        try:
+            if self._npre is not None:
+                self._settle_predraw()                     # a queued draw still writes _noise_alt
+        except Exception:
+            pass
 
     def close(self):
         if self._npre is not None:

@@ -104,60 +104,57 @@ def _noise_check(epsilon, K: int, T: int, du: int):
     return float(epsilon[0, 0, 0] + epsilon[-1, -1, -1])
 
 
-class PinnedReadback:
-    """sampled_traj_list's host arrays (control.py:135-145): a device tensor widened to fp64 on the device and
-    copied into a page-locked host buffer that no caller holds any more, returned as the array over it.  A
-    buffer is reused only when nothing outside the pool refers to its array (views of it included: their base
-    is that array), so every returned array is the caller's alone, as control.py:137's fresh np.zeros is.  The
-    DMA into locked pages skips the pageable copy's staging and the first touch of a fresh array (134 MB at
-    K = 65536, T = 64: 10.4-13.3 -> 2.5 ms per call).
+class SampledReadback:
+    """sampled_traj_list's host arrays (control.py:135-145): the device re-roll's fp32 states read back and
+    widened to fp64 on the host (engine.HostReadback: chunked DMA of the fp32 bytes, host threads widening
+    each landed chunk; fp32 -> fp64 is exact, so the values are the device-side widening's, with half the
+    bytes over the host link: 2.5 -> ~1.3 ms at K = 65536, T = 64) into an array of a pool that no caller
+    holds any more, returned as is.  An array is reused only when nothing outside the pool refers to it (views
+    of it included: their base is that array), so every returned array is the caller's alone, as
+    control.py:137's fresh np.zeros is; a reused array's pages are already mapped.
 
-    Page-locked memory is bounded: at most MAX buffers and MAX_BYTES in all (a buffer larger than that, e.g.
-    the chain's 1.9 GB at config 5, is never pinned).  Past the bound, or when pinning fails, the plain
-    pageable read-back.  clear() drops the pool and returns the freed blocks that torch's caching host
-    allocator keeps to the system."""
+    The pool is bounded: at most MAX arrays and MAX_BYTES in all (a larger array, e.g. the chain's 1.9 GB at
+    config 5, is a fresh one per call).  A CPU tensor (tests) is widened by torch."""
 
-    MAX = 3                 # buffers held at most (run.py's loop holds one array across a call: it cycles through two)
-    MAX_BYTES = 768 << 20   # page-locked bytes held at most (3 x 134 MB at K = 65536, T = 64 fit)
+    MAX = 3                 # arrays held at most (run.py's loop holds one array across a call: it cycles through two)
+    MAX_BYTES = 768 << 20   # bytes held at most (3 x 134 MB at K = 65536, T = 64 fit)
 
     def __init__(self):
-        self._pool = []   # (tensor, array over it)
+        self._pool = []    # arrays
+        self._rb = None    # engine.HostReadback of the device last read from
 
     def clear(self) -> None:
-        had = bool(self._pool)
-        self._pool = []   # arrays the caller still holds keep their tensors alive
-        if had and hasattr(torch._C, "_host_emptyCache"):
-            torch._C._host_emptyCache()   # freed page-locked blocks back to the system, not kept cached
+        self._pool = []    # arrays the caller still holds stay theirs
+        if self._rb is not None:
+            self._rb.close()
+            self._rb = None
 
     def __len__(self) -> int:
         return len(self._pool)
 
-    @staticmethod
-    def _pageable(tr: torch.Tensor) -> np.ndarray:
-        out = tr.double().cpu()
-        return (out.clone() if out.data_ptr() == tr.data_ptr() else out).numpy()   # never the caller's tensor
+    def _fill(self, tr: torch.Tensor, out: np.ndarray) -> np.ndarray:
+        if not tr.is_cuda:
+            np.copyto(out, tr.double().numpy())
+            return out
+        if self._rb is None or self._rb.device != tr.device:
+            from .engine import HostReadback
+            if self._rb is not None:
+                self._rb.close()
+            self._rb = HostReadback(tr.device)
+        return self._rb.run(tr.contiguous(), out)
 
     def __call__(self, tr: torch.Tensor) -> np.ndarray:
         shape = tuple(tr.shape)
         pool = self._pool
-        if pool and tuple(pool[0][1].shape) != shape:
-            self.clear()   # K or T changed
-            pool = self._pool
-        for i in range(len(pool)):
-            if sys.getrefcount(pool[i][1]) == 2:   # the pool's own reference and the argument's
-                buf, arr = pool[i]
-                buf.copy_(tr.double())
-                return arr
-        if len(pool) >= self.MAX or (len(pool) + 1) * tr.numel() * 8 > self.MAX_BYTES:
-            return self._pageable(tr)
-        try:
-            buf = torch.empty(shape, dtype=torch.float64, pin_memory=tr.is_cuda)
-        except RuntimeError:          # page-locking refused (host limits): the pageable read-back
-            return self._pageable(tr)
-        buf.copy_(tr.double())
-        arr = buf.numpy()
-        pool.append((buf, arr))
-        return arr
+        if pool and tuple(pool[0].shape) != shape:
+            self._pool = pool = []   # K or T changed
+        for arr in pool:
+            if sys.getrefcount(arr) == 3:   # the pool list's reference, the loop variable's and the argument's
+                return self._fill(tr, arr)
+        arr = np.empty(shape)
+        if len(pool) < self.MAX and (len(pool) + 1) * arr.nbytes <= self.MAX_BYTES:
+            pool.append(arr)
+        return self._fill(tr, arr)
 
 
 class MPPIControllerForPathTracking:
@@ -232,7 +229,7 @@ class MPPIControllerForPathTracking:
         self.last_S = None
         self._bound = None             # what the engine's drop-in tick is bound to (_bind_key)
         self._last_sampled = None      # the previous call's sampled_traj_list (_fresh_sampled)
-        self._sampled_pool = PinnedReadback()   # sampled_traj_list's read-back buffers (_sampled_host)
+        self._sampled_pool = SampledReadback()   # sampled_traj_list's read-back arrays (_sampled_host)
         self._fast = None              # what the last bound tick checked (calc_control_input's fast test)
         self.numpy_noise_on_device = numpy_noise_on_device   # noise="numpy": the same stream drawn on the device
         self._npdev = None             # its engine.NpDeviceStream (False: unavailable here)
@@ -426,7 +423,7 @@ class MPPIControllerForPathTracking:
             check = _noise_check(epsilon, self.K, self.T, self.dim_u)
             self._multi_setup(eng, check)
         if not self.host_update:
-            return self._fused_step(eng, x0, u, world)
+            return self._fused_step(eng, x0, u, world, predraw=isinstance(epsilon, DeviceDrawn) and world == 1)
         S_out = self._S_dev if self.keep_costs else None
         if world == 1:
             eng.rollout(self._noise_dev, S_out=S_out)
@@ -457,7 +454,7 @@ class MPPIControllerForPathTracking:
     def _sampled_host(self, tr: torch.Tensor, world: int) -> np.ndarray:
         """sampled_traj_list (K, T, 4) fp64 (control.py:135-145) from the device re-roll: widened to fp64 on
         the device and read back into a host array that is returned as is (no second 134 MB copy into an
-        np.zeros; PinnedReadback); the ranks' shards gathered into one array with a process group."""
+        np.zeros; SampledReadback); the ranks' shards gathered into one array with a process group."""
         if world > 1:
             from .distributed import gather_trajectories
             out = np.zeros((self.K, self.T, self.dim_x))
@@ -574,12 +571,13 @@ class MPPIControllerForPathTracking:
         optimal_traj = traj if traj is not None else np.zeros((self.T, self.dim_x))
         return u[0], u, optimal_traj, self._fresh_sampled()
 
-    def _fused_step(self, eng: RolloutEngine, x0, u: np.ndarray, world: int):
+    def _fused_step(self, eng: RolloutEngine, x0, u: np.ndarray, world: int, predraw: bool = False):
         """control.py:81-152 with the update inside the launch (the multi-GPU merge
         launch, or the rollout when sampled trajectories are asked for): median filter
         + u += w_eps + shift on device, the result read from host-mapped memory, the
         optimal trajectory in fp64 on the host from the update.  u is self.u_prev
-        (updated in place)."""
+        (updated in place).  predraw: the next call's NumPy draw is queued behind the
+        trajectory re-roll, so it runs during the sampled trajectories' read-back."""
         S_out = self._S_dev if self.keep_costs else None
         u_before = u.copy() if self.visualze_sampled_trajs else None
         if world == 1:
@@ -589,6 +587,8 @@ class MPPIControllerForPathTracking:
         tr = None
         if self.visualze_sampled_trajs:
             tr = eng.trajectories(base_u=u_before, noise=self._noise_dev)   # pre-update u, v[k, t-1]
+        if predraw:
+            self._queue_predraw(eng)
         u_new, traj = eng.wait_outputs(x0 if self.visualize_optimal_traj else None)
         if self.keep_costs:
             self.last_S = self._S_dev.cpu().numpy()
@@ -660,6 +660,7 @@ class MPPIControllerForPathTracking:
             self._np_ev = torch.cuda.Event()
         self._np_ev.record(eng.stream)
         self._np_stream.wait_event(self._np_ev)
+        self._noise_alt.record_stream(self._np_stream)    # its block is not reused before the draw has run
         self._npdev.draw(state, (int(self.K), int(self.T), self.dim_u), plan, self._noise_alt,
                          self._np_stream.cuda_stream, eng.k_offset, eng.K_local,
                          (eng.K_local * self.dim_u, self.dim_u, 1))
@@ -784,6 +785,13 @@ class MPPIControllerForPathTracking:
         for d in range(xx.shape[1]):
             out[:, d] = median_filter(xx[:, d], size=window_size, mode='reflect')
         return out
+
+    def __del__(self):  # pragma: no cover - best effort
+        try:
+            if self._npre is not None:
+                self._settle_predraw()                     # a queued draw still writes _noise_alt
+        except Exception:
+            pass
 
     def close(self):
         if self._npre is not None:

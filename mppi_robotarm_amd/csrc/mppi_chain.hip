@@ -27,7 +27,6 @@
 
 #include <string>
 
-#define MPPI_CHAIN_TU
 #include "mppi_device.h"
 #include "mppi_host.h"
 #include "mppi_rocm.h"
@@ -41,27 +40,11 @@ constexpr int kCDebugN = 7;                  // the link count with slot-recordi
 constexpr int kCT = 256;                    // threads per workgroup, one lane per sample
 constexpr int kCMaxCh = 4;                  // column chunks of a partial row: T N + 1 <= 4 x 256 ... (N <= 7)
 constexpr int kCMaxVals = kMaxT * kCMax;    // T N values per row, at most
-#ifndef MPPI_CHAIN_CPF
-#define MPPI_CHAIN_CPF 2
-#endif
-#ifndef MPPI_CHAIN_CPU
-#define MPPI_CHAIN_CPU 2
-#endif
-#ifndef MPPI_CHAIN_LIST   // A/B variant: list-only rows with the poll hand-off (mppi_device.h "list rows", TRIED.md)
-#define MPPI_CHAIN_LIST 0
-#endif
-#ifndef MPPI_CHAIN_PRED_NATS
-#define MPPI_CHAIN_PRED_NATS 60.0
-#endif
-// a row is predicted weightless when its rho_b lies this many lambdas above the predicted minimum: the merge
-// floor 2^-64 (44.4) and 15.6 more
-constexpr double kPredNats = MPPI_CHAIN_PRED_NATS;
-constexpr int kCPF = MPPI_CHAIN_CPF;        // noise steps in flight per lane (N rows each)
-#ifndef MPPI_Q4_PF
-#define MPPI_Q4_PF 4   // 2 and 4 measured: equal at K = 16384, 4 -2.1 % at K = 32768 (profiles/r13/chain_quad_ring_depth_ab.txt)
-#endif
-constexpr int kQPF = MPPI_Q4_PF;            // the same for a quad per sample (its steps are ~4x shorter)
-constexpr int kCPU = MPPI_CHAIN_CPU;        // per-step constant rows in flight
+constexpr int kCPF = 2;                     // noise steps in flight per lane (N rows each)
+// the same for a quad per sample (its steps are ~4x shorter); 2 and 4 measured: equal at K = 16384, 4 -2.1 % at
+// K = 32768 (profiles/r13/chain_quad_ring_depth_ab.txt)
+constexpr int kQPF = 4;
+constexpr int kCPU = 2;                     // per-step constant rows in flight
 
 // Device-resident per-step parameter block (ping-pong pair in the context).
 struct alignas(16) ChainStep {
@@ -684,11 +667,8 @@ __device__ __forceinline__ double chain_horizon_q4(const ChainConst& c, const Ch
                                                    float4* s_win, int* slots, unsigned long long* dbg) {
     static_assert(N <= 8, "four link pairs");
     // the column after which the search is placed: after 2 / 3 / 4 / 5 / 6 measured 77.0 / 76.6 / 77.6 / 75.3 /
-    // 77.3 us at K = 16384 (one process, profiles/r13/chain_quad_search_at_ab.txt); MPPI_Q4_SEARCH_AT for A/B builds
-#ifndef MPPI_Q4_SEARCH_AT
-#define MPPI_Q4_SEARCH_AT 5
-#endif
-    constexpr int kSearchAt = N > MPPI_Q4_SEARCH_AT ? MPPI_Q4_SEARCH_AT : N - 1;
+    // 77.3 us at K = 16384 (one process, profiles/r13/chain_quad_search_at_ab.txt)
+    constexpr int kSearchAt = N > 5 ? 5 : N - 1;
     const int tid = threadIdx.x, sub = tid & 3, K = c.K_local, T = c.T;
     if (tid < kSlots) s_win[tid] = st->win[tid];
     for (int i = tid; i < (T + kQPF) * 4; i += kCT) {
@@ -827,11 +807,9 @@ __device__ __forceinline__ double chain_horizon_q4(const ChainConst& c, const Ch
                 constexpr int kk = decltype(k_c)::value;
                 if constexpr (kk > j) {
                     Ln[kk][j] = qbc<kk / 2>(elem<kk>(col[j])) * nrd;
-#ifndef MPPI_Q4_NO_LAST_ROW_PIN
                     // the last row's products, left free, are paired by the SLP vectoriser into a v_pk_mul_f32,
                     // which has no DPP form: their broadcasts come back as separate moves (7 per step)
                     if constexpr (kk == N - 1) asm volatile("" : "+v"(Ln[kk][j]));
-#endif
                     col[kk] = __builtin_elementwise_fma(splat(Ln[kk][j]), col[j], col[kk]);
                 }
             }, std::make_integer_sequence<int, N>{});
@@ -933,7 +911,7 @@ __global__ __launch_bounds__(kCT) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
     __shared__ int s_k[kCT];
     __shared__ double s_e[kCT];
     __shared__ unsigned s_flag, s_parity;
-    __shared__ double s_run, s_pred;
+    __shared__ double s_run;
     __shared__ CScratch sm;
 
     static_assert(LPS == 1 || (LPS == 4 && !F64), "lanes per sample: 1, or 4 for the fp32 rollout");
@@ -953,8 +931,8 @@ __global__ __launch_bounds__(kCT) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
     STAMP(8, (unsigned long long)__builtin_amdgcn_s_getreg(0xF804));   // HW_ID
     STAMP(9, (unsigned long long)__builtin_amdgcn_s_getreg(0xF814));   // XCC_ID
 #endif
-    // poll tags stay below kListTagBit (list-only rows set it, mppi_device.h) and never 0 (fresh memory)
-    unsigned tag_v = POLL ? (__hip_atomic_load(epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) + 1u) & ~kListTagBit : 0u;
+    // poll tags are never 0 (fresh memory)
+    unsigned tag_v = POLL ? __hip_atomic_load(epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) + 1u : 0u;
     if (POLL && tag_v == 0u) tag_v = 1u;
     double u_cur[kMedRun];
     chain_nominal_prefetch<N>(st, T, flags & MPPI_FLAG_FUSED_UPDATE, u_cur);
@@ -976,19 +954,10 @@ __global__ __launch_bounds__(kCT) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
     // past the last step read step T - 1 again (never used)
     // (uniform step base + a 32-bit lane byte offset: the saddr form of global_load)
     const unsigned kb = (unsigned)k * (unsigned)N * 4u;
-#ifdef MPPI_CHAIN_NOISE_BUFFER
-    // row offset in the buffer instruction's scalar soffset: no 64-bit VALU address per load
-    const __amdgpu_buffer_rsrc_t nrs = rows_rsrc(noise, T * N * K * 4);
-    auto nrow = [&](int t, int d) {
-        const int so = __builtin_amdgcn_readfirstlane(min(t, T - 1) * K * N * 4);
-        return __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(nrs, (int)kb + 4 * d, so, 0));
-    };
-#else
     auto nrow = [&](int t, int d) {
         const char* row = (const char*)(noise + (size_t)min(t, T - 1) * K * N + d);
         return *(const float*)(row + kb);
     };
-#endif
     cfloat* cua = (cfloat*)(&st->ua[0][0]);
     float ring[kCPF][N];
     float uring[kCPU][2 * N];
@@ -1061,13 +1030,8 @@ __global__ __launch_bounds__(kCT) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
     // finishing spread out) the atomic's fresher return skips more gathers (measured: +1.7 % with the early
     // read at config 5, -1.7 % at its shard)
     constexpr bool kEarlyRun = LPS == 4;
-    constexpr bool kList = POLL && MPPI_CHAIN_LIST;
-    unsigned long long run0 = ~0ull, prev0 = ~0ull, prev1 = ~0ull;   // prev: the last two launches' merged rho
+    unsigned long long run0 = ~0ull;
     if (kEarlyRun && tid == 0) run0 = __hip_atomic_load(runmin, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    if (kList && tid == 0) {
-        prev0 = __hip_atomic_load(runmin + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        prev1 = __hip_atomic_load(runmin + 2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    }
     const double rho_b = block_min_f64<kCT>(owner ? S : INFINITY, sm);
     // fp64, like the reference's weights; a wave whose samples all lie below the
     // floor (exp(-44.4) = 2^-64: the usual case, S spread >> lambda) skips the exp
@@ -1098,10 +1062,6 @@ __global__ __launch_bounds__(kCT) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
             run = old < key ? old : key;
         }
         s_run = ord_val(run);
-        // the last merged rho extrapolated by its last change (a drifting loop), when both are known
-        const double p0 = ord_val(prev0), p1 = ord_val(prev1);
-        const double pp = prev0 == ~0ull ? NAN : prev1 == ~0ull ? p0 : p0 + (p0 - p1);
-        s_pred = min_raw_f64(ord_val(run), pp);
     }
     __syncthreads();
     const bool skip = exp((s_run - rho_b) * c.inv_lambda) < kMergeFloor;   // uniform
@@ -1137,25 +1097,12 @@ __global__ __launch_bounds__(kCT) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
     };
     // rho_b and eta_b leave first (see rollout_kernel in mppi_rocm.hip)
     nl = __builtin_amdgcn_readfirstlane(nl);
-    // List-only rows (poll hand-off, list rows in mppi_device.h): a row with few weighted samples whose rho_b lies
-    // kPredNats beyond the predicted minimum — the running minimum so far or the last launch's merged rho, the
-    // better of the two — publishes its samples instead of gathering its columns.  The prediction only steers
-    // traffic: a list-only row that does carry weight (the minimum jumped up) is gathered by the merger.
-    const bool lonly = kList && !skip && nl <= kListMax && 2 * nl + 1 <= nval &&
-                       (rho_b - s_pred) * c.inv_lambda > kPredNats;   // uniform (NaN: no prediction)
     if (tid == 0) {
-        if constexpr (POLL) st_gran(slab_r, blockIdx.x * stride, skip ? INFINITY : rho_b, lonly ? tag | kListTagBit : tag);
-        else publish(blockIdx.x * stride, skip ? INFINITY : rho_b);
+        publish(blockIdx.x * stride, skip ? INFINITY : rho_b);
         publish(blockIdx.x * stride + 1, eta_b);
     }
     if (skip) {
         // no merge reads this row past rho
-    } else if (lonly) {
-        if (tid == 0) publish(blockIdx.x * stride + 2, list_mode_word(nl));
-        if (tid < nl) {
-            publish(blockIdx.x * stride + 3 + 2 * tid, (double)s_k[tid]);
-            publish(blockIdx.x * stride + 4 + 2 * tid, s_e[tid]);
-        }
     } else if (nl <= kSparseMax) {
         // column (t, d) = t N + d of the noise: sample k's value at noise[(t K + k) N + d]
         for (int col = tid; col < nval; col += kCT) {
@@ -1205,19 +1152,15 @@ __global__ __launch_bounds__(kCT) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
     if constexpr (POLL) {
         if ((int)blockIdx.x != g * kGroup) return;
         STAMP(3, NOW());
-        const ListSrc ls{noise, K, N};
         if (ngroups == 1) {
-            merge_rows_block<kCT, kCMaxCh, true, true, decltype(sm), kList>(slab_r, 0, gsz, geo, c.inv_lambda, sm,
-                                                                            nullptr, 0, partial_out, w_eps_out, tag,
-                                                                            tmo, 0ull, nullptr, ls);
+            merge_rows_block<kCT, kCMaxCh, true, true>(slab_r, 0, gsz, geo, c.inv_lambda, sm, nullptr, 0, partial_out,
+                                                       w_eps_out, tag, tmo);
         } else if (blockIdx.x == 0 && nrows <= kDirectRows &&
-                   direct_merge<kCT, kCMaxCh, true, decltype(sm), kList>(slab_r, nrows, geo, c.inv_lambda, sm,
-                                                                         partial_out, w_eps_out, tag, tmo, nullptr,
-                                                                         ls)) {
+                   direct_merge<kCT, kCMaxCh, true>(slab_r, nrows, geo, c.inv_lambda, sm, partial_out, w_eps_out, tag,
+                                                    tmo)) {
         } else {
-            merge_rows_block<kCT, kCMaxCh, false, true, decltype(sm), kList>(slab_r, g * kGroup, gsz, geo,
-                                                                             c.inv_lambda, sm, &gslab_r, g, nullptr,
-                                                                             nullptr, tag, tmo, 0ull, nullptr, ls);
+            merge_rows_block<kCT, kCMaxCh, false, true>(slab_r, g * kGroup, gsz, geo, c.inv_lambda, sm, &gslab_r, g,
+                                                        nullptr, nullptr, tag, tmo);
             STAMP(10, NOW());
             if (blockIdx.x != 0) return;
             STAMP(4, NOW());
@@ -1227,10 +1170,6 @@ __global__ __launch_bounds__(kCT) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
         if (threadIdx.x == 0) {
             __hip_atomic_store(epoch, tag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             __hip_atomic_store(runmin, ~0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);   // every row is in
-            if (kList) {
-                __hip_atomic_store(runmin + 2, prev0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                __hip_atomic_store(runmin + 1, ord_key(sm.rho_fin), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            }
         }
     } else {
         if (!arrive_last(counters + g, (unsigned)gsz, &s_flag, c.acquire != 0)) return;

@@ -45,34 +45,21 @@ constexpr int kGroup = 16;             // workgroups per first-level merge group
 // (which has s = 1 and eta >= 1): far below the fp64 resolution of the result.
 constexpr double kMergeFloor = 5.421010862427522e-20;  // 2^-64
 constexpr int kDirectRows = 256;       // workgroup rows the direct merge scans (4 per lane)
-#ifndef MPPI_DIRECT_MAX
-#define MPPI_DIRECT_MAX 16
-#endif
-constexpr int kDirectMax = MPPI_DIRECT_MAX;  // weighted rows it merges; more go through the group rows
+constexpr int kDirectMax = 16;         // weighted rows it merges; more go through the group rows
 constexpr int kSparseMax = 16;         // weighted samples per workgroup handled by the epilogue gather
 
 // ------------------------------------------------------------------ helpers
 
 // Hardware v_sin_f32 / v_cos_f32 (argument pre-scaled by 1/(2 pi)): 30 % faster
 // rollouts than OCML's sincosf at K=65536 T=64, parity unchanged (S rel-err
-// budget 5e-5 in tests/test_gpu_parity.py).  -DMPPI_ACCURATE_TRIG selects sincosf.
-__device__ __forceinline__ void sincos_f32(float x, float* s, float* c) {
-#ifdef MPPI_ACCURATE_TRIG
-    sincosf(x, s, c);
-#else
-    __sincosf(x, s, c);
-#endif
-}
+// budget 5e-5 in tests/test_gpu_parity.py).
+__device__ __forceinline__ void sincos_f32(float x, float* s, float* c) { __sincosf(x, s, c); }
 
 // Every control used here (quad_perm, row_mirror, row_half_mirror, row_ror) reads
 // a valid lane, so bound_ctrl changes no value; set, it lets the compiler fold the
 // move into a VOP1 / VOP2 consumer (v_mul_f32_dpp, v_add_f32_dpp, v_rsq_f32_dpp:
 // GCNDPPCombine takes a move with an undefined old value only under bound_ctrl).
-#ifdef MPPI_DPP_NOBC
-constexpr bool kDppBC = false;
-#else
 constexpr bool kDppBC = true;
-#endif
 template <int CTRL>
 __device__ __forceinline__ float dpp_f32(float v) {
     return __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), CTRL, 0xF, 0xF, kDppBC));
@@ -272,11 +259,7 @@ struct Search {
         const f32x2 ax2 = {dx, dx}, ay2 = {dy, dy};
         const float pp = fmaf(dx, dx, dy * dy);
         const f32x2 pp2 = {pp, pp};
-#ifdef MPPI_MIN_CHAIN
-        float best = 3.0e38f;
-#else
         float kk[2 * SP];
-#endif
 #pragma unroll
         for (int i = 0; i < SP; ++i) {
             f32x2 key = __builtin_elementwise_fma(ax2, krx[i], __builtin_elementwise_fma(ay2, kry[i], kc[i]));
@@ -286,18 +269,12 @@ struct Search {
             const unsigned j = (unsigned)(sub * SL + 2 * i);
             const float k0 = __uint_as_float((__float_as_uint(key.x) & ~31u) | j);
             const float k1 = __uint_as_float((__float_as_uint(key.y) & ~31u) | (j + 1));
-#ifdef MPPI_MIN_CHAIN
-            best = min3_raw(best, k0, k1);
-#else
             kk[2 * i] = k0;
             kk[2 * i + 1] = k1;
-#endif
         }
-#ifndef MPPI_MIN_CHAIN
         // the same v_min3 count as a running minimum, but 4 levels deep instead of
         // 15 (the keys carry distinct indices, so the order of the minima is free)
         float best = min_tree<2 * SP>(kk);
-#endif
         if (LPS >= 2) best = min_raw(best, dpp_f32<0xB1>(best));  // quad_perm xor 1
         if (LPS >= 4) best = min_raw(best, dpp_f32<0x4E>(best));  // quad_perm xor 2
         if (LPS >= 8) best = min_raw(best, dpp_f32<0x141>(best));  // row_half_mirror: the other quad of 8
@@ -440,18 +417,11 @@ constexpr unsigned kSpinMax = 1u << 20;
 __device__ __forceinline__ void report_timeout(unsigned* tmo) {
     if (tmo) __hip_atomic_store(tmo, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
 }
-#if defined(MPPI_LIST_DEBUG) && defined(MPPI_CHAIN_TU)   // diagnostic builds: which poll gave up
-#define MPPI_GIVE_UP_TRACE(lane) \
-    if ((lane) == 0) printf("poll gave up: block %d thread %d line %d\n", (int)blockIdx.x, (int)threadIdx.x, __LINE__)
-#else
-#define MPPI_GIVE_UP_TRACE(lane) (void)0
-#endif
 #define MPPI_SPIN_OR_GIVE_UP(spins, tmo, lane) MPPI_SPIN_OR_GIVE_UP_L(spins, 0ull, tmo, lane, (void)0)
 // with a deadline of its own (s_memrealtime ticks, 100 MHz; 0: the spin bound alone) and a statement run
 // when it gives up (the exchange's polls)
 #define MPPI_SPIN_OR_GIVE_UP_L(spins, deadline, tmo, lane, on_give_up)                                   \
     if (spins >= kSpinMax || ((deadline) && __builtin_amdgcn_s_memrealtime() > (deadline))) {            \
-        MPPI_GIVE_UP_TRACE(lane);                                                                        \
         if ((lane) == 0) report_timeout(tmo);                                                            \
         on_give_up;                                                                                      \
         break;                                                                                           \
@@ -531,104 +501,6 @@ __device__ __forceinline__ void put_final(double rho, const double (&acc)[MAXCH]
     __syncthreads();
 }
 
-// ------------------------------------------------------------ list rows
-// A workgroup row whose weighted samples are few (nl <= kListMax) can carry them instead of its noise columns
-// (the chain kernel, poll hand-off): slot 2 holds the mode word {lo = nl, hi = kListHi} (a signalling NaN, which
-// no column sum is), slots 3 + 2l and 4 + 2l the l-th weighted sample's local index and weight, ascending.  The
-// merger that needs the row's columns gathers them from the noise itself with the row gather's operations in its
-// order (gather_col_n: fp64 fma over l from 0), so a list row merges to the same bits as the column row it
-// replaces, and only the rows that carry weight in some merge are ever gathered: a row's own gather cannot know
-// that, and read a cache line per value for every row (the chain's noise: ~T lines per sample).  Not the product: an A/B
-// variant (MPPI_CHAIN_LIST in mppi_chain.hip; TRIED.md) that cut the c5 shard's traffic 1.14x -> 1.04x at +1.9 %
-// time.
-#ifndef MPPI_LIST_MAX
-#define MPPI_LIST_MAX 2
-#endif
-constexpr int kListMax = MPPI_LIST_MAX;
-constexpr unsigned kListHi = 0x7ff4c0deu;
-struct ListSrc {
-    const float* noise = nullptr;   // the row's column j = t n + d of sample k at noise[(t K + k) n + d]
-    int K = 0, n = 1;
-};
-// A list-only row (its columns not published) says so in its rho granule: both tag words carry kListTagBit
-// (tags stay below it), so the merger knows from the rho poll which weighted rows it must gather itself, and a
-// row that gathered costs the merge nothing more than before.
-constexpr unsigned kListTagBit = 0x80000000u;
-__device__ __forceinline__ bool gran_ok_lst(u32x4 x, unsigned tag) {
-    return (x[1] & ~kListTagBit) == tag && x[3] == x[1];
-}
-__device__ __forceinline__ bool gran_lst(u32x4 x) { return (x[1] & kListTagBit) != 0u; }
-__device__ __forceinline__ int* list_flags_lds() {   // the direct merge's per-row list-only flags
-    __shared__ int f[kDirectRows];
-    return f;
-}
-__device__ __forceinline__ double list_mode_word(int nl) {
-    return __longlong_as_double((long long)(((unsigned long long)kListHi << 32) | (unsigned)nl));
-}
-
-// The lane's row header at granule offset `off` (kOffRange: none): eta (slot 1), the mode word and, for a list
-// row, its entries, polled until valid.  nl = 0: the row carries columns.  True if a poll gave up.
-__device__ __forceinline__ bool poll_list_header(__amdgpu_buffer_rsrc_t rows, int off, unsigned tag, double& eta,
-                                                 int& nl, int (&k)[kListMax], double (&w)[kListMax], unsigned* tmo,
-                                                 unsigned long long deadline) {
-    const int lane = threadIdx.x & 63;
-    u32x4 h[2 + 2 * kListMax];
-    bool gave_up = false;
-    for (unsigned spins = 0;; ++spins) {
-        asm volatile("" ::: "memory");
-#pragma unroll
-        for (int s = 0; s < 2 + 2 * kListMax; ++s) h[s] = ld_gran(rows, off + 1 + s);
-        const int n = h[1][2] == kListHi ? (int)(h[1][0] & 0xffu) : 0;
-        bool ok = gran_ok(h[0], tag) && gran_ok(h[1], tag);
-#pragma unroll
-        for (int l = 0; l < kListMax; ++l) ok = ok && (l >= n || (gran_ok(h[2 + 2 * l], tag) && gran_ok(h[3 + 2 * l], tag)));
-        if (__all(off >= kOffRange || ok)) break;
-        MPPI_SPIN_OR_GIVE_UP_L(spins, deadline, tmo, lane, gave_up = true);
-    }
-    eta = gran_val(h[0]);
-    nl = h[1][2] == kListHi ? min((int)(h[1][0] & 0xffu), kListMax) : 0;
-#pragma unroll
-    for (int l = 0; l < kListMax; ++l) {
-        k[l] = l < nl ? (int)gran_val(h[2 + 2 * l]) : 0;
-        w[l] = gran_val(h[3 + 2 * l]);
-    }
-    return gave_up;
-}
-
-// Entries of a load batch (x[j]: row b0 + j / MAXCH of the lanes' headers, merged column tid + (j % MAXCH) NT)
-// for the list rows among them; column rows' entries are left as loaded.  Merged column 0 is eta, column 1 + c
-// the noise column c.
-template <int NT, int MAXCH, int LB>
-__device__ __forceinline__ void list_entries(double (&x)[LB], int b0, int nb, int nl_l, const int (&k_l)[kListMax],
-                                             const double (&w_l)[kListMax], double eta_l, int ncol, const ListSrc& ls) {
-    const int tid = threadIdx.x;
-    float e[LB][kListMax];
-#pragma unroll
-    for (int j = 0; j < LB; ++j) {
-        const int i = min(b0 + j / MAXCH, 63), col = tid + (j % MAXCH) * NT;
-        const int nli = b0 + j / MAXCH < nb ? __builtin_amdgcn_readlane(nl_l, i) : 0;   // uniform
-        const int cc = min(max(col - 1, 0), ncol - 2), tt = cc / ls.n;
-        const size_t cb = (size_t)tt * ls.K * ls.n + (cc - tt * ls.n);
-#pragma unroll
-        for (int l = 0; l < kListMax; ++l) {
-            const int kk = __builtin_amdgcn_readlane(k_l[l], i);
-            e[j][l] = l < nli ? ls.noise[cb + (size_t)kk * ls.n] : 0.f;
-        }
-    }
-#pragma unroll
-    for (int j = 0; j < LB; ++j) {
-        const int i = min(b0 + j / MAXCH, 63), col = tid + (j % MAXCH) * NT;
-        const int nli = b0 + j / MAXCH < nb ? __builtin_amdgcn_readlane(nl_l, i) : 0;
-        if (nli > 0) {
-            double a = 0.0;
-#pragma unroll
-            for (int l = 0; l < kListMax; ++l)
-                if (l < nli) a = fma(readlane_f64(w_l[l], i), (double)e[j][l], a);
-            x[j] = col == 0 ? readlane_f64(eta_l, i) : col < ncol ? a : 0.0;
-        }
-    }
-}
-
 // Merge n rows (read write-through from `rows`, rows row0 .. row0 + n - 1) with
 // a log-sum-exp rescale: rho = min rho_i, s_i = exp((rho - rho_i) / lambda),
 // eta = sum s_i eta_i, N = sum s_i N_i, in ascending row order (deterministic);
@@ -648,15 +520,14 @@ __device__ __forceinline__ void list_entries(double (&x)[LB], int b0, int nb, in
 //   rows that carry weight, 16 / MAXCH rows per load batch.
 // The merged row goes to out_wt (same format, next level) or, with `final`,
 // to put_final.
-template <int NT, int MAXCH, bool final, bool GRAN, class SM, bool LIST = false>
+template <int NT, int MAXCH, bool final, bool GRAN, class SM>
 __device__ __forceinline__ void merge_rows_block(__amdgpu_buffer_rsrc_t rows, int row0, int n, const RowGeo& geo,
                                                  double inv_lambda, SM& sm, const __amdgpu_buffer_rsrc_t* out_wt,
                                                  int out_idx, double* out_row, double* w_eps_out, unsigned tag,
                                                  unsigned* tmo, unsigned long long deadline = 0ull,
-                                                 bool* failed = nullptr, const ListSrc& ls = ListSrc{}) {
+                                                 bool* failed = nullptr) {
     // deadline / failed: the polls' deadline (s_memrealtime; 0: the spin bound alone), and (when given) whether
-    // any poll of the workgroup gave up (uniform).  LIST (GRAN only): the rows may be list rows (above).
-    static_assert(!LIST || GRAN, "list rows: poll hand-off");
+    // any poll of the workgroup gave up (uniform).
     constexpr bool EAGER = !GRAN && MAXCH == 1;  // one round trip per round of 32 rows
     constexpr int LB = EAGER ? 32 : 16;         // loads per batch per thread
     constexpr int RB = LB / MAXCH;              // rows per load batch
@@ -674,17 +545,15 @@ __device__ __forceinline__ void merge_rows_block(__amdgpu_buffer_rsrc_t rows, in
         const int rb = row0 + r0;
         const int lrow = lane < nr ? (rb + lane) * stride : kOffRange;
         double rho_r, eta_l = 0.0, v[EAGER ? LB : 1];
-        bool lst_r = false;   // LIST: this lane's row is list-only
         if constexpr (GRAN) {
             u32x4 gr;
             for (unsigned spins = 0;; ++spins) {
                 asm volatile("" ::: "memory");
                 gr = ld_gran(rows, lrow);
-                if (__all(lane >= nr || (LIST ? gran_ok_lst(gr, tag) : gran_ok(gr, tag)))) break;
+                if (__all(lane >= nr || gran_ok(gr, tag))) break;
                 MPPI_SPIN_OR_GIVE_UP_L(spins, deadline, tmo, lane, gave_up = true);
             }
             rho_r = gran_val(gr);
-            lst_r = LIST && lane < nr && gran_lst(gr);
         } else if constexpr (!EAGER) {
             rho_r = ld_wt(rows, lrow);
         } else {
@@ -728,21 +597,8 @@ __device__ __forceinline__ void merge_rows_block(__amdgpu_buffer_rsrc_t rows, in
         } else {
             // lane k < nrr: the round's k-th weighted row (ascending)
             const int krow = lane < nrr ? select_bit(rel, lane) : 0;
-            // LIST: the list-only weighted rows' headers (eta with them) before their entries
-            int nl_l = 0, k_l[kListMax];
-            double w_l[kListMax];
-            if constexpr (LIST) {
-                // the shuffle runs in every lane: a cross-lane read returns nothing from a lane the EXEC mask has off
-                const int lst_k = __shfl(lst_r ? 1 : 0, krow);
-                const bool need = lane < nrr && lst_k != 0;
-                if (__any(need))
-                    gave_up |= poll_list_header(rows, need ? (rb + krow) * stride : kOffRange, tag, eta_l, nl_l, k_l,
-                                                w_l, tmo, deadline);
-                if (!need) nl_l = 0;
-            }
-            const unsigned long long lmask = LIST ? __ballot(nl_l != 0) : 0ull;   // the list rows among them
             for (int b0 = 0; b0 < nrr; b0 += RB) {
-                const bool eta_on = b0 == 0 && lane < nrr && nl_l == 0;
+                const bool eta_on = b0 == 0 && lane < nrr;
                 const int eidx = eta_on ? (rb + krow) * stride + 1 : kOffRange;
                 double x[LB];
                 if constexpr (GRAN) {
@@ -754,7 +610,7 @@ __device__ __forceinline__ void merge_rows_block(__amdgpu_buffer_rsrc_t rows, in
 #pragma unroll
                         for (int j = 0; j < LB; ++j) {
                             const int i = b0 + j / MAXCH, col = tid + (j % MAXCH) * NT;
-                            const bool on = i < nrr && col < ncol && !((lmask >> min(i, 63)) & 1ull);
+                            const bool on = i < nrr && col < ncol;
                             gv[j] = ld_gran(rows, on ? (rb + __builtin_amdgcn_readlane(krow, i)) * stride + 1 + col
                                                      : kOffRange);
                             ok = ok && (!on || gran_ok(gv[j], tag));
@@ -765,7 +621,6 @@ __device__ __forceinline__ void merge_rows_block(__amdgpu_buffer_rsrc_t rows, in
                     if (eta_on) eta_l = gran_val(ge);
 #pragma unroll
                     for (int j = 0; j < LB; ++j) x[j] = gran_val(gv[j]);
-                    if (LIST && lmask) list_entries<NT, MAXCH, LB>(x, b0, nrr, nl_l, k_l, w_l, eta_l, ncol, ls);
                 } else {
                     if (b0 == 0) eta_l = ld_wt(rows, eidx);
 #pragma unroll
@@ -813,12 +668,10 @@ __device__ __forceinline__ void merge_rows_block(__amdgpu_buffer_rsrc_t rows, in
 // on the critical path instead of two.  Returns false (uniformly) when more rows
 // carry weight; the caller then merges through the group rows.  Wave-local
 // like merge_rows_block; the result goes out as in a final merge.
-template <int NT, int MAXCH, bool GRAN, class SM, bool LIST = false>
+template <int NT, int MAXCH, bool GRAN, class SM>
 __device__ __forceinline__ bool direct_merge(__amdgpu_buffer_rsrc_t rows, int n, const RowGeo& geo,
                                              double inv_lambda, SM& sm, double* out_row, double* w_eps_out,
-                                             unsigned tag, unsigned* tmo, unsigned long long* dbg = nullptr,
-                                             const ListSrc& ls = ListSrc{}) {
-    static_assert(!LIST || (GRAN && MAXCH > 1), "list rows: poll hand-off, one row group");
+                                             unsigned tag, unsigned* tmo, unsigned long long* dbg = nullptr) {
     constexpr int P = kDirectRows / 64;
     constexpr int LB = 16;                      // loads per batch per thread
     constexpr int RB = LB / MAXCH;              // rows per load batch
@@ -838,16 +691,13 @@ __device__ __forceinline__ bool direct_merge(__amdgpu_buffer_rsrc_t rows, int n,
                 for (int j = 0; j < P; ++j) {
                     const int r = lane + 64 * j;
                     gr[j] = ld_gran(rows, r < n ? r * stride : kOffRange);
-                    ok = ok && (r >= n || (LIST ? gran_ok_lst(gr[j], tag) : gran_ok(gr[j], tag)));
+                    ok = ok && (r >= n || gran_ok(gr[j], tag));
                 }
                 if (__all(ok)) break;
                 MPPI_SPIN_OR_GIVE_UP(spins, tmo, lane);
             }
 #pragma unroll
-            for (int j = 0; j < P; ++j) {
-                sm.rho[lane + 64 * j] = lane + 64 * j < n ? gran_val(gr[j]) : INFINITY;
-                if constexpr (LIST) list_flags_lds()[lane + 64 * j] = gran_lst(gr[j]) ? 1 : 0;
-            }
+            for (int j = 0; j < P; ++j) sm.rho[lane + 64 * j] = lane + 64 * j < n ? gran_val(gr[j]) : INFINITY;
         }
         __syncthreads();
 #pragma unroll
@@ -910,20 +760,10 @@ __device__ __forceinline__ bool direct_merge(__amdgpu_buffer_rsrc_t rows, int n,
     if (G == 1) {
         // one group: the rows of a batch are wave-uniform (v_readlane); eta as a
         // scalar in the same row order as column 0
-        // LIST: every weighted row's header first (eta with it)
-        int nl_l = 0, k_l[kListMax];
-        double w_l[kListMax];
-        if constexpr (LIST) {
-            const bool need = mine && list_flags_lds()[row] != 0;
-            if (__any(need))
-                (void)poll_list_header(rows, need ? row * stride : kOffRange, tag, eta_k, nl_l, k_l, w_l, tmo, 0ull);
-            if (!need) nl_l = 0;
-        }
-        const unsigned long long lmask = LIST ? __ballot(nl_l != 0) : 0ull;   // the list rows among them
         for (int b0 = 0; b0 < nrel; b0 += RB) {
             double v[LB];
             if constexpr (GRAN) {
-                const bool eta_on = b0 == 0 && mine && nl_l == 0;
+                const bool eta_on = b0 == 0 && mine;
                 u32x4 ge, gv[LB];
                 for (unsigned spins = 0;; ++spins) {
                     asm volatile("" ::: "memory");
@@ -932,7 +772,7 @@ __device__ __forceinline__ bool direct_merge(__amdgpu_buffer_rsrc_t rows, int n,
 #pragma unroll
                     for (int j = 0; j < LB; ++j) {
                         const int i = b0 + j / MAXCH, col = tid + (j % MAXCH) * NT;
-                        const bool on = i < nrel && col < ncol && !((lmask >> min(i, 63)) & 1ull);
+                        const bool on = i < nrel && col < ncol;
                         gv[j] = ld_gran(rows, on ? __builtin_amdgcn_readlane(row, i) * stride + 1 + col : kOffRange);
                         ok = ok && (!on || gran_ok(gv[j], tag));
                     }
@@ -942,7 +782,6 @@ __device__ __forceinline__ bool direct_merge(__amdgpu_buffer_rsrc_t rows, int n,
                 if (eta_on) eta_k = gran_val(ge);
 #pragma unroll
                 for (int j = 0; j < LB; ++j) v[j] = gran_val(gv[j]);
-                if (LIST && lmask) list_entries<NT, MAXCH, LB>(v, b0, nrel, nl_l, k_l, w_l, eta_k, ncol, ls);
             } else {
                 if (b0 == 0) eta_k = ld_wt(rows, mine ? row * stride + 1 : kOffRange);
 #pragma unroll
@@ -1244,10 +1083,7 @@ __device__ __forceinline__ bool exchange_verdict(const XDesc& x, const RowGeo& g
 // 2^kPrioShift ticks (100 MHz: ~41 us), the phase flipped by the ticket parity.
 // Priority steers scheduling only; no result depends on it.
 constexpr int kCuSlots = 2048;   // (XCC, SE, SH, CU) keys
-#ifndef MPPI_PRIO_SHIFT
-#define MPPI_PRIO_SHIFT 12
-#endif
-constexpr int kPrioShift = MPPI_PRIO_SHIFT;
+constexpr int kPrioShift = 12;
 __device__ __forceinline__ unsigned cu_key() {
     const unsigned hw = __builtin_amdgcn_s_getreg(0xF804);    // HW_ID
     const unsigned xcc = __builtin_amdgcn_s_getreg(0xF814);   // XCC_ID

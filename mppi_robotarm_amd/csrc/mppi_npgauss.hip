@@ -11,8 +11,7 @@
 //                    J words on is sum_d phi_d F^d(key) with phi = x^J mod P (P: the characteristic
 //                    polynomial, found and powered on the host, np_legacy_gauss.c) and F^d(key) the window
 //                    [d, d + 624) of the word sequence (Haramoto et al. 2008, the window form): a table product
-//                    over 4-bit chunks of phi, the 16 entries of a chunk in each lane's registers (np_jump_kernel,
-//                    the XOR of the sequence words at phi's ~10k set bits from LDS, stays for A/B).
+//                    over 4-bit chunks of phi, the 16 entries of a chunk in each lane's registers.
 //   np_gen_kernel    one workgroup per stream twists its range of blocks; a block's 624 words are each a
 //                    function of the previous block alone (the twist's in-block dependencies unrolled: up to
 //                    three tempering-free mix terms per word), so one barrier per block.
@@ -57,31 +56,13 @@ constexpr int kSeqBlocks = (kDeg + kN) / kN + 1;      // 34: the windows d + j <
 constexpr int kNT = 256;                              // threads of the attempt kernels
 constexpr int kTT = 704;                              // threads of the twist kernels: one word per thread, the
                                                       // twist's three ranges on whole waves (twist_slot)
-constexpr int kJHalf = 320;                           // lanes of a jump group; a lane's second word: 5 x 64 on
-constexpr int kJGroups = 3;                           // groups of a jump workgroup, each a share of the bits
-constexpr int kJT = kJGroups * kJHalf;                // threads of a jump workgroup (15 waves)
-constexpr int kJSplit = 4;                            // workgroups per stream, each a quarter of the set bits
-constexpr int kJBatch = 32;                           // set bits of a jump polynomial read per batch
-constexpr int kSeqPad = kSeqBlocks * kN;              // list padding: s_seq[kSeqPad + j] = 0 for j < 640
-constexpr int kJListStride = ((kDeg + 1 + kJSplit * kJBatch - 1) / (kJSplit * kJBatch)) * kJSplit * kJBatch;
-constexpr int kJPart = kJListStride / kJSplit;        // list entries per workgroup (a multiple of kJBatch)
-#ifndef MPPI_NP_JUMP_WGS
-#define MPPI_NP_JUMP_WGS 512
-#endif
-#ifndef MPPI_NP_JUMP_TABLE
-#define MPPI_NP_JUMP_TABLE 1   // 0: the set-bit list jump (np_jump_kernel), for A/B
-#endif
 constexpr int kNibS = 32;                             // table jump: streams per workgroup
 constexpr int kNibW = kNibS / 8;                      // their nibbles of one chunk: 4 words
 constexpr int kChunks = (kDeg + 3) / 4;               // 4-bit chunks of a jump polynomial
 constexpr int kJNT = 640;                             // table jump threads: output word i per lane (< 624)
-constexpr int kJTableWGs = MPPI_NP_JUMP_WGS;                       // table jump: chunk ranges x stream groups, about
-#ifndef MPPI_NP_ATT_ROUNDS
-#define MPPI_NP_ATT_ROUNDS 8
-#endif
-constexpr int kAttRounds = MPPI_NP_ATT_ROUNDS;                         // attempts per thread, interleaved: attempt a0 + 256 r + t
+constexpr int kJTableWGs = 512;                       // table jump: chunk ranges x stream groups, about
+constexpr int kAttRounds = 8;                         // attempts per thread, interleaved: attempt a0 + 256 r + t
 constexpr int kAttPerWG = kNT * kAttRounds;
-constexpr size_t kJumpLds = (kSeqPad + 2 * kJHalf + kJPart) * sizeof(uint32_t);   // 107 KB
 
 __device__ __forceinline__ uint32_t mt_mix(uint32_t a, uint32_t b) {
     const uint32_t y = (a & kUp) | (b & kLo);
@@ -167,99 +148,6 @@ __global__ __launch_bounds__(kTT) void np_seq_kernel(const uint32_t* __restrict_
             seq[(size_t)b * kN + i] = v;
         }
         __syncthreads();   // the next twist reads this block and writes the buffer this one read
-    }
-}
-
-// stream s = blockIdx.y + 1 starts at block P s: its jump polynomial is x^(624 (P s - 1)) mod P, giving block
-// P s - 1 up to the 31 low bits of its word 0 (outside the 19937-bit state); np_gen_kernel twists once more.
-// The polynomial comes as the list of its set bits (mppi_np_set_jumps) as LDS byte offsets, split over
-// kJSplit workgroups (blockIdx.x), each list part padded to kJPart entries with the offset of kSeqPad (a window
-// of zero words past the sequence); each workgroup writes its partial XOR of every output word and
-// np_gen_kernel XORs the parts.  Per batch of kJBatch bits: the offsets (broadcast LDS reads), then every
-// window read of the batch issued together (one ds_read2st64 per bit and lane: its two output words), then XOR3s.
-__global__ __launch_bounds__(kJT) void np_jump_kernel(const uint32_t* __restrict__ seq, const uint32_t* __restrict__ bits,
-                                                      const int* __restrict__ nbits, uint32_t* __restrict__ parts) {
-    extern __shared__ uint32_t s_seq[];   // kSeqBlocks x 624 words, 640 zero words, then the list part
-    uint32_t* s_list = s_seq + kSeqPad + 2 * kJHalf;
-    {   // every load in flight before the first LDS store
-        constexpr int kVec = kSeqBlocks * kN / 4, kIt = (kVec + kJT - 1) / kJT;
-        constexpr int kLVec = kJPart / 4, kLIt = (kLVec + kJT - 1) / kJT;
-        const uint4* src = reinterpret_cast<const uint4*>(seq);
-        const uint4* lsrc = reinterpret_cast<const uint4*>(bits + (size_t)blockIdx.y * kJListStride + blockIdx.x * kJPart);
-        uint4 v[kIt], l[kLIt];
-#pragma unroll
-        for (int q = 0; q < kIt; ++q) {
-            const int i = threadIdx.x + q * kJT;
-            if (i < kVec) v[q] = src[i];
-        }
-#pragma unroll
-        for (int q = 0; q < kLIt; ++q) {
-            const int i = threadIdx.x + q * kJT;
-            if (i < kLVec) l[q] = lsrc[i];
-        }
-#pragma unroll
-        for (int q = 0; q < kIt; ++q) {
-            const int i = threadIdx.x + q * kJT;
-            if (i < kVec) reinterpret_cast<uint4*>(s_seq)[i] = v[q];
-        }
-#pragma unroll
-        for (int q = 0; q < kLIt; ++q) {
-            const int i = threadIdx.x + q * kJT;
-            if (i < kLVec) reinterpret_cast<uint4*>(s_list)[i] = l[q];
-        }
-        for (int i = threadIdx.x; i < 2 * kJHalf; i += kJT) s_seq[kSeqPad + i] = 0u;
-    }
-    const int nb = min(max(nbits[blockIdx.y] - (int)blockIdx.x * kJPart, 0), kJPart);   // a multiple of kJBatch
-    __syncthreads();
-    // kJGroups groups of kJHalf lanes, each a contiguous share of the list part; lane t of a group: output words
-    // t and t + 320 (< 624), read as one ds_read2st64_b32 (offset1 = 5 x 64 words); the window offsets come
-    // from the list in LDS (broadcast reads, in order with the window reads: no scalar load's wait couples to
-    // them); the groups' XORs meet in LDS at the end
-    const int grp = threadIdx.x / kJHalf, t = threadIdx.x - grp * kJHalf;
-    const int per = (nb / kJBatch + kJGroups - 1) / kJGroups * kJBatch;
-    const int b0 = grp * per, b1 = min(b0 + per, nb);
-    const uint32_t jb = 4u * t;
-    const uint4* L = reinterpret_cast<const uint4*>(s_list);
-    const char* S = reinterpret_cast<const char*>(s_seq);
-    uint32_t lo = 0, hi = 0;
-    for (int b = b0; b < b1; b += kJBatch) {
-        uint32_t d[kJBatch];
-#pragma unroll
-        for (int q = 0; q < kJBatch / 4; ++q) {
-            const uint4 e = L[b / 4 + q];
-            d[4 * q] = e.x;
-            d[4 * q + 1] = e.y;
-            d[4 * q + 2] = e.z;
-            d[4 * q + 3] = e.w;
-        }
-        uint32_t r[kJBatch], h[kJBatch];
-#pragma unroll
-        for (int q = 0; q < kJBatch; ++q) {
-            const char* a = S + (d[q] + jb);
-            r[q] = *reinterpret_cast<const uint32_t*>(a);
-            h[q] = *reinterpret_cast<const uint32_t*>(a + 4 * kJHalf);
-        }
-#pragma unroll
-        for (int q = 0; q < kJBatch; q += 2) {
-            lo = lo ^ r[q] ^ r[q + 1];
-            hi = hi ^ h[q] ^ h[q + 1];
-        }
-    }
-    __syncthreads();   // every group is done with the sequence: its first words hold the groups' results
-    if (grp > 0) {
-        s_seq[(grp - 1) * 2 * kJHalf + t] = lo;
-        s_seq[(grp - 1) * 2 * kJHalf + kJHalf + t] = hi;
-    }
-    __syncthreads();
-    if (grp == 0) {
-#pragma unroll
-        for (int g = 1; g < kJGroups; ++g) {
-            lo ^= s_seq[(g - 1) * 2 * kJHalf + t];
-            hi ^= s_seq[(g - 1) * 2 * kJHalf + kJHalf + t];
-        }
-        uint32_t* out = parts + ((size_t)blockIdx.y * kJSplit + blockIdx.x) * kN;
-        out[t] = lo;
-        if (t + kJHalf < kN) out[t + kJHalf] = hi;
     }
 }
 
@@ -414,11 +302,8 @@ __device__ long long look_back(unsigned long long* look, long long w, unsigned l
 // LDS, then written through the transform in the engine's layout row by row: for each step t, the workgroup's
 // samples are contiguous there, so consecutive threads write consecutive addresses (written straight from the
 // attempts, every lane of a wave hit its own row: one cache line per 8 bytes).
-#ifndef MPPI_NP_WRITE_WAVES
-#define MPPI_NP_WRITE_WAVES 4
-#endif
 // at most 128 VGPRs: four waves per SIMD (130 gave three)
-__global__ __launch_bounds__(kNT) __attribute__((amdgpu_waves_per_eu(MPPI_NP_WRITE_WAVES))) void np_write_kernel(const uint32_t* __restrict__ words, long long base, long long A,
+__global__ __launch_bounds__(kNT) __attribute__((amdgpu_waves_per_eu(4))) void np_write_kernel(const uint32_t* __restrict__ words, long long base, long long A,
                                                        unsigned long long* __restrict__ look,
                                                        unsigned long long epoch, const double* __restrict__ logd,
                                                        NpShape sh, long long pairs, long long n, int o, double cached,
@@ -577,12 +462,10 @@ struct mppi_np_ctx {
     double* d_log = nullptr;
     uint32_t* d_key = nullptr;      // the draw's starting key array
     uint32_t* d_seq = nullptr;      // kSeqBlocks blocks
-    uint32_t* d_bits = nullptr;     // (streams - 1) jump polynomials of block stride P, as set-bit byte offsets
-    int* d_nbits = nullptr;
     int poly_P = 0, poly_streams = 0;
     uint32_t* d_nibs = nullptr;     // table jump: the polynomials' 4-bit chunks, [chunk][group][4 words]
     int jG = 0, jR = 0, jcpw = 0;   // table jump: stream groups, chunk ranges, chunks per range
-    int jparts = kJSplit;           // partial XORs per stream that np_gen_kernel combines
+    int jparts = 1;                 // partial XORs per stream that np_gen_kernel combines
     uint32_t* d_jumped = nullptr;
     uint32_t* d_words = nullptr;
     size_t words_cap = 0;           // words
@@ -612,11 +495,11 @@ struct Plan {
 
 // attempts generated: 4/3 of the pairs plus 4096 (acceptance pi/4: 1.27 attempts per pair expected), as the
 // host path (np_legacy_gauss.c); the block stride P of the streams from a cost model of the two parallel
-// phases, measured on MI355X (profiles/r15np/, profiles/r15npj/): the table jump costs ~0.48 us per stream (the
-// list jump ran in rounds of 64 streams of ~70 us), a stream twists its P blocks at ~0.38 us each (MPPI_NP_STRIDE
-// forces P, for measurements).  Config 3 (8.4 M normals, 35.9 k blocks): P = 256, 141 streams.
-constexpr double kJumpRoundUs = 70.0, kBlockUs = 0.38;   // the set-bit list jump: rounds of 64 streams
-constexpr double kJumpStreamUs = 0.48;                     // the table jump: ~linear in the streams (67.8 us for 140)
+// phases, measured on MI355X (profiles/r15np/, profiles/r15npj/): the table jump costs ~0.48 us per stream, a
+// stream twists its P blocks at ~0.38 us each (MPPI_NP_STRIDE forces P, for measurements).  Config 3 (8.4 M
+// normals, 35.9 k blocks): P = 256, 141 streams.
+constexpr double kBlockUs = 0.38;
+constexpr double kJumpStreamUs = 0.48;   // ~linear in the streams (67.8 us for 140)
 Plan make_plan(long long n, int pos, int has_gauss) {
     Plan p;
     p.need = n - (has_gauss ? 1 : 0);
@@ -630,8 +513,7 @@ Plan make_plan(long long n, int pos, int has_gauss) {
     for (int P = 16; P <= (1 << 22); P <<= 1) {
         const long long streams = (p.nblk - 1 + P - 1) / P;
         if (streams > MPPI_NP_MAX_STREAMS || (forced && P != forced)) continue;
-        const double jump = MPPI_NP_JUMP_TABLE ? (double)(streams - 1) * kJumpStreamUs
-                                               : (double)((streams - 1 + 63) / 64) * kJumpRoundUs;
+        const double jump = (double)(streams - 1) * kJumpStreamUs;
         const double cost = jump + P * kBlockUs;
         if (cost < best) {
             best = cost;
@@ -665,11 +547,6 @@ int mppi_np_ctx_create(int device, const double* log_params, mppi_np_ctx** out) 
         mppi_np_ctx_destroy(c);
         return fail(MPPI_E_HIP, std::string("mppi_np_ctx_create: ") + hipGetErrorString(e));
     }
-    if (hipFuncSetAttribute((const void*)np_jump_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
-                            (int)kJumpLds) != hipSuccess) {
-        mppi_np_ctx_destroy(c);
-        return fail(MPPI_E_HIP, "mppi_np_ctx_create: the jump kernel's LDS");
-    }
     *out = c;
     return MPPI_OK;
 }
@@ -680,8 +557,6 @@ void mppi_np_ctx_destroy(mppi_np_ctx* c) {
     (void)hipFree(c->d_log);
     (void)hipFree(c->d_key);
     (void)hipFree(c->d_seq);
-    (void)hipFree(c->d_bits);
-    (void)hipFree(c->d_nbits);
     (void)hipFree(c->d_nibs);
     (void)hipFree(c->d_jumped);
     (void)hipFree(c->d_words);
@@ -709,16 +584,12 @@ int mppi_np_set_jumps(mppi_np_ctx* c, int block_stride, int streams, const unsig
         return fail(MPPI_E_ARG, "mppi_np_set_jumps: bad stride, stream count or polynomial size");
     NP_CHECK(hipSetDevice(c->device));
     if (c->pending) NP_CHECK(hipEventSynchronize(c->done));   // the buffers may be in use by the last draw
-    (void)hipFree(c->d_bits);
-    (void)hipFree(c->d_nbits);
     (void)hipFree(c->d_nibs);
     (void)hipFree(c->d_jumped);
-    c->d_bits = nullptr;
-    c->d_nbits = nullptr;
     c->d_nibs = nullptr;
     c->d_jumped = nullptr;
     c->poly_P = c->poly_streams = 0;
-    if (streams > 1 && MPPI_NP_JUMP_TABLE) {
+    if (streams > 1) {
         const int ns = streams - 1;
         const int G = (ns + kNibS - 1) / kNibS;
         int R = std::max(1, std::min(128, (kJTableWGs + G - 1) / G));   // at most 128 parts for np_gen_kernel to XOR
@@ -745,26 +616,6 @@ int mppi_np_set_jumps(mppi_np_ctx* c, int block_stride, int streams, const unsig
         c->jR = R;
         c->jcpw = cpw;
         c->jparts = R;
-    } else if (streams > 1) {
-        const size_t ns = (size_t)(streams - 1);
-        std::vector<uint32_t> lists(ns * kJListStride, 4u * kSeqPad);
-        std::vector<int> counts(ns);
-        for (size_t q = 0; q < ns; ++q) {
-            int nb = 0;
-            for (int w = 0; w < kPolyWords; ++w)
-                for (uint64_t m = polys[q * kPolyWords + w]; m; m &= m - 1) {
-                    const int d = 64 * w + __builtin_ctzll(m);
-                    if (d >= kDeg) return fail(MPPI_E_ARG, "mppi_np_set_jumps: a polynomial of degree >= 19937");
-                    lists[q * kJListStride + nb++] = 4u * (uint32_t)d;
-                }
-            counts[q] = (nb + kJBatch - 1) / kJBatch * kJBatch;
-        }
-        NP_CHECK(hipMalloc(&c->d_bits, lists.size() * sizeof(uint32_t)));
-        NP_CHECK(hipMemcpy(c->d_bits, lists.data(), lists.size() * sizeof(uint32_t), hipMemcpyHostToDevice));
-        NP_CHECK(hipMalloc(&c->d_nbits, ns * sizeof(int)));
-        NP_CHECK(hipMemcpy(c->d_nbits, counts.data(), ns * sizeof(int), hipMemcpyHostToDevice));
-        NP_CHECK(hipMalloc(&c->d_jumped, ns * kJSplit * kN * sizeof(uint32_t)));
-        c->jparts = kJSplit;
     }
     c->poly_P = block_stride;
     c->poly_streams = streams;
@@ -811,13 +662,8 @@ int mppi_np_draw(mppi_np_ctx* c, void* stream, const mppi_np_state* st, long lon
     NP_CHECK(hipMemcpyAsync(c->d_key, c->h_key, kN * sizeof(uint32_t), hipMemcpyHostToDevice, s));
     if (p.streams > 1) {
         hipLaunchKernelGGL(np_seq_kernel, dim3(1), dim3(kTT), 0, s, c->d_key, c->d_seq);
-        if (MPPI_NP_JUMP_TABLE)
-            hipLaunchKernelGGL(np_jumpn_kernel, dim3(c->jR, c->jG), dim3(kJNT),
-                               (4 * c->jcpw + kN + 3) * sizeof(uint32_t), s, c->d_seq, c->d_nibs, c->jG, c->jcpw,
-                               p.streams - 1, c->jR, c->d_jumped);
-        else
-            hipLaunchKernelGGL(np_jump_kernel, dim3(kJSplit, p.streams - 1), dim3(kJT), kJumpLds, s, c->d_seq, c->d_bits,
-                               c->d_nbits, c->d_jumped);
+        hipLaunchKernelGGL(np_jumpn_kernel, dim3(c->jR, c->jG), dim3(kJNT), (4 * c->jcpw + kN + 3) * sizeof(uint32_t),
+                           s, c->d_seq, c->d_nibs, c->jG, c->jcpw, p.streams - 1, c->jR, c->d_jumped);
     }
     hipLaunchKernelGGL(np_gen_kernel, dim3(p.streams), dim3(kTT), 0, s, c->d_key, c->d_jumped, c->d_words, p.P,
                        (int)p.nblk, c->jparts, c->d_res);

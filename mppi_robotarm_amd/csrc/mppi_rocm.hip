@@ -146,15 +146,7 @@ __device__ __forceinline__ DynK make_dynk(const KConst& c, float cx, float cy) {
 __device__ __forceinline__ f32x2 splat(float x) { return f32x2{x, x}; }
 
 // (cos, sin) of an angle given in revolutions
-__device__ __forceinline__ f32x2 cossin_rev(float a) {
-#ifdef MPPI_ACCURATE_TRIG
-    float s, co;
-    sincosf(a * 6.283185307179586f, &s, &co);
-    return f32x2{co, s};
-#else
-    return f32x2{__builtin_amdgcn_cosf(a), __builtin_amdgcn_sinf(a)};
-#endif
-}
+__device__ __forceinline__ f32x2 cossin_rev(float a) { return f32x2{__builtin_amdgcn_cosf(a), __builtin_amdgcn_sinf(a)}; }
 
 __device__ __forceinline__ void arm_init(Arm& x, float4 x0) {
     x.Q = f32x2{x0.x, x0.y} * 0.15915494309189535f;
@@ -338,9 +330,6 @@ __global__ __launch_bounds__(NT) void rollout_kernel(
     // load shares lgkmcnt with the deferred row lookup below
     for (int i = tid; i < T + kPF; i += NT) s_ua[i] = st->ua[i < T ? i : T - 1];
     if (tid < kSlots) s_win[tid] = wrow;
-#ifdef MPPI_LAST_WAVE_RHO
-    if (tid == 0) s_flag = 0u;   // the block minimum's arrival count (MPPI_LAST_WAVE_RHO, A/B only)
-#endif
     __syncthreads();
     float4 uring[kPF];  // per-step constants (u_t, a_t), uniform
 #pragma unroll
@@ -478,34 +467,8 @@ __global__ __launch_bounds__(NT) void rollout_kernel(
         if constexpr (POLL) st_gran(slab_r, idx, v, tag);
         else st_wt(slab_r, idx, v);
     };
-#ifdef MPPI_LAST_WAVE_RHO
-    // A/B variant (DESIGN Appendix A): the block's last wave to finish publishes rho_b as soon as it has the
-    // other waves' minima (LDS arrival count), before the barrier every wave then waits at
-    double rho_b;
-    {
-        const double vw = wave_min_f64(owner ? S : INFINITY);
-        unsigned arrived = 0u;
-        if (lane == 0) {
-            sm.red[wave] = vw;
-            arrived = __hip_atomic_fetch_add(&s_flag, 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
-        }
-        arrived = (unsigned)__builtin_amdgcn_readfirstlane((int)arrived);
-        if (arrived == NT / 64 - 1 && lane == 0) {
-            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");   // the other waves' red[]
-            double r = sm.red[0];
-#pragma unroll
-            for (int w = 1; w < NT / 64; ++w) r = min_raw_f64(r, sm.red[w]);
-            publish(blockIdx.x * stride, r);
-        }
-        __syncthreads();
-        rho_b = sm.red[0];
-#pragma unroll
-        for (int w = 1; w < NT / 64; ++w) rho_b = min_raw_f64(rho_b, sm.red[w]);
-    }
-#else
     const double rho_b = block_min_f64<NT>(owner ? S : INFINITY, sm);
     if (tid == 0) publish(blockIdx.x * stride, rho_b);   // the merger's first need, out at once
-#endif
     // weights below 2^-64 of the block's best are dropped (see kMergeFloor)
     // fp64, like the reference's weights; a wave whose samples all lie below the
     // floor (exp(-44.4) = 2^-64: the usual case, S spread >> lambda) skips the exp

@@ -410,6 +410,68 @@ class RolloutEngine:
             raise ValueError(f"noise must be a contiguous fp32 {(self.T, self.K_local, 2)} tensor on {self.device}")
 
 
+def readback_workers() -> int:
+    """Host threads of a HostReadback: MPPI_READBACK_WORKERS, else this process's CPUs (OMP_NUM_THREADS when
+    set, the GPU box's share), at most 16."""
+    import os
+    env = os.environ.get("MPPI_READBACK_WORKERS")
+    if env:
+        return max(1, min(64, int(env)))
+    n = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else (os.cpu_count() or 1)
+    omp = os.environ.get("OMP_NUM_THREADS", "")
+    if omp.isdigit() and int(omp) > 0:
+        n = min(n, int(omp))
+    return max(1, min(16, n))
+
+
+class HostReadback:
+    """sampled_traj_list's read-back (control.py:135-145, include/mppi_rocm.h mppi_readback_*): the fp32 states
+    DMA'd in chunks through a page-locked ring and widened to fp64 (exact) by host threads into the caller's
+    array while the later chunks are in flight.  Half the link bytes of a device-side widening, same values."""
+
+    CHUNK = 1 << 20   # floats per chunk (4 MB; the last three 2, 1 and 0.5 MB)
+    SLOTS = 8         # ring slots (32 MB page-locked)
+    STREAMS = 2       # copy streams: a copy's start-up overlaps the one before it
+
+    def __init__(self, device: torch.device, workers: int | None = None, chunk: int | None = None,
+                 slots: int | None = None, streams: int | None = None):
+        self._lib = N.load()
+        self.device = device
+        self.workers = readback_workers() if workers is None else int(workers)
+        self.chunk = self.CHUNK if chunk is None else int(chunk)
+        self.slots = self.SLOTS if slots is None else int(slots)
+        self.streams = self.STREAMS if streams is None else int(streams)
+        rb = C.c_void_p()
+        with torch.cuda.device(device):
+            N.check(self._lib.mppi_readback_create(device.index, self.workers, self.slots, self.chunk, self.streams,
+                                                   C.byref(rb)), "mppi_readback_create")
+        self._rb = rb
+
+    def run(self, src: torch.Tensor, dst: np.ndarray) -> np.ndarray:
+        """dst[...] = src (fp32 device tensor, contiguous) widened to fp64; dst C-contiguous fp64 of the same
+        size.  Ordered after the work queued on the device's current stream; returns when dst is written."""
+        if not (src.dtype == torch.float32 and src.is_contiguous() and src.device == self.device
+                and dst.dtype == np.float64 and dst.flags.c_contiguous and dst.flags.writeable
+                and dst.size == src.numel()):
+            raise ValueError("HostReadback.run: a contiguous fp32 device tensor into a writable C-contiguous "
+                             "fp64 array of the same size")
+        N.check(self._lib.mppi_readback_run(self._rb, C.c_void_p(_raw_stream(self.device.index)),
+                                            C.c_void_p(src.data_ptr()), C.c_void_p(dst.ctypes.data), src.numel()),
+                "mppi_readback_run")
+        return dst
+
+    def close(self) -> None:
+        if getattr(self, "_rb", None):
+            self._lib.mppi_readback_destroy(self._rb)
+            self._rb = None
+
+    def __del__(self):  # pragma: no cover - best effort
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
 class NpDeviceStream:
     """The reference's noise draw (control.py:154-164: np.random.multivariate_normal on NumPy's legacy global
     RandomState) generated on the device bit for bit (include/mppi_rocm.h mppi_np_*): the MT19937 words, the
@@ -433,6 +495,8 @@ class NpDeviceStream:
         self._jumps = (0, 0)   # (block stride, streams) uploaded
         self._st = N.NpStateC()
         self._tgt = N.NpTargetC()
+        self.draws = 0      # draws queued
+        self.retries = 0    # draws that came back MPPI_E_RETRY (the caller then drew on the host)
 
     def close(self) -> None:
         if getattr(self, "_ctx", None):
@@ -474,6 +538,7 @@ class NpDeviceStream:
         for d in range(du):
             t.src[d], t.scale[d], t.mean[d] = int(src[d]), float(scale[d]), float(mean[d])
         N.check(self._lib.mppi_np_draw(self._ctx, C.c_void_p(stream), C.byref(st), n, C.byref(t)), "mppi_np_draw")
+        self.draws += 1
 
     def result(self):
         """The state the last draw leaves, as np.random.get_state()'s tuple (waits for the draw), or None when
@@ -481,7 +546,8 @@ class NpDeviceStream:
         st = self._st
         rc = self._lib.mppi_np_draw_result(self._ctx, C.byref(st))
         if rc == N.MPPI_E_RETRY:
-            return None   # too few accepted attempts (never seen): np.random untouched
+            self.retries += 1
+            return None   # too few accepted attempts or a look-back that gave up: np.random untouched
         N.check(rc, "mppi_np_draw_result")
         key = np.frombuffer(st.key, dtype=np.uint32).copy()
         return ("MT19937", key, st.pos, st.has_gauss, st.gauss)

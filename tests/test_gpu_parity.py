@@ -832,7 +832,7 @@ def test_random_configs_against_c_oracle(i, K, T, lam, lps, expl, prev, paths):
 
 
 def test_sampled_trajs_arrays_stay_the_callers_across_calls(paths):
-    """sampled_traj_list comes from pinned read-back buffers (PinnedReadback): every call's array matches the
+    """sampled_traj_list comes from pooled read-back arrays (SampledReadback): every call's array matches the
     reference's (control.py:135-145) and no later call writes into an array the caller still holds, written to
     or viewed; dropped arrays' buffers come back."""
     g = load_step("runpy_k100_t30")
@@ -848,7 +848,7 @@ def test_sampled_trajs_arrays_stay_the_callers_across_calls(paths):
         np.testing.assert_allclose(samp, g["sampled_traj"], rtol=1e-4, atol=1e-4)
         return samp
 
-    held = [call() for _ in range(5)]            # 3 pinned buffers, then plain read-backs
+    held = [call() for _ in range(5)]            # 3 pooled arrays, then fresh ones
     ref = held[0].copy()
     for i, a in enumerate(held):
         assert a.flags.writeable and a.dtype == np.float64

@@ -247,12 +247,12 @@ def test_host_nearest_waypoint_skips_nan_rows(paths):
 
 
 def test_sampled_readback_buffers_are_never_shared_with_a_live_array():
-    """sampled_traj_list comes from a pool of read-back buffers (page-locked on the GPU); a buffer is reused only
+    """sampled_traj_list comes from a pool of read-back buffers (widened on the host from a chunked fp32 DMA on the GPU); a buffer is reused only
     once the caller holds neither its array nor any view of it, so each returned array behaves as the fresh
-    np.zeros of control.py:137 (CPU tensors here: the pool logic without pinning)."""
+    np.zeros of control.py:137 (CPU tensors here: the pool logic, torch widening)."""
     import torch
-    from mppi_robotarm_amd.controller import PinnedReadback
-    rb = PinnedReadback()
+    from mppi_robotarm_amd.controller import SampledReadback
+    rb = SampledReadback()
     tr = [torch.full((6, 5, 4), float(i) + 0.25, dtype=torch.float32) for i in range(8)]
     a1 = rb(tr[1])
     assert a1.dtype == np.float64 and a1.shape == (6, 5, 4) and a1.flags.writeable and np.all(a1 == 1.25)
