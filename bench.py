@@ -297,7 +297,7 @@ def sampled_latency(K, T, device, calls=20, warm=5, noise="device"):
     return float(np.median(ts[warm:])) * 1e3, detail
 
 
-def numpy_noise_latency(K, T, device, calls=20, warm=5):
+def numpy_noise_latency(K, T, device, calls=20, warm=5, sigma=None):
     """calc_control_input back to back (ms, median) with the drop-in's default noise="numpy": the reference's
     own draw, np.random.multivariate_normal on the legacy global RNG (control.py:154-164), NumPy's values and
     state, drawn on the device (mppi_np_*, engine.NpDeviceStream; the host draw, hostrng, for other Sigmas)."""
@@ -306,6 +306,8 @@ def numpy_noise_latency(K, T, device, calls=20, warm=5):
     path = np.load(os.path.join(ROOT, "tests", "golden", "paths.npz"))["xydq_circle"][:, :4]
     kw = runpy_config()
     kw.update(number_of_samples_K=K, horizon_step_T=T, visualze_sampled_trajs=False)
+    if sigma is not None:
+        kw["sigma"] = sigma
     c = MPPIControllerForPathTracking(ref_path=path, noise="numpy", verbose=False, device=device, **kw)
     np.random.seed(0)
     ts = []
@@ -642,6 +644,8 @@ def main():
             progress("NumPy-noise leg")
             out["control_step_latency_numpy_noise_ms"], out["numpy_noise_detail"] = numpy_noise_latency(
                 K, T, local_rank)
+            out["control_step_latency_numpy_noise_general_sigma_ms"], out["numpy_noise_general_sigma_detail"] = (
+                numpy_noise_latency(K, T, local_rank, sigma=np.array([[20.0, 6.0], [6.0, 12.0]])))
             out["control_step_latency_numpy_noise_closed_loop_ms"] = numpy_noise_closed_loop(K, T, local_rank)
             out["control_step_latency_def"] = (
                 "median wall time of MPPIControllerForPathTracking.calc_control_input (drop-in, noise='device') "
@@ -658,6 +662,8 @@ def main():
                 "drop-in's default noise='numpy', the reference's own np.random.multivariate_normal stream "
                 "(NumPy's values and RNG state) drawn on the device every call (mppi_np_*): each call queues the "
                 "next call's draw beside its step, used when np.random is still where the call left it; "
+                "numpy_noise_general_sigma: numpy_noise with Sigma = [[20, 6], [6, 12]] (a full 2 x 2 transform, np.dot's "
+                "rounding pinned at run time, hostrng.dot2_model); "
                 "numpy_noise_closed_loop: the same in run.py's closed loop (100 ticks after 30). "
                 "ms_per_step is the device-resident loop")
         if world == 1 and c5:

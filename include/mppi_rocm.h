@@ -439,10 +439,15 @@ typedef struct {
 } mppi_np_state;
 
 /* Where the draw goes: the standard normals z of shape (K, T, du) (C order,
- * n = K T du of them) become out(t, k, d) = (float)(z[k][t][src[d]] * scale[d]
- * + mean[d]) (fp64 multiply and add, each rounded, as NumPy's np.dot with one
- * nonzero per column and `x += mean`; then the fp32 rounding of the upload),
- * stored at out_dev[t * stride_t + (k - k_offset) * stride_k + d * stride_d]
+ * n = K T du of them) become out(t, k, d) = (float)(x + mean[d]) with
+ *   dot2 = 0: x = z[k][t][src[d]] * scale[d] (NumPy's np.dot when its matrix
+ *             has one nonzero per column: the other products are exact zeros),
+ *   dot2 = 1 (du = 2, any matrix): x = fma(z[k][t][1], mat[2 + d],
+ *             z[k][t][0] * mat[d]) — np.dot(z, mat) as the host BLAS rounds a
+ *             2-term product (pinned on the host at run time, hostrng.dot2_model),
+ * (fp64, each operation rounded as NumPy's, `x += mean`; then the fp32
+ * rounding of the upload), stored at
+ * out_dev[t * stride_t + (k - k_offset) * stride_k + d * stride_d]
  * for the samples k_offset <= k < k_offset + K_local of this rank (every rank
  * draws the whole stream, as every rank of the reference's loop would). */
 typedef struct {
@@ -454,6 +459,8 @@ typedef struct {
     int src[MPPI_NP_MAX_DU];
     double scale[MPPI_NP_MAX_DU];
     double mean[MPPI_NP_MAX_DU];
+    int dot2;                 /* 1: the general 2 x 2 transform mat (row-major, z @ mat) */
+    double mat[4];
 } mppi_np_target;
 
 typedef struct mppi_np_ctx mppi_np_ctx;

@@ -72,7 +72,8 @@ class NpTargetC(C.Structure):
     _fields_ = [("out_dev", C.c_void_p), ("K", C.c_longlong), ("T", C.c_longlong), ("du", C.c_int),
                 ("k_offset", C.c_longlong), ("K_local", C.c_longlong), ("stride_t", C.c_longlong),
                 ("stride_k", C.c_longlong), ("stride_d", C.c_longlong), ("src", C.c_int * NP_MAX_DU),
-                ("scale", C.c_double * NP_MAX_DU), ("mean", C.c_double * NP_MAX_DU)]
+                ("scale", C.c_double * NP_MAX_DU), ("mean", C.c_double * NP_MAX_DU), ("dot2", C.c_int),
+                ("mat", C.c_double * 4)]
 
 
 class ArmParamsC(C.Structure):

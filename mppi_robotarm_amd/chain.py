@@ -409,7 +409,7 @@ class ChainMPPIController:
         self._npre = None              # (start state, spec, buffer) of the next call's draw, queued beside a step
         self._np_spec = None           # (spec, plan) of this call's device draw
         self._np_left = None           # the state it left np.random in
-        self._np_plan = None           # (Sigma bytes, dtype, hostrng.monomial_plan) of the last draw
+        self._np_plan = None           # (Sigma bytes, dtype, hostrng.device_plan) of the last draw
         self._npre_used = 0            # calls that used the queued draw
         self._np_stream = None         # the stream of the queued draws
         self._np_ev = None
@@ -503,11 +503,15 @@ class ChainMPPIController:
             self.prev_waypoints_idx = nearest_idx
         return nearest_idx
 
+    def _custom_epsilon(self) -> bool:
+        """_calc_epsilon replaced on the instance or a subclass: the caller's noise, not the reference's draw."""
+        return "_calc_epsilon" in self.__dict__ or type(self)._calc_epsilon is not ChainMPPIController._calc_epsilon
+
     def _reference_noise(self):
         """control.py:84 as MPPIControllerForPathTracking._reference_noise: the standard normals into a
         page-locked buffer and the transform on the device when Sigma allows it (the chain's diagonal Sigma
         does), else _calc_epsilon's array."""
-        if "_calc_epsilon" in self.__dict__ or type(self)._calc_epsilon is not ChainMPPIController._calc_epsilon:
+        if self._custom_epsilon():
             return self._calc_epsilon(self.Sigma, self.K, self.T, self.dim_u)
         sigma = self.Sigma
         if sigma.shape[0] != sigma.shape[1] or sigma.shape[0] != self.dim_u or self.dim_u < 1:
@@ -559,7 +563,7 @@ class ChainMPPIController:
         from .controller import DeviceDrawn, MPPIControllerForPathTracking as _C
         if not self.numpy_noise_on_device or self._npdev is False:
             return self._drop_predraw()
-        if "_calc_epsilon" in self.__dict__ or type(self)._calc_epsilon is not ChainMPPIController._calc_epsilon:
+        if self._custom_epsilon():
             return self._drop_predraw()
         sig = self.Sigma
         if not (isinstance(sig, np.ndarray) and sig.shape == (self.dim_u, self.dim_u)):
@@ -572,7 +576,7 @@ class ChainMPPIController:
             return self._drop_predraw()
         sb = sig.tobytes()
         if self._np_plan is None or self._np_plan[0] != sb or self._np_plan[1] != sig.dtype:
-            self._np_plan = (sb, sig.dtype, hostrng.monomial_plan(np.zeros(self.dim_u), sig))
+            self._np_plan = (sb, sig.dtype, hostrng.device_plan(np.zeros(self.dim_u), sig))
         plan = self._np_plan[2]
         if plan is None:
             return self._drop_predraw()
@@ -615,7 +619,7 @@ class ChainMPPIController:
             return None
         np.random.set_state(new)
         self._np_left = new
-        d = DeviceDrawn(float(np.sum(new[1][:16], dtype=np.float64)) + new[2])
+        d = DeviceDrawn()
         d.buf = self._noise_dev
         return d
 
@@ -701,7 +705,7 @@ class ChainMPPIController:
         world, _ = self._shard()
         S_out = self._S_dev if self.keep_costs else None
         if world > 1 and self._xmode is None:
-            self._multi_setup(eng, _noise_check(epsilon, self.K, self.T, self.dim_u))
+            self._multi_setup(eng, _noise_check(self, epsilon))
         self.last_precision = prec
         if self.T >= 5 and not self.visualze_sampled_trajs and (world == 1 or self._xmode == "launch"):
             # the update of control.py:120-149 inside the launch (the median of 10 is a selection and the

@@ -86,20 +86,21 @@ def _pinned_zbuf(buf, ev, n: int):
 
 class DeviceDrawn:
     """The reference's draw (control.py:84) made on the device straight into the engine's noise buffer
-    (engine.NpDeviceStream); `check` is the value the ranks compare (from the RNG state the draw left)."""
-
-    def __init__(self, check: float):
-        self.check = check
+    (engine.NpDeviceStream)."""
 
 
-def _noise_check(epsilon, K: int, T: int, du: int):
-    """The value the ranks compare to agree on the noise stream: eps[0, 0, 0] + eps[-1, -1, -1] of the draw
-    (an array, a hostrng.StdNoise, or None for device noise), or the device draw's state check."""
-    if epsilon is None:
+def _noise_check(ctrl, epsilon):
+    """The value the ranks compare at their first step to agree on the noise stream.  The reference's own draw
+    (NumPy's global RNG, control.py:163): the RNG state it left, which the device draw and the host draw leave
+    alike, so a rank that fell back to the host draw still agrees with one that drew on the device; a replaced
+    _calc_epsilon: eps[0, 0, 0] + eps[-1, -1, -1] of its array; device noise: None (the seed is compared)."""
+    if ctrl.noise_source != "numpy" or epsilon is None:
         return None
-    if isinstance(epsilon, DeviceDrawn):
-        return epsilon.check
+    if not ctrl._custom_epsilon():
+        st = np.random.get_state()
+        return (float(np.sum(np.asarray(st[1][:16], dtype=np.float64))), int(st[2]), int(st[3]), float(st[4]))
     if isinstance(epsilon, hostrng.StdNoise):
+        K, T, du = epsilon.z.shape
         return epsilon.eps(0, 0, 0) + epsilon.eps(K - 1, T - 1, du - 1)
     return float(epsilon[0, 0, 0] + epsilon[-1, -1, -1])
 
@@ -236,7 +237,7 @@ class MPPIControllerForPathTracking:
         self._npre = None              # (start state, spec) of the next call's draw, queued at the end of a call
         self._np_spec = None           # (spec, plan) of this call's device draw
         self._npre_used = 0            # calls that used the queued draw
-        self._np_plan = None           # (Sigma bytes, dtype, hostrng.monomial_plan) of the last draw
+        self._np_plan = None           # (Sigma bytes, dtype, hostrng.device_plan) of the last draw
         self._np_left = None           # the state this call's draw left np.random in
         self._noise_alt = None         # the second noise buffer: the queued draw writes it while a step reads the other
         self._np_stream = None         # the stream of the queued draws (concurrent with the step)
@@ -420,7 +421,7 @@ class MPPIControllerForPathTracking:
             return self._dropin_step(eng, x0, window, u)
         eng.set_step_inputs(np.asarray(x0, dtype=np.float64), window, u)
         if world > 1 and self._xmode is None:
-            check = _noise_check(epsilon, self.K, self.T, self.dim_u)
+            check = _noise_check(self, epsilon)
             self._multi_setup(eng, check)
         if not self.host_update:
             return self._fused_step(eng, x0, u, world, predraw=isinstance(epsilon, DeviceDrawn) and world == 1)
@@ -615,6 +616,11 @@ class MPPIControllerForPathTracking:
             print("[ERROR] sigma must be a square matrix with the size of size_dim_u.")
             raise ValueError
 
+    def _custom_epsilon(self) -> bool:
+        """_calc_epsilon replaced on the instance or a subclass: the caller's noise, not the reference's draw."""
+        cls = MPPIControllerForPathTracking
+        return "_calc_epsilon" in self.__dict__ or type(self)._calc_epsilon is not cls._calc_epsilon
+
     def _reference_noise(self):
         """control.py:84, the reference's draw on the legacy global RNG.  When _calc_epsilon is the reference's
         (not replaced on the instance or a subclass) and Sigma's transform is a scaled column permutation
@@ -622,8 +628,7 @@ class MPPIControllerForPathTracking:
         buffer that goes to the device in one DMA, where the same fp64 multiply and add make the noise
         (hostrng.multivariate_normal_std, engine.upload_std_noise) instead of NumPy's np.dot and `x += mean`
         over the 67 MB draw and a pageable copy.  Otherwise _calc_epsilon's array."""
-        cls = MPPIControllerForPathTracking
-        if "_calc_epsilon" in self.__dict__ or type(self)._calc_epsilon is not cls._calc_epsilon:
+        if self._custom_epsilon():
             return self._calc_epsilon(self.Sigma, self.K, self.T, self.dim_u)
         self._check_sigma(self.Sigma, self.dim_u)
         std = hostrng.multivariate_normal_std(np.full((self.dim_u), 0.0), self.Sigma, (self.K, self.T),
@@ -675,14 +680,14 @@ class MPPIControllerForPathTracking:
         """control.py:84 on the device: the reference's own stream (np.random.multivariate_normal on the legacy
         global RNG, NumPy's values and the state it leaves) drawn straight into the engine's noise buffer
         (engine.NpDeviceStream, include/mppi_rocm.h mppi_np_*), when _calc_epsilon is the reference's and Sigma's
-        transform is a scaled column permutation (run.py's 20 I).  None: not applicable here (the host path
+        transform is a scaled column permutation (run.py's 20 I) or, for the 2-link arm, any matrix whose np.dot
+        rounding hostrng.dot2_model pins.  None: not applicable here (the host path
         draws then; nothing was drawn).  A singular Sigma takes the host path too, which draws before
         np.linalg.inv raises, as control.py:84,106 do.  The draw the last call queued is waited for only after
         these checks (they run while it does), and used when it started from NumPy's current state."""
         if not self.numpy_noise_on_device or self._npdev is False:
             return self._drop_predraw()
-        cls = MPPIControllerForPathTracking
-        if "_calc_epsilon" in self.__dict__ or type(self)._calc_epsilon is not cls._calc_epsilon:
+        if self._custom_epsilon():
             return self._drop_predraw()
         sig = self.Sigma
         if not (isinstance(sig, np.ndarray) and sig.shape == (self.dim_u, self.dim_u)):
@@ -695,7 +700,7 @@ class MPPIControllerForPathTracking:
             return self._drop_predraw()
         sb = sig.tobytes()
         if self._np_plan is None or self._np_plan[0] != sb or self._np_plan[1] != sig.dtype:
-            self._np_plan = (sb, sig.dtype, hostrng.monomial_plan(np.full((self.dim_u), 0.0), sig))
+            self._np_plan = (sb, sig.dtype, hostrng.device_plan(np.full((self.dim_u), 0.0), sig))
         plan = self._np_plan[2]
         if plan is None:
             return self._drop_predraw()
@@ -736,7 +741,7 @@ class MPPIControllerForPathTracking:
             return None
         np.random.set_state(new)
         self._np_left = new
-        return DeviceDrawn(float(np.sum(new[1][:16], dtype=np.float64)) + new[2])
+        return DeviceDrawn()
 
     def _zbuf_numpy(self, n: int) -> np.ndarray:
         """The page-locked buffer of the standard normals (>= n values), free to be rewritten: the DMA of the

@@ -19,8 +19,9 @@
 //                    by look-back over its predecessors' published counts (one pass, no separate count and
 //                    scan); each accepted pair's place from it; f with glibc's log
 //                    reproduced (np_glibc_log.h), IEEE division and square root; the transform of the drop-in
-//                    (a scaled column permutation, hostrng.monomial_transform) and the rounding to fp32, into
-//                    the engine's noise layout for this rank's samples.
+//                    (a scaled column permutation, hostrng.monomial_transform, or for du = 2 any matrix through
+//                    the host BLAS's 2-term rounding, hostrng.dot2_model) and the rounding to fp32, into the
+//                    engine's noise layout for this rank's samples.
 //   np_state_kernel  the state NumPy leaves: the key array holding the last consumed word, its position, and
 //                    the cached Gaussian of an odd count.
 //
@@ -129,6 +130,8 @@ struct NpShape {
     long long st, sk, sd;       // out element (t, k - k_offset, d)
     int src[MPPI_NP_MAX_DU];
     double scale[MPPI_NP_MAX_DU], mean[MPPI_NP_MAX_DU];
+    int dot2;                   // du = 2, a general transform: x_d = fma(z1, mat[2 + d], z0 mat[d]) (mppi_np_target)
+    double mat[4];
 };
 
 // ------------------------------------------------------------------ generation
@@ -312,6 +315,7 @@ __global__ __launch_bounds__(kNT) __attribute__((amdgpu_waves_per_eu(4))) void n
     __shared__ int s_cnt[kAttRounds][kNT / 64];
     __shared__ long long s_qw;
     __shared__ double s_z[2 * kAttPerWG];
+    __shared__ double s_next;   // dot2: the normal after this workgroup's (the next accepted pair's f x2)
     for (int i = threadIdx.x; i < NPLOG_NDATA; i += kNT) s_log[i] = logd[i];
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     const long long a0 = (long long)blockIdx.x * kAttPerWG + threadIdx.x;
@@ -399,6 +403,21 @@ __global__ __launch_bounds__(kNT) __attribute__((amdgpu_waves_per_eu(4))) void n
             l0 += round;
         }
     }
+    // dot2: a step's two normals may straddle two workgroups; the workgroup holding the first writes the step,
+    // and the second is then the next workgroup's first normal: its first accepted attempt's f x2, recomputed
+    // here with the same operations (one or two attempts past this workgroup's, acceptance pi / 4)
+    if (sh.dot2) {   // uniform
+        if (threadIdx.x == 0 && q0 < pairs) {
+            double y1 = 0.0, y2 = 0.0, rr = 2.0;
+            for (long long a = (w + 1) * (long long)kAttPerWG; a < A; ++a) {
+                attempt(words, base, a, y1, y2, rr);
+                if (accepted(rr)) break;
+            }
+            const double r2 = y1 * y1 + y2 * y2;   // as attempt()
+            s_next = y2 * sqrt(-2.0 * np_glibc_log(s_log, r2) / r2);
+        }
+        __syncthreads();
+    }
     // normals [m0, m1) of this workgroup: pairs [qw, q0) below `pairs`; the cached Gaussian (m = 0) comes first
     const long long zb = o + 2 * qw;   // normal of s_z[0]
     const long long m0 = blockIdx.x == 0 ? 0 : zb;
@@ -424,14 +443,17 @@ __global__ __launch_bounds__(kNT) __attribute__((amdgpu_waves_per_eu(4))) void n
             d = j - kk * du;
         }
         const long long k = s_lo + kk;
-        long long m = k * sh.per_k + sh.src[d] + (long long)g0 * du;
+        // dot2: m is the step's first normal (the step is this workgroup's when m is in its range)
+        long long m = k * sh.per_k + (sh.dot2 ? 0 : sh.src[d]) + (long long)g0 * du;
         float* op = sh.out + (k - sh.k_offset) * sh.sk + (long long)d * sh.sd + (long long)g0 * sh.st;
-        const double sc = sh.scale[d], mu = sh.mean[d];
+        const double sc = sh.dot2 ? sh.mat[d] : sh.scale[d], mu = sh.mean[d], sc1 = sh.mat[2 + (d & 1)];
         const long long dm = (long long)G * du, dop = (long long)G * sh.st;
         for (unsigned t = g0; t < nt; t += G, m += dm, op += dop) {
             if (m < m0 || m >= m1) continue;
             const double z = m < zb ? cached : s_z[m - zb];
-            *op = (float)(z * sc + mu);
+            double x = z * sc;
+            if (sh.dot2) x = fma(m + 1 < m1 ? s_z[m + 1 - zb] : s_next, sc1, x);   // np.dot's 2-term rounding
+            *op = (float)(x + mu);
         }
     }
 }
@@ -630,7 +652,8 @@ int mppi_np_draw(mppi_np_ctx* c, void* stream, const mppi_np_state* st, long lon
         tgt->k_offset < 0 || tgt->K_local < 0 || tgt->k_offset + tgt->K_local > tgt->K)
         return fail(MPPI_E_ARG, "mppi_np_draw: the target's (K, T, du) and slice must match n");
     for (int d = 0; d < tgt->du; ++d)
-        if (tgt->src[d] < 0 || tgt->src[d] >= tgt->du) return fail(MPPI_E_ARG, "mppi_np_draw: bad src");
+        if (!tgt->dot2 && (tgt->src[d] < 0 || tgt->src[d] >= tgt->du)) return fail(MPPI_E_ARG, "mppi_np_draw: bad src");
+    if (tgt->dot2 && tgt->du != 2) return fail(MPPI_E_ARG, "mppi_np_draw: dot2 needs du = 2");
     const Plan p = make_plan(n, st->pos, st->has_gauss);
     if (p.P != c->poly_P || p.streams > c->poly_streams)
         return fail(MPPI_E_ARG, "mppi_np_draw: the jump polynomials of mppi_np_plan's stride and count are not set");
@@ -676,6 +699,8 @@ int mppi_np_draw(mppi_np_ctx* c, void* stream, const mppi_np_state* st, long lon
     sh.st = tgt->stride_t;
     sh.sk = tgt->stride_k;
     sh.sd = tgt->stride_d;
+    sh.dot2 = tgt->dot2 ? 1 : 0;
+    for (int i = 0; i < 4; ++i) sh.mat[i] = tgt->mat[i];
     for (int d = 0; d < MPPI_NP_MAX_DU; ++d) {
         sh.src[d] = d < tgt->du ? tgt->src[d] : 0;
         sh.scale[d] = d < tgt->du ? tgt->scale[d] : 0.0;

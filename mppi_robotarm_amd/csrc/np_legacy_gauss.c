@@ -255,7 +255,9 @@ static int char_poly_init(void) {
 // a (bits 0 .. 2 MT_DEG, 2 PW words) reduced mod P in place: each set bit i >= MT_DEG is replaced by the
 // terms of P below x^MT_DEG shifted by i - MT_DEG (the leading term cancels it).  A word at a time, top down:
 // P's highest term below x^MT_DEG is x^19314 (623 below), so the bits a word's high part maps to lie at least
-// 623 positions lower, in words not yet visited (checked when P is found: g_cp.gap).
+// 623 positions lower, in words not yet visited (checked when P is found: MT_DEG - top > 64).  In the lowest
+// word (w0 = 311) only bits >= 33 are set, so a term below 33 lands at a negative word offset pos: its low half
+// (q = -1) is all zero and skipped, its high half goes to word 0.
 static void reduce_mod(uint64_t* a) {
     const int64_t w0 = MT_DEG >> 6;
     for (int64_t w = (2 * MT_DEG) >> 6; w >= w0; --w) {
@@ -267,7 +269,7 @@ static void reduce_mod(uint64_t* a) {
             const int64_t pos = 64 * w - MT_DEG + g_cp.terms[e];
             const int64_t q = pos >> 6;
             const int sh = (int)(pos & 63);
-            a[q] ^= v << sh;
+            if (q >= 0) a[q] ^= v << sh;
             if (sh) a[q + 1] ^= v >> (64 - sh);
         }
     }
@@ -747,4 +749,16 @@ int64_t mppi_np_log_mismatches(const double* D, const double* x, int64_t n) {
         bad += memcmp(&a, &b, 8) != 0;
     }
     return bad;
+}
+
+// np.dot(z, M) of an (n, 2) by (2, 2) product as one candidate rounding of the host BLAS: out[i][j] =
+// fma(z[i][1], M[1][j], z[i][0] * M[0][j]) (the product z0 M0j rounded, the second term fused into it: OpenBLAS's
+// dgemm kernels accumulate k = 0, 1 with FMAs from a zero accumulator).  hostrng.dot2_model compares it with
+// np.dot bit for bit at run time before the device draw applies the same operations (mppi_npgauss.hip).
+void mppi_np_dot2_fma(const double* z, int64_t n, const double* M, double* out) {
+    for (int64_t i = 0; i < n; ++i)
+        for (int j = 0; j < 2; ++j) {
+            const double p = z[2 * i] * M[j];
+            out[2 * i + j] = fma(z[2 * i + 1], M[2 + j], p);
+        }
 }

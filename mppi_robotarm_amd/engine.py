@@ -475,7 +475,7 @@ class HostReadback:
 class NpDeviceStream:
     """The reference's noise draw (control.py:154-164: np.random.multivariate_normal on NumPy's legacy global
     RandomState) generated on the device bit for bit (include/mppi_rocm.h mppi_np_*): the MT19937 words, the
-    polar method with glibc's log, the Sigma transform (a scaled column permutation) and the fp32 rounding,
+    polar method with glibc's log, the Sigma transform (a scaled column permutation, or a 2 x 2 matrix through np.dot's pinned rounding) and the fp32 rounding,
     straight into an engine's noise buffer; the RNG state is read from and written back to np.random, as
     NumPy's own draw leaves it.  One per device; raises RuntimeError at construction when the host pieces it
     needs (hostrng.log_params, hostrng.jump_polys) are unavailable."""
@@ -511,7 +511,7 @@ class NpDeviceStream:
 
     def draw(self, state, shape, plan, out: torch.Tensor, stream, k_offset: int, K_local: int, strides) -> None:
         """Queue the draw of the (K, T, du) standard normals `shape` from `state` (np.random.get_state()) through
-        `plan` (hostrng.monomial_plan: src, scale, mean) into `out` (fp32 device), samples [k_offset, k_offset +
+        `plan` (hostrng.device_plan: src, scale, mean, psd, mat) into `out` (fp32 device), samples [k_offset, k_offset +
         K_local) at strides (t, k, d); result() returns the state it leaves."""
         from . import hostrng
         K, T, du = shape
@@ -537,6 +537,11 @@ class NpDeviceStream:
         src, scale, mean = plan[:3]
         for d in range(du):
             t.src[d], t.scale[d], t.mean[d] = int(src[d]), float(scale[d]), float(mean[d])
+        mat = plan[4] if len(plan) > 4 else None   # hostrng.device_plan: a general 2 x 2 transform
+        t.dot2 = 0 if mat is None else 1
+        if mat is not None:
+            for i, v in enumerate(np.asarray(mat, dtype=np.float64).ravel()):
+                t.mat[i] = float(v)
         N.check(self._lib.mppi_np_draw(self._ctx, C.c_void_p(stream), C.byref(st), n, C.byref(t)), "mppi_np_draw")
         self.draws += 1
 

@@ -32,6 +32,8 @@ def _load():
         lib.mppi_np_poly_words.restype = C.c_int
         lib.mppi_np_log_mismatches.restype = C.c_int64
         lib.mppi_np_log_mismatches.argtypes = [C.c_void_p, C.c_void_p, C.c_int64]
+        lib.mppi_np_dot2_fma.restype = None
+        lib.mppi_np_dot2_fma.argtypes = [C.c_void_p, C.c_int64, C.c_void_p, C.c_void_p]
         _lib = lib
     return _lib
 
@@ -133,6 +135,59 @@ def multivariate_normal(mean, cov, size) -> np.ndarray:
     x += mean
     x.shape = tuple(final_shape)
     return x
+
+
+_dot2_cache = {}
+
+
+def dot2_model(m: np.ndarray) -> bool:
+    """Whether this process's np.dot rounds an (n, 2) @ (2, 2) float64 product `z @ m` as
+    fma(z1, m[1, j], z0 * m[0, j]) (np_legacy_gauss.c mppi_np_dot2_fma) — the operations the device draw applies
+    for a general 2 x 2 transform (mppi_npgauss.hip, mppi_np_target.dot2).  The host BLAS picks its kernel at run
+    time (CPU type, problem size), so it is pinned here, the way the log constants are: np.dot against the C
+    model bit for bit on 4096 and 2^19 rows of standard normals (both sides of OpenBLAS's small-matrix limit,
+    M N K = 10^6), and through the same product NumPy's draw makes (a C-contiguous (n, 2) float64 array times
+    this m).  Cached per matrix."""
+    m = np.ascontiguousarray(m, dtype=np.float64)
+    key = m.tobytes()
+    hit = _dot2_cache.get(key)
+    if hit is None:
+        lib = _load()
+        hit = False
+        if lib is not None and m.shape == (2, 2) and np.all(np.isfinite(m)):
+            z = np.random.default_rng(0x5EED).standard_normal(1 << 20).reshape(-1, 2)
+            ok = True
+            for rows in (4096, 1 << 19):
+                zz = np.ascontiguousarray(z[:rows])
+                want = np.dot(zz, m)
+                got = np.empty_like(want)
+                lib.mppi_np_dot2_fma(zz.ctypes.data, rows, m.ctypes.data, got.ctypes.data)
+                ok = ok and np.array_equal(want.view(np.uint64), got.view(np.uint64))
+            hit = bool(ok)
+        _dot2_cache[key] = hit
+    return hit
+
+
+def device_plan(mean, cov):
+    """The device draw's transform of multivariate_normal (NumPy's svd of cov and its positive-semidefinite test,
+    without the warning): (src, scale, mean, psd, mat) with mat None for a scaled column permutation
+    (monomial_plan), or for du = 2 the whole matrix sqrt(s)[:, None] * v when dot2_model pins np.dot's rounding
+    of it (src and scale then unused); None otherwise (the host draws)."""
+    plan = monomial_plan(mean, cov)
+    if plan is not None:
+        return plan + (None,)
+    mean = np.array(mean)
+    cov = np.array(cov)
+    if len(mean.shape) != 1 or cov.shape != (2, 2) or mean.shape[0] != 2:
+        return None
+    cov = cov.astype(np.double)
+    (u, s, v) = np.linalg.svd(cov)
+    m = np.sqrt(s)[:, None] * v
+    if not dot2_model(m):
+        return None
+    psd = np.allclose(np.dot(v.T * s, v), cov, rtol=1e-8, atol=1e-8)
+    return (np.arange(2, dtype=np.int64), np.ones(2), mean.astype(np.float64), bool(psd),
+            np.ascontiguousarray(m, dtype=np.float64))
 
 
 def monomial_plan(mean, cov):

@@ -86,17 +86,19 @@ int main(void) {
                     Cc.precision.offset, N.CHAIN_MAX_DOF]
 
 
-def test_dropin_binding_layout_matches_header(tmp_path):
+@pytest.mark.parametrize("cname,pyname", [("mppi_dropin_binding", "DropinBindingC"), ("mppi_np_state", "NpStateC"),
+                                          ("mppi_np_target", "NpTargetC")])
+def test_struct_layout_matches_header(tmp_path, cname, pyname):
     from mppi_robotarm_amd import _native as N
-    probe = tmp_path / "probe_bind.c"
-    fields = [f for f, _ in N.DropinBindingC._fields_]
+    probe = tmp_path / f"probe_{cname}.c"
+    B = getattr(N, pyname)
+    fields = [f for f, _ in B._fields_]
     probe.write_text("#include <stddef.h>\n#include <stdio.h>\n#include \"mppi_rocm.h\"\nint main(void) {\n"
-                     + "".join(f'  printf("%zu ", offsetof(mppi_dropin_binding, {f}));\n' for f in fields)
-                     + '  printf("%zu\\n", sizeof(mppi_dropin_binding));\n  return 0;\n}\n')
-    exe = tmp_path / "probe_bind"
+                     + "".join(f'  printf("%zu ", offsetof({cname}, {f}));\n' for f in fields)
+                     + f'  printf("%zu\\n", sizeof({cname}));\n  return 0;\n}}\n')
+    exe = tmp_path / f"probe_{cname}"
     subprocess.run(["gcc", "-I", os.path.dirname(HEADER), str(probe), "-o", str(exe)], check=True)
     vals = [int(v) for v in subprocess.run([str(exe)], capture_output=True, text=True, check=True).stdout.split()]
-    B = N.DropinBindingC
     assert vals == [getattr(B, f).offset for f in fields] + [C.sizeof(B)]
 
 

@@ -198,6 +198,27 @@ def _late_rank_chain(pg, exchange):
     return out
 
 
+def _mixed_draw(pg, exchange):
+    """The drop-in's default NumPy noise with rank 1 on the host draw (numpy_noise_on_device=False) and rank 0
+    on the device draw: the ranks' first-step check compares the RNG state each draw leaves (the same for both),
+    so they agree and take the in-launch exchange; the steps equal the single-process controller's."""
+    from mppi_robotarm_amd.controller import MPPIControllerForPathTracking
+    g, paths = load_loop("k64_t20"), load_paths()
+    rank = pg.rank() if pg is not None else 0
+    c = MPPIControllerForPathTracking(delta_t=0.006, ref_path=paths["xydq_circle"], horizon_step_T=DEV_T,
+                                      number_of_samples_K=DEV_K, verbose=False, process_group=pg, exchange=exchange,
+                                      numpy_noise_on_device=rank == 0, **RUNPY)
+    np.random.seed(17)
+    useq = []
+    for i in range(3):
+        _, u_seq, _, _ = c.calc_control_input(g["states"][i])
+        useq.append(u_seq.copy())
+    out = dict(u_seq=np.array(useq), rng=np.random.get_state()[1][:8].astype(np.int64), xmode=str(c._xmode),
+               rankonly_devdraw=bool(c._npdev))
+    c.close()
+    return out
+
+
 SCENARIOS = {
     "step_auto": (_step_runpy, "auto"), "step_rccl": (_step_runpy, "rccl"),
     "loop_auto": (_loop, "auto"),
@@ -207,6 +228,7 @@ SCENARIOS = {
     "chainfused_auto": (lambda pg, ex: _chain_step(pg, ex, sampled=False), "auto"),
     "late_auto": (_late_rank_ticks, "auto"),
     "latechain_auto": (_late_rank_chain, "auto"),
+    "mixdraw_auto": (_mixed_draw, "auto"),
 }
 
 
@@ -247,11 +269,12 @@ def _get(res, name):
 def test_ranks_agree_and_match_single_process(ranks, single, name):
     r0, r1, s = _get(ranks[0], name), _get(ranks[1], name), single[name]
     for k in r0:
-        np.testing.assert_array_equal(r0[k], r1[k], err_msg=f"{name}.{k}: ranks differ")
+        if not k.startswith("rankonly_"):
+            np.testing.assert_array_equal(r0[k], r1[k], err_msg=f"{name}.{k}: ranks differ")
     want = "rccl" if name.endswith("rccl") or name.startswith("late") else "launch"
     assert str(r0["xmode"]) == want, "exchange='auto' must pick the in-launch exchange when its check passes"
     for k, v in s.items():
-        if k in ("xmode", "bound", "modes"):
+        if k in ("xmode", "bound", "modes") or k.startswith("rankonly_"):
             continue
         if np.asarray(v).dtype.kind == "f":
             np.testing.assert_allclose(r0[k], v, rtol=X_TOL, atol=X_TOL, err_msg=f"{name}.{k}")
@@ -307,3 +330,11 @@ def test_late_rank_falls_back_on_every_rank(ranks, name):
         modes = list(_get(r, name)["modes"])
         assert modes[:LATE_TICK] == ["launch"] * LATE_TICK, modes
         assert all(m == "rccl" for m in modes[LATE_TICK:]), modes
+
+
+def test_ranks_agree_on_the_noise_stream_whichever_way_they_drew(ranks):
+    """one rank on the device NumPy draw, the other on the host draw — the first-step check passed
+    (no 'ranks disagree' error, the in-launch exchange taken) and every step matched
+    (test_ranks_agree_and_match_single_process[mixdraw_auto])."""
+    assert bool(_get(ranks[0], "mixdraw_auto")["rankonly_devdraw"])
+    assert not bool(_get(ranks[1], "mixdraw_auto")["rankonly_devdraw"])

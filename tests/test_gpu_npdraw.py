@@ -36,8 +36,8 @@ def _device_draw(nd, K, T, sigma, k_offset=0, K_local=None):
     from mppi_robotarm_amd import hostrng
     du = sigma.shape[0]
     K_local = K if K_local is None else K_local
-    plan = hostrng.monomial_plan(np.zeros(du), sigma)
-    assert plan is not None
+    plan = hostrng.device_plan(np.zeros(du), sigma)
+    assert plan is not None, "np.dot's rounding of this transform is not the pinned model on this host"
     out = torch.full((T, K_local, du), float("nan"), dtype=torch.float32, device="cuda")
     nd.draw(np.random.get_state(), (K, T, du), plan, out, torch.cuda.current_stream().cuda_stream, k_offset, K_local,
             (K_local * du, du, 1))
@@ -55,8 +55,13 @@ CASES = [
     (4097, 33, 2, "runpy"),        # odd K and T
     (512, 64, 3, "permuted"),      # Sigma's transform swaps the components
     (128, 129, 4, "scaled"),       # just over the size the controller hands to the device
+    (4097, 33, 6, "general"),      # a full 2 x 2 transform through np.dot's pinned rounding (hostrng.dot2_model)
+    (65536, 64, 7, "general"),     # the same at config 3's size
+    (3001, 17, 8, "general2"),
 ]
-SIGMAS = {"runpy": np.eye(2) * 20.0, "permuted": np.diag([2.0, 9.0]), "scaled": np.diag([0.3, 7.0])}
+SIGMAS = {"runpy": np.eye(2) * 20.0, "permuted": np.diag([2.0, 9.0]), "scaled": np.diag([0.3, 7.0]),
+          "general": np.array([[20.0, 6.0], [6.0, 12.0]]),    # the sigma_k128_t20 fixture's Sigma
+          "general2": np.array([[2.0, -1.5], [-1.5, 3.0]])}
 
 
 @pytest.mark.parametrize("K,T,seed,sig", CASES)
@@ -102,12 +107,14 @@ def test_rank_slices_are_slices_of_the_whole_draw(nd):
         assert _same_state(st_part, st_full)   # every rank leaves the same state
 
 
-def _loop(device_draw: bool, ticks=4, K=4096, T=32, between=None):
+def _loop(device_draw: bool, ticks=4, K=4096, T=32, between=None, sigma=None):
     from mppi_robotarm_amd.controller import MPPIControllerForPathTracking
     from mppi_robotarm_amd.params import X0_RUNPY, runpy_config
     from conftest import load_paths
     kw = runpy_config()
     kw.update(number_of_samples_K=K, horizon_step_T=T, visualze_sampled_trajs=False)
+    if sigma is not None:
+        kw["sigma"] = sigma
     c = MPPIControllerForPathTracking(ref_path=load_paths()["xydq_circle"], verbose=False, device=0,
                                       numpy_noise_on_device=device_draw, **kw)
     np.random.seed(21)
@@ -131,6 +138,20 @@ def test_controller_device_draw_equals_host_draw():
     b, st_b, _, _ = _loop(False)
     assert used, "the controller did not take the device draw"
     assert hits == 3, "calls 2-4 use the draw queued by the call before"
+    for (ua, oa), (ub, ob) in zip(a, b):
+        np.testing.assert_array_equal(ua, ub)
+        np.testing.assert_array_equal(oa, ob)
+    assert _same_state(st_a, st_b)
+
+
+def test_controller_device_draw_general_sigma():
+    """A Sigma whose transform is a full 2 x 2 matrix (the sigma_k128_t20 fixture's [[20, 6], [6, 12]]) stays on
+    the device draw: the host draw's steps and RNG state bit for bit, the queued draw used."""
+    sig = SIGMAS["general"]
+    a, st_a, used, hits = _loop(True, sigma=sig)
+    b, st_b, _, _ = _loop(False, sigma=sig)
+    assert used, "the controller did not take the device draw"
+    assert hits == 3
     for (ua, oa), (ub, ob) in zip(a, b):
         np.testing.assert_array_equal(ua, ub)
         np.testing.assert_array_equal(oa, ob)

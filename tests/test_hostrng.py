@@ -1,6 +1,8 @@
 """The drop-in's NumPy-stream noise (control.py:154-164): hostrng.multivariate_normal, whose standard-normal
 stream is threaded in C (csrc/np_legacy_gauss.c), equals np.random.multivariate_normal value for value and
 leaves the global RNG in the state NumPy leaves (the next draws agree too)."""
+import os
+
 import numpy as np
 import pytest
 
@@ -182,3 +184,29 @@ def test_jump_polynomials_reach_the_stream_starts(P, s):
         jumped ^= seq[d:d + 624]
     nxt = _mt_blocks(jumped, 2)[1]
     np.testing.assert_array_equal(nxt, blocks[P * s])
+
+
+@pytest.mark.parametrize("cov", [[[20.0, 6.0], [6.0, 12.0]], [[2.0, -1.5], [-1.5, 3.0]], [[1.0, 0.999], [0.999, 1.0]]])
+def test_dot2_model_pins_numpys_rounding(cov):
+    """The device draw's general 2 x 2 transform (mppi_np_target.dot2): on this host np.dot(z, m) of
+    multivariate_normal's matrix equals fma(z1, m[1, j], z0 * m[0, j]) bit for bit (hostrng.dot2_model, checked
+    again at run time wherever the draw runs), and device_plan hands that matrix over; a diagonal Sigma keeps the
+    scaled column permutation."""
+    cov = np.array(cov)
+    u, s, v = np.linalg.svd(cov)
+    m = np.sqrt(s)[:, None] * v
+    assert hostrng.dot2_model(m)
+    plan = hostrng.device_plan(np.zeros(2), cov)
+    assert plan is not None and plan[4] is not None and np.array_equal(plan[4], m)
+    # the reference's own draw reproduced with the model on NumPy's standard normals
+    np.random.seed(3)
+    want = np.random.multivariate_normal(np.zeros(2), cov, (50, 7))
+    np.random.seed(3)
+    z = np.random.standard_normal((50 * 7, 2))
+    got = np.empty_like(z)
+    hostrng._load().mppi_np_dot2_fma(z.ctypes.data, z.shape[0], np.ascontiguousarray(m).ctypes.data, got.ctypes.data)
+    got += 0.0
+    np.testing.assert_array_equal(got.reshape(50, 7, 2), want)
+    diag = hostrng.device_plan(np.zeros(2), np.eye(2) * 20.0)
+    assert diag is not None and diag[4] is None
+

@@ -14,7 +14,7 @@ K, T = (int(a) for a in sys.argv[1:3]) if len(sys.argv) > 2 else (65536, 64)
 torch.cuda.set_device(0)
 nd = NpDeviceStream(torch.device("cuda", 0))
 sigma = np.eye(2) * 20.0
-plan = hostrng.monomial_plan(np.zeros(2), sigma)
+plan = hostrng.device_plan(np.zeros(2), sigma)
 out = torch.empty((T, K, 2), dtype=torch.float32, device="cuda")
 s = torch.cuda.current_stream()
 np.random.seed(0)
