@@ -358,6 +358,51 @@ def chain_dropin_latency(K, T, device, precision="f32", calls=40, warm=10, noise
     return float(np.median(ts[warm:])) * 1e3
 
 
+def exchange_costs(eng, noise, partial, gathered, world, xmode, args, steps=200):
+    """N > 1, after the timed region: the per-step cost of each way to finish a multi-GPU step on this node,
+    timed the same way as the headline (barrier + synchronise on both sides, max over ranks): the rank's fused
+    step without any exchange (its own shard's update: the floor), the in-launch exchange (when attached), and
+    rollout + RCCL all-gather + merge launch.  The ranks' nominals diverge here, which nothing after reads."""
+    import torch.distributed as dist
+
+    def sync():
+        if torch.cuda.is_available():   # (a CPU test drives this with a stand-in engine)
+            torch.cuda.synchronize()
+
+    def timed(fn):
+        dist.barrier()
+        sync()
+        t0 = time.perf_counter()
+        for i in range(steps):
+            fn(i)
+        sync()
+        dist.barrier()
+        el = time.perf_counter() - t0
+        dev = eng.device if args.backend == "nccl" else "cpu"
+        tt = torch.tensor([el], dtype=torch.float64, device=dev)
+        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+        return float(tt[0]) * 1e3 / steps
+
+    nb = len(noise)
+
+    def local(i):
+        eng.rollout(noise[i % nb], fused_update=True)
+
+    def launch(i):
+        eng.rollout(noise[i % nb], fused_update=True, exchange=True)
+
+    def rccl(i):
+        eng.rollout(noise[i % nb], partial_out=partial)
+        exchange_partials(partial, gathered)
+        eng.merge(gathered, world, fused_update=True)
+
+    out = {"steps": steps, "no_exchange_ms_per_step": timed(local),
+           "rccl_allgather_merge_ms_per_step": timed(rccl),
+           "in_launch_ms_per_step": timed(launch) if xmode == "launch" else None}
+    eng.synchronize()
+    return out
+
+
 def launch_ranks(args) -> int:
     """`--gpus N` (N > 1) without a launcher: start N rank processes under
     torch.distributed.run on this node (127.0.0.1) and return their exit code.
@@ -369,7 +414,15 @@ def launch_ranks(args) -> int:
         s.bind(("127.0.0.1", 0))
         port = s.getsockname()[1]
     cmd = launcher_cmd(args.gpus, port, sys.argv[1:])
-    return subprocess.call(cmd, env=dict(os.environ, HSA_ENABLE_IPC_MODE_LEGACY="0"))
+    return subprocess.call(cmd, env=launcher_env())
+
+
+def launcher_env() -> dict:
+    """The ranks' environment: this one with HSA_ENABLE_IPC_MODE_LEGACY=0 (distributed.IPC_ENV: the host
+    driver's HIP IPC is dmabuf only, which the in-launch exchange's inbox handles and RCCL's intra-node
+    transport both need; an external torchrun inherits it from the driver's environment)."""
+    from mppi_robotarm_amd.distributed import IPC_ENV
+    return dict(os.environ, **{IPC_ENV: "0"})
 
 
 def launcher_cmd(n: int, port: int, argv) -> list:
@@ -466,11 +519,14 @@ def main():
     steps = (args.steps + chunk - 1) // chunk * chunk
 
     xmode = "none" if world == 1 else "rccl"
+    xreport = {}   # the step-1 self-check: which exchange, and why a fallback happened (distributed.py)
     if world > 1 and args.exchange != "rccl":
-        ok = attach_exchange(eng) and check_exchange(eng, noise[0], partial, gathered)
+        ok = attach_exchange(eng, report=xreport) and check_exchange(eng, noise[0], partial, gathered,
+                                                                     report=xreport)
         if not ok and args.exchange == "launch":
-            raise RuntimeError("in-launch exchange unavailable")
+            raise RuntimeError(f"in-launch exchange unavailable: {xreport}")
         xmode = "launch" if ok else "rccl"
+    xreport["picked"] = xmode
 
     # c5: the plant-less device loop (fixed start state, the nominal updated every step) drifts for the chain:
     # |u| grows ~1 N m per step and after ~250 steps most rollouts overflow (tools/loop_drift.py).  Every
@@ -573,6 +629,7 @@ def main():
     eng.synchronize()   # raises if an in-launch hand-off timed out anywhere in the run (results invalid)
     u_final = eng.nominal()
     assert np.all(np.isfinite(u_final)), "non-finite nominal control"
+    xcosts = exchange_costs(eng, noise, partial, gathered, world, xmode, args) if world > 1 and not c5 else None
 
     if rank == 0:
         ms_per_step = elapsed * 1e3 / args.steps
@@ -625,6 +682,8 @@ def main():
                            + (" (RCCL)" if args.backend == "nccl" else f" ({args.backend})"))) if world > 1
                        else "single device, fused update" + (f", HIP graph of {chunk} steps" if use_graph
                                                                else ", back-to-back launches")},
+            "exchange_selfcheck": xreport if world > 1 else None,
+            "exchange_costs": xcosts,
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": achieved / HBM_PEAK_GBS, "traffic": traffic},
             "valu_roofline": valu,

@@ -310,8 +310,10 @@ class MPPIControllerForPathTracking:
                                "(and pass the same seed / K / T)")
         mode = "rccl"
         if self.exchange != "rccl" and not self._x_failed:   # after a failed exchange: the all-gather for good
-            ok = attach_exchange(eng, pg)
-            ok = ok and check_exchange(eng, self._noise_dev, self._partial, self._gathered, pg)
+            self.exchange_report = {}                      # why an exchange was (not) picked (distributed.py)
+            ok = attach_exchange(eng, pg, report=self.exchange_report)
+            ok = ok and check_exchange(eng, self._noise_dev, self._partial, self._gathered, pg,
+                                       report=self.exchange_report)
             if not ok and self.exchange == "launch":
                 raise RuntimeError("the in-launch exchange failed its self-check (exchange='launch')")
             mode = "launch" if ok else "rccl"

@@ -15,8 +15,23 @@ check_exchange is its one-step self-check against the all-gather.
 """
 from __future__ import annotations
 
+import os
+import sys
+
 import torch
 import torch.distributed as dist
+
+# The in-launch exchange maps every rank's inbox through hipIpcGetMemHandle / hipIpcOpenMemHandle.  On this
+# pool's host driver only the dmabuf form of HIP IPC exists; ROCm picks it when HSA_ENABLE_IPC_MODE_LEGACY=0,
+# and without it the export fails with "hipIpcGetMemHandle: invalid argument" (RCCL's own intra-node transport
+# uses the same IPC and fails the same way).  bench.py's self-launch sets it for its ranks; an external launcher
+# must export it (the driver's and the GPU box's environment already does).
+IPC_ENV = "HSA_ENABLE_IPC_MODE_LEGACY"
+
+
+def ipc_env_ok() -> bool:
+    """Whether this process has the dmabuf IPC mode the in-launch exchange needs (IPC_ENV=0)."""
+    return os.environ.get(IPC_ENV) == "0"
 
 
 def shard_geometry(K: int, world: int, rank: int) -> tuple[int, int]:
@@ -77,7 +92,7 @@ def gather_trajectories(tr: torch.Tensor, K_total: int, out, group=None):
     return out
 
 
-def attach_exchange(engine, group=None) -> bool:
+def attach_exchange(engine, group=None, report: dict | None = None) -> bool:
     """Set up the in-launch exchange (include/mppi_rocm.h mppi_exchange_*): every
     rank exports its inbox's IPC handle, the handles are all-gathered over the
     group once, and every rank maps its peers' inboxes.  Afterwards
@@ -85,39 +100,74 @@ def attach_exchange(engine, group=None) -> bool:
     multi-GPU control step in one launch per rank.
 
     Collective-safe: every rank joins every collective whatever fails locally,
-    and all ranks return the same answer (False: use exchange_partials)."""
+    and all ranks return the same answer (False: use exchange_partials).
+    `report` (a dict) receives report["attach"]: the verdict, the failing ranks
+    and their errors, and each rank's IPC_ENV (the same on every rank); a failure
+    is also printed to stderr."""
     world, rank = dist.get_world_size(group), dist.get_rank(group)
+    env = os.environ.get(IPC_ENV)
+    err = None
     try:
         h = engine.exchange_handle(world)
-    except Exception:  # noqa: BLE001 - reported to every rank below
-        h = None
+    except Exception as e:  # noqa: BLE001 - reported to every rank below
+        h, err = None, f"handle: {e}"
+        if env != "0":
+            err += f" ({IPC_ENV}={env!r}: this driver's IPC needs {IPC_ENV}=0)"
     handles = [None] * world
     dist.all_gather_object(handles, h, group=group)
-    ok = all(x is not None for x in handles)
-    if ok:
+    if err is None and all(x is not None for x in handles):
         try:
             engine.exchange_attach(rank, world, handles)
-        except Exception:  # noqa: BLE001
-            ok = False
-    return _all_ranks(ok, group)
+        except Exception as e:  # noqa: BLE001
+            err = f"attach: {e}"
+    elif err is None:
+        err = "a peer failed to export its handle"
+    infos = [None] * world
+    dist.all_gather_object(infos, (err, env), group=group)
+    ok = all(i[0] is None for i in infos)
+    if report is not None:
+        report["attach"] = {"ok": ok, "failed_ranks": [r for r, i in enumerate(infos) if i[0] is not None],
+                            "errors": {str(r): i[0] for r, i in enumerate(infos) if i[0] is not None},
+                            "ipc_env": [i[1] for i in infos]}
+    if not ok and rank == 0:
+        first = next(i[0] for i in infos if i[0] is not None)
+        print(f"mppi multi-GPU: in-launch exchange unavailable ({first}); the RCCL all-gather is used",
+              file=sys.stderr, flush=True)
+    return ok
 
 
-def check_exchange(engine, noise, partial, gathered, group=None) -> bool:
+def check_exchange(engine, noise, partial, gathered, group=None, report: dict | None = None) -> bool:
     """One step both ways from the same state (no update): the in-launch exchange
     must reproduce all-gather + device merge (1e-9) without a hand-off timeout.
-    Every rank gets the same verdict."""
+    Every rank gets the same verdict; `report` receives report["check"] (the
+    verdict, the failing ranks and why, each rank's largest w_eps difference)."""
     import numpy as np
     engine.rollout(noise, partial_out=partial)
     exchange_partials(partial, gathered, group)
     engine.merge(gathered, dist.get_world_size(group))
     w_ref = engine.weighted_noise()
+    err, diff = None, None
     try:
         engine.rollout(noise, exchange=True)
         engine.synchronize()          # raises on a hand-off timeout
-        ok = bool(np.allclose(engine.weighted_noise(), w_ref, rtol=1e-9, atol=1e-12))
-    except Exception:  # noqa: BLE001
-        ok = False
-    return _all_ranks(ok, group)
+        w = engine.weighted_noise()
+        diff = float(np.max(np.abs(w - w_ref)))
+        if not np.allclose(w, w_ref, rtol=1e-9, atol=1e-12):
+            err = f"w_eps differs from the all-gather's by {diff:.3g}"
+    except Exception as e:  # noqa: BLE001
+        err = f"in-launch step: {e}"
+    infos = [None] * dist.get_world_size(group)
+    dist.all_gather_object(infos, (err, diff), group=group)
+    ok = all(i[0] is None for i in infos)
+    if report is not None:
+        report["check"] = {"ok": ok, "failed_ranks": [r for r, i in enumerate(infos) if i[0] is not None],
+                           "errors": {str(r): i[0] for r, i in enumerate(infos) if i[0] is not None},
+                           "max_abs_diff": [i[1] for i in infos]}
+    if not ok and dist.get_rank(group) == 0:
+        first = next(i[0] for i in infos if i[0] is not None)
+        print(f"mppi multi-GPU: the in-launch exchange failed its self-check ({first}); the RCCL all-gather is used",
+              file=sys.stderr, flush=True)
+    return ok
 
 
 def same_on_all_ranks(obj, group=None) -> bool:
@@ -126,8 +176,3 @@ def same_on_all_ranks(obj, group=None) -> bool:
     dist.all_gather_object(objs, obj, group=group)
     return all(o == objs[0] for o in objs)
 
-
-def _all_ranks(ok: bool, group=None) -> bool:
-    flags = [None] * dist.get_world_size(group)
-    dist.all_gather_object(flags, bool(ok), group=group)
-    return all(flags)

@@ -278,3 +278,117 @@ def test_multi_gpu_controller_checks_the_noise_stream(tmp_path, seeds_differ):
                        start_method="spawn")
     for r in range(world):
         assert np.load(f"{out}.{r}.npy").tolist() == [1, 0, 0 if seeds_differ else 1]
+
+
+def _report_worker(rank, world, port, bad, where, out_path):
+    import json
+    import sys
+    sys.path.insert(0, ROOT)
+    from mppi_robotarm_amd.distributed import attach_exchange
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    if rank == 1 and where == "handle":
+        os.environ.pop("HSA_ENABLE_IPC_MODE_LEGACY", None)   # the env the driver's IPC needs, missing on one rank
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        rep = {}
+        ok = attach_exchange(_FakeEngine(rank, bad, where), report=rep)
+        json.dump({"ok": ok, "report": rep}, open(f"{out_path}.{rank}.json", "w"))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("bad,where", [(-1, ""), (1, "handle"), (0, "attach")])
+def test_attach_exchange_reports_why(tmp_path, bad, where):
+    """bench.py --gpus N records the step-1 self-check (exchange_selfcheck): every rank gets the same report of
+    the failing ranks, their errors (a failed handle export names the missing HSA_ENABLE_IPC_MODE_LEGACY=0) and
+    each rank's IPC environment."""
+    import json
+    world = 2
+    out = str(tmp_path / "rep")
+    env = dict(os.environ)
+    os.environ["HSA_ENABLE_IPC_MODE_LEGACY"] = "0"
+    try:
+        mp.start_processes(_report_worker, args=(world, _free_port(), bad, where, out), nprocs=world, join=True,
+                           start_method="spawn")
+    finally:
+        os.environ.clear()
+        os.environ.update(env)
+    r = [json.load(open(f"{out}.{k}.json")) for k in range(world)]
+    assert r[0] == r[1]
+    a = r[0]["report"]["attach"]
+    assert r[0]["ok"] is a["ok"] is (bad < 0)
+    if bad < 0:
+        assert a["failed_ranks"] == [] and a["errors"] == {} and a["ipc_env"] == ["0", "0"]
+    elif where == "handle":
+        assert 1 in a["failed_ranks"] and "no inbox" in a["errors"]["1"]
+        assert "HSA_ENABLE_IPC_MODE_LEGACY=0" in a["errors"]["1"] and a["ipc_env"] == ["0", None]
+    else:
+        assert a["failed_ranks"] == [0] and "cannot map" in a["errors"]["0"]
+
+
+class _CostEngine:
+    device = "cpu"
+
+    def __init__(self):
+        self.calls = []
+
+    def rollout(self, noise, partial_out=None, fused_update=False, exchange=False):
+        self.calls.append(("rollout", exchange, partial_out is not None))
+
+    def merge(self, gathered, n, fused_update=False):
+        self.calls.append(("merge", n))
+
+    def synchronize(self):
+        pass
+
+
+def _cost_worker(rank, world, port, xmode, out_path):
+    import json
+    import sys
+    sys.path.insert(0, ROOT)
+    import bench
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        eng = _CostEngine()
+        partial, gathered = torch.zeros(6, dtype=torch.float64), torch.zeros(12, dtype=torch.float64)
+
+        class A:
+            backend = "gloo"
+        out = bench.exchange_costs(eng, [None, None], partial, gathered, world, xmode, A(), steps=5)
+        json.dump({"costs": out, "calls": eng.calls}, open(f"{out_path}.{rank}.json", "w"))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("xmode", ["launch", "rccl"])
+def test_bench_exchange_costs_fields(tmp_path, xmode):
+    """bench.py's exchange_costs (the N > 1 JSON line's per-step cost of each exchange on the node): the fields,
+    each leg's launches, and the in-launch leg only when that exchange was attached."""
+    import json
+    world = 2
+    out = str(tmp_path / "cost")
+    mp.start_processes(_cost_worker, args=(world, _free_port(), xmode, out), nprocs=world, join=True,
+                       start_method="spawn")
+    for k in range(world):
+        r = json.load(open(f"{out}.{k}.json"))
+        c = r["costs"]
+        assert set(c) == {"steps", "no_exchange_ms_per_step", "rccl_allgather_merge_ms_per_step", "in_launch_ms_per_step"}
+        assert c["steps"] == 5 and c["no_exchange_ms_per_step"] > 0 and c["rccl_allgather_merge_ms_per_step"] > 0
+        assert (c["in_launch_ms_per_step"] is None) == (xmode != "launch")
+        n_ex = sum(1 for x in r["calls"] if x[0] == "rollout" and x[1])
+        assert n_ex == (5 if xmode == "launch" else 0)
+        assert sum(1 for x in r["calls"] if x[0] == "merge") == 5
+
+
+def test_bench_launcher_env_and_command():
+    """bench.py --gpus N without a launcher: the ranks get HSA_ENABLE_IPC_MODE_LEGACY=0 and a 127.0.0.1
+    rendezvous."""
+    import sys
+    sys.path.insert(0, ROOT)
+    import bench
+    env = bench.launcher_env()
+    assert env["HSA_ENABLE_IPC_MODE_LEGACY"] == "0"
+    cmd = bench.launcher_cmd(8, 29500, ["--gpus", "8"])
+    assert "--master-addr" in cmd and cmd[cmd.index("--master-addr") + 1] == "127.0.0.1"
+    assert "--nproc-per-node=8" in cmd and cmd[-2:] == ["--gpus", "8"]

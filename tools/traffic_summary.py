@@ -9,11 +9,12 @@ with a known byte count; FETCH_SIZE reports that pattern at ~0.5x its true
 bytes, WRITE_SIZE at 1.0x) and writes:
 
   profiles/TAG/kernel_stats.csv      rocprofv3 --kernel-trace --stats summary
-  profiles/TAG/pmc_*.csv             the counter CSVs (one per pass)
+  profiles/TAG/pmc_*.csv.gz          the counter CSVs (one per pass), gzipped
   profiles/TAG/sq_counters.json      SQ issue / wait summary
   profiles/traffic.json              HBM bytes and VALU instructions per rollout launch (read by bench.py)
 """
 import csv
+import gzip
 import json
 import os
 import re
@@ -44,8 +45,9 @@ def main():
     shutil.copy(os.path.join(src, "stats", "run_kernel_stats.csv"), os.path.join(dst, "kernel_stats.csv"))
     for p in ("fetch", "write", "cfetch", "cwrite", "sq", "grbm"):
         f = os.path.join(src, p, "p_counter_collection.csv")
-        if os.path.exists(f):
-            shutil.copy(f, os.path.join(dst, f"pmc_{p}.csv"))
+        if os.path.exists(f):   # kept gzipped: the raw counter rows are large and only the summaries are cited
+            with open(f, "rb") as fi, gzip.open(os.path.join(dst, f"pmc_{p}.csv.gz"), "wb", compresslevel=9) as fo:
+                shutil.copyfileobj(fi, fo)
     avg_ns = None
     with open(os.path.join(src, "stats", "run_kernel_stats.csv")) as f:
         for row in csv.DictReader(f):
