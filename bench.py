@@ -293,6 +293,17 @@ def sampled_latency(K, T, device, calls=20, warm=5, noise="device"):
         detail["readback_only_ms"] = float(np.median(rt[2:])) * 1e3
         detail["readback_workers"] = rb.workers
         detail["readback_bytes_over_link"] = int(tr.numel() * 4)
+        # its floor: the same fp32 bytes in one DMA into page-locked memory, nothing widened
+        pin = torch.empty((K, T, 4), dtype=torch.float32, pin_memory=True)
+        ft = []
+        for i in range(12):
+            torch.cuda.synchronize()
+            t0 = time.perf_counter()
+            pin.copy_(tr)
+            torch.cuda.synchronize()
+            ft.append(time.perf_counter() - t0)
+        detail["fp32_dma_floor_ms"] = float(np.median(ft[2:])) * 1e3
+        del pin
     c.close()
     return float(np.median(ts[warm:])) * 1e3, detail
 
