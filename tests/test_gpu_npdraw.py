@@ -185,15 +185,19 @@ def _chain_loop(device_draw: bool, lam: float, ticks=3, K=4096, T=16):
     c = ChainMPPIController(0.006, load_paths()["xydq_circle"], T, K, param_lambda=lam, device=0,
                             u_init=gravity_torque(CHAIN7_X0[:7]), numpy_noise_on_device=device_draw)
     np.random.seed(4)
-    out, precs = [], []
+    out, precs, first = [], [], []
     for i in range(ticks):
         c.prev_waypoints_idx = 0
+        first.append("f64" if c._spread else "f32")   # the engine this call's draw goes to first
         u0, u_seq, opt, _ = c.calc_control_input(CHAIN7_X0)
         out.append((u_seq.copy(), opt.copy()))
         precs.append(c.last_precision)
     used, hits = c._npdev, c._npre_used
     c.close()
-    return out, np.random.get_state(), used, precs, hits
+    # the draw a call queues goes to that call's first engine; the next call uses it when its own first engine is
+    # the same one (precision="auto" switches engines when the weights spread or stop spreading)
+    want = sum(first[i] == first[i - 1] for i in range(1, ticks))
+    return out, np.random.get_state(), used, precs, (hits, want)
 
 
 @pytest.mark.parametrize("lam", [100.0, 3.0e5])
@@ -201,10 +205,10 @@ def test_chain_controller_device_draw_equals_host_draw(lam):
     """The 7-link drop-in's default noise on the device: the host draw's steps bit for bit; at lambda = 3e5 the
     weights spread and precision="auto" re-runs each step in fp64 on the other engine (the draw copied into its
     noise buffer)."""
-    a, st_a, used, precs, hits = _chain_loop(True, lam)
+    a, st_a, used, precs, (hits, want) = _chain_loop(True, lam)
     b, st_b, _, precs_b, _ = _chain_loop(False, lam)
     assert used, "the chain controller did not take the device draw"
-    assert hits >= 1, "a call used the draw queued beside the step before (same engine: same precision)"
+    assert hits == want, "every call whose first engine is the last call's uses the draw queued beside that step"
     assert precs == precs_b
     assert lam < 1e4 or "f64" in precs
     for (ua, oa), (ub, ob) in zip(a, b):
