@@ -12,9 +12,9 @@
 //                    polynomial, found and powered on the host, np_legacy_gauss.c) and F^d(key) the window
 //                    [d, d + 624) of the word sequence (Haramoto et al. 2008, the window form): a table product
 //                    over 4-bit chunks of phi, the 16 entries of a chunk in each lane's registers.
-//   np_gen_kernel    one workgroup per stream twists its range of blocks; a block's 624 words are each a
-//                    function of the previous block alone (the twist's in-block dependencies unrolled: up to
-//                    three tempering-free mix terms per word), so one barrier per block.
+//   np_gen_kernel    one workgroup per stream twists its range of blocks; the words 227 apart form one chain
+//                    of the twist, so a thread computes three of them from the previous block (one mix each,
+//                    in registers): one LDS round trip and one barrier per block.
 //   np_write_kernel  the attempts, 2048 consecutive ones per workgroup; the index of the workgroup's first pair
 //                    by look-back over its predecessors' published counts (one pass, no separate count and
 //                    scan); each accepted pair's place from it; f with glibc's log
@@ -55,10 +55,10 @@ constexpr int kDeg = 19937;
 constexpr int kPolyWords = MPPI_NP_POLY_WORDS;        // 312 x 64 bits: a polynomial of degree < 19937
 constexpr int kSeqBlocks = (kDeg + kN) / kN + 1;      // 34: the windows d + j < 19937 + 624 of the jumps
 constexpr int kNT = 256;                              // threads of the attempt kernels
-constexpr int kTT = 704;                              // threads of the twist kernels: one word per thread, the
-                                                      // twist's three ranges on whole waves (twist_slot)
+constexpr int kR = kN - kM;                           // 227: the twist's dependency distance
+constexpr int kTT = 256;                              // threads of the twist kernels: thread t < 227 owns words t,
+                                                      // t + 227 and (t < 170) t + 454 (twist3)
 constexpr int kNibS = 32;                             // table jump: streams per workgroup
-constexpr int kNibW = kNibS / 8;                      // their nibbles of one chunk: 4 words
 constexpr int kChunks = (kDeg + 3) / 4;               // 4-bit chunks of a jump polynomial
 constexpr int kJNT = 640;                             // table jump threads: output word i per lane (< 624)
 constexpr int kJTableWGs = 512;                       // table jump: chunk ranges x stream groups, about
@@ -70,26 +70,27 @@ __device__ __forceinline__ uint32_t mt_mix(uint32_t a, uint32_t b) {
     return (y >> 1) ^ ((0u - (y & 1u)) & kMatA);
 }
 
-// The key array after o (LDS) into k (LDS).  NumPy's twist (in place, word order) is k[i] = o[i + 397] ^
+// The key array after o (LDS), thread t's words.  NumPy's twist (in place, word order) is k[i] = o[i + 397] ^
 // mix(o[i], o[i + 1]) for i < 227, k[i] = k[i - 227] ^ mix(o[i], o[i + 1]) up to 622, and k[623] =
-// k[396] ^ mix(o[623], k[0]); substituting the earlier k's, every word depends on o only.
-__device__ __forceinline__ uint32_t twist_word(const uint32_t* o, int i) {
-    if (i < kN - kM) return o[i + kM] ^ mt_mix(o[i], o[i + 1]);
-    if (i < 2 * (kN - kM)) return o[i + 170] ^ mt_mix(o[i - 227], o[i - 226]) ^ mt_mix(o[i], o[i + 1]);
-    if (i < kN - 1)
-        return o[i - 57] ^ mt_mix(o[i - 454], o[i - 453]) ^ mt_mix(o[i - 227], o[i - 226]) ^ mt_mix(o[i], o[i + 1]);
-    const uint32_t k0 = o[kM] ^ mt_mix(o[0], o[1]);
-    const uint32_t k396 = o[566] ^ mt_mix(o[169], o[170]) ^ mt_mix(o[396], o[397]);
-    return k396 ^ mt_mix(o[623], k0);
+// k[396] ^ mix(o[623], k[0]).  The words 227 apart are one chain, so thread t (< 227) computes k[t], k[t + 227]
+// and k[t + 454] in order, each from its predecessor in a register: one mix per word, every LDS read of the block
+// issued at once.  Word 623 is thread 169's third (its second is k[396]); the new k[0] it needs is recomputed
+// from broadcast reads by every lane (cheaper than a branch on one lane).  Threads t >= 227 compute garbage that
+// twist_block does not store.
+__device__ __forceinline__ void twist3(const uint32_t* o, int t, uint32_t k[3]) {
+    const int u = min(t, kR - 1);
+    const uint32_t a0 = o[u], a1 = o[u + 1], am = o[u + kM];
+    const uint32_t b0 = o[u + kR], b1 = o[u + kR + 1];
+    const uint32_t c0 = o[min(u + 2 * kR, kN - 1)], c1 = o[min(u + 2 * kR + 1, kN - 1)];
+    const uint32_t z0 = o[0], z1 = o[1], zm = o[kM];
+    k[0] = am ^ mt_mix(a0, a1);
+    k[1] = k[0] ^ mt_mix(b0, b1);
+    const uint32_t knew0 = zm ^ mt_mix(z0, z1);
+    k[2] = k[1] ^ mt_mix(c0, u == kN - 1 - 2 * kR ? knew0 : c1);
 }
 
-// The word a twist thread computes (-1: none): waves 0-3 words [0, 227), waves 4-7 [227, 454), waves 8-10
-// [454, 624), so each wave runs one branch of twist_word (the last one also word 623's)
-__device__ __forceinline__ int twist_slot(int t) {
-    if (t < 256) return t < kN - kM ? t : -1;
-    if (t < 512) return t - 256 < kN - kM ? t - 256 + (kN - kM) : -1;
-    return t - 512 < kN - 2 * (kN - kM) ? t - 512 + 2 * (kN - kM) : -1;
-}
+// words thread t stores: k[t], k[t + 227] for t < 227, k[t + 454] for t < 170
+__device__ __forceinline__ int twist_words(int t) { return t < kN - 2 * kR ? 3 : t < kR ? 2 : 0; }
 
 __device__ __forceinline__ uint32_t temper(uint32_t y) {
     y ^= (y >> 11);
@@ -135,21 +136,30 @@ struct NpShape {
 };
 
 // ------------------------------------------------------------------ generation
+// One twist of buffer o into n (LDS) and, with kStore, into out (global); a barrier must follow before n is read.
+template <bool kStore>
+__device__ __forceinline__ void twist_block(const uint32_t* o, uint32_t* n, uint32_t* __restrict__ out, int t) {
+    uint32_t k[3];
+    twist3(o, t, k);
+    const int m = twist_words(t);
+#pragma unroll
+    for (int r = 0; r < 3; ++r)
+        if (r < m) {
+            n[t + r * kR] = k[r];
+            if (kStore) out[t + r * kR] = k[r];
+        }
+}
+
 __global__ __launch_bounds__(kTT) void np_seq_kernel(const uint32_t* __restrict__ key, uint32_t* __restrict__ seq) {
     __shared__ uint32_t buf[2][kN];
-    const int i = twist_slot(threadIdx.x);
-    uint32_t v = i >= 0 ? key[i] : 0u;
-    if (i >= 0) {
-        buf[0][i] = v;
-        seq[i] = v;
+    for (int q = threadIdx.x; q < kN; q += kTT) {
+        const uint32_t v = key[q];
+        buf[0][q] = v;
+        seq[q] = v;
     }
     __syncthreads();
     for (int b = 1; b < kSeqBlocks; ++b) {
-        if (i >= 0) {
-            v = twist_word(buf[(b - 1) & 1], i);
-            buf[b & 1][i] = v;
-            seq[(size_t)b * kN + i] = v;
-        }
+        twist_block<true>(buf[(b - 1) & 1], buf[b & 1], seq + (size_t)b * kN, threadIdx.x);
         __syncthreads();   // the next twist reads this block and writes the buffer this one read
     }
 }
@@ -187,13 +197,11 @@ __global__ __launch_bounds__(kJNT) void np_jumpn_kernel(const uint32_t* __restri
         T[7] = e ^ T[3];
 #pragma unroll
         for (int v = 0; v < 8; ++v) T[8 + v] = T[v] ^ d;
-        const uint32_t* nb = nibs + ((size_t)c * G + g) * kNibW;
+        // one word per jump, the nibble already extracted (< 16, set_jumps): the index goes from the scalar load
+        // straight into s_set_gpr_idx_on, no scalar bit-field extract per lookup
+        const uint32_t* nb = nibs + ((size_t)c * G + g) * kNibS;
 #pragma unroll
-        for (int w = 0; w < kNibW; ++w) {
-            const uint32_t word = __builtin_amdgcn_readfirstlane(nb[w]);
-#pragma unroll
-            for (int q = 0; q < 8; ++q) o[8 * w + q] ^= T[(word >> (4 * q)) & 15u];
-        }
+        for (int j = 0; j < kNibS; ++j) o[j] ^= T[__builtin_amdgcn_readfirstlane(nb[j])];
     }
     if (i < kN) {
 #pragma unroll
@@ -209,46 +217,55 @@ __global__ __launch_bounds__(kTT) void np_gen_kernel(const uint32_t* __restrict_
                                                      uint32_t* __restrict__ words, int P, int nblk, int nparts,
                                                      NpResult* res) {
     __shared__ uint32_t buf[2][kN];
-    const int s = blockIdx.x, i = twist_slot(threadIdx.x);
+    const int s = blockIdx.x, t = threadIdx.x;
     const int b0 = 1 + P * s, b1 = min(1 + P * (s + 1), nblk);
+    constexpr int kQ = (kN + kTT - 1) / kTT;   // 3 words per thread in the coalesced prologue
     if (s == 0) {
-        if (threadIdx.x == 0) {   // the draw's result, before np_write_kernel fills it
+        if (t == 0) {   // the draw's result, before np_write_kernel fills it
             res->last_attempt = -1;
             res->total = 0;
             res->status = 0;
         }
-        if (i >= 0) {
-            const uint32_t v = key[i];
-            buf[0][i] = v;
-            words[i] = v;
+        for (int q = t; q < kN; q += kTT) {
+            const uint32_t v = key[q];
+            buf[0][q] = v;
+            words[q] = v;
         }
         __syncthreads();
     } else {
-        if (i >= 0) {
-            const uint32_t* q = parts + (size_t)(s - 1) * nparts * kN + i;
-            uint32_t v = 0;
-            int h = 0;
-            for (; h + 8 <= nparts; h += 8) {   // eight loads in flight
-                uint32_t x[8];
+        const uint32_t* base = parts + (size_t)(s - 1) * nparts * kN;
+        uint32_t v[kQ];
+        int qi[kQ];
 #pragma unroll
-                for (int u = 0; u < 8; ++u) x[u] = q[(size_t)(h + u) * kN];
-#pragma unroll
-                for (int u = 0; u < 8; ++u) v ^= x[u];
-            }
-            for (; h < nparts; ++h) v ^= q[(size_t)h * kN];
-            buf[1][i] = v;
+        for (int r = 0; r < kQ; ++r) {
+            v[r] = 0u;
+            qi[r] = min(t + r * kTT, kN - 1);   // lanes past word 623 repeat it (not stored)
         }
+        int h = 0;
+        for (; h + 8 <= nparts; h += 8) {   // 8 parts x 3 words: 24 loads in flight
+            uint32_t x[8][kQ];
+#pragma unroll
+            for (int u = 0; u < 8; ++u)
+#pragma unroll
+                for (int r = 0; r < kQ; ++r) x[u][r] = base[(size_t)(h + u) * kN + qi[r]];
+#pragma unroll
+            for (int u = 0; u < 8; ++u)
+#pragma unroll
+                for (int r = 0; r < kQ; ++r) v[r] ^= x[u][r];
+        }
+        for (; h < nparts; ++h)
+#pragma unroll
+            for (int r = 0; r < kQ; ++r) v[r] ^= base[(size_t)h * kN + qi[r]];
+#pragma unroll
+        for (int r = 0; r < kQ; ++r)
+            if (t + r * kTT < kN) buf[1][t + r * kTT] = v[r];
         __syncthreads();
-        if (i >= 0) buf[0][i] = twist_word(buf[1], i);   // block P s, exactly
+        twist_block<false>(buf[1], buf[0], nullptr, t);   // block P s, exactly
         __syncthreads();
     }
     int cur = 0;
     for (int b = b0; b < b1; ++b) {
-        if (i >= 0) {
-            const uint32_t v = twist_word(buf[cur], i);
-            buf[cur ^ 1][i] = v;
-            words[(size_t)b * kN + i] = v;
-        }
+        twist_block<true>(buf[cur], buf[cur ^ 1], words + (size_t)b * kN, t);
         __syncthreads();
         cur ^= 1;
     }
@@ -485,7 +502,7 @@ struct mppi_np_ctx {
     uint32_t* d_key = nullptr;      // the draw's starting key array
     uint32_t* d_seq = nullptr;      // kSeqBlocks blocks
     int poly_P = 0, poly_streams = 0;
-    uint32_t* d_nibs = nullptr;     // table jump: the polynomials' 4-bit chunks, [chunk][group][4 words]
+    uint32_t* d_nibs = nullptr;     // table jump: the polynomials' 4-bit chunks, [chunk][group][jump], one per word
     int jG = 0, jR = 0, jcpw = 0;   // table jump: stream groups, chunk ranges, chunks per range
     int jparts = 1;                 // partial XORs per stream that np_gen_kernel combines
     uint32_t* d_jumped = nullptr;
@@ -617,7 +634,7 @@ int mppi_np_set_jumps(mppi_np_ctx* c, int block_stride, int streams, const unsig
         int R = std::max(1, std::min(128, (kJTableWGs + G - 1) / G));   // at most 128 parts for np_gen_kernel to XOR
         const int cpw = (kChunks + R - 1) / R;
         R = (kChunks + cpw - 1) / cpw;
-        std::vector<uint32_t> nibs((size_t)kChunks * G * kNibW, 0u);
+        std::vector<uint32_t> nibs((size_t)kChunks * G * kNibS, 0u);
         for (int j = 0; j < ns; ++j)
             for (int w = 0; w < kPolyWords; ++w) {
                 const uint64_t m = polys[(size_t)j * kPolyWords + w];
@@ -628,7 +645,7 @@ int mppi_np_set_jumps(mppi_np_ctx* c, int block_stride, int streams, const unsig
                     const uint32_t v = (uint32_t)(m >> (4 * h)) & 15u;
                     const int ch = 16 * w + h;
                     if (v && ch < kChunks)
-                        nibs[((size_t)ch * G + j / kNibS) * kNibW + (j % kNibS) / 8] |= v << (4 * (j % 8));
+                        nibs[((size_t)ch * G + j / kNibS) * kNibS + j % kNibS] = v;
                 }
             }
         NP_CHECK(hipMalloc(&c->d_nibs, nibs.size() * sizeof(uint32_t)));
