@@ -237,6 +237,7 @@ class MPPIControllerForPathTracking:
         self._npre = None              # (start state, spec) of the next call's draw, queued at the end of a call
         self._np_spec = None           # (spec, plan) of this call's device draw
         self._npre_used = 0            # calls that used the queued draw
+        self._np_queued = False        # this call queued the next call's draw already
         self._np_plan = None           # (Sigma bytes, dtype, hostrng.device_plan) of the last draw
         self._np_left = None           # the state this call's draw left np.random in
         self._noise_alt = None         # the second noise buffer: the queued draw writes it while a step reads the other
@@ -418,8 +419,9 @@ class MPPIControllerForPathTracking:
         window = self.ref_path[self.prev_waypoints_idx:(self.prev_waypoints_idx + SEARCH_IDX_LEN)]
         world, _ = self._shard()
         if not self.host_update and world == 1 and not self.visualze_sampled_trajs:
-            if isinstance(epsilon, DeviceDrawn):
+            if isinstance(epsilon, DeviceDrawn) and not self._np_queued:
                 self._queue_predraw(eng)                   # the next call's draw, beside this step
+            self._np_queued = False
             return self._dropin_step(eng, x0, window, u)
         eng.set_step_inputs(np.asarray(x0, dtype=np.float64), window, u)
         if world > 1 and self._xmode is None:
@@ -741,8 +743,11 @@ class MPPIControllerForPathTracking:
             new = self._npdev.result()
         if new is None:
             return None
-        np.random.set_state(new)
         self._np_left = new
+        if not self.host_update and not self.visualze_sampled_trajs and self._shard()[0] == 1:
+            self._queue_predraw(eng)                       # the next call's draw, now: the device is idle until
+            self._np_queued = True                         # it is queued (the step follows on its own stream)
+        np.random.set_state(new)
         return DeviceDrawn()
 
     def _zbuf_numpy(self, n: int) -> np.ndarray:

@@ -120,7 +120,8 @@ struct NpResult {
     long long last_attempt;   // the attempt of the last wanted pair
     double last_fx1;          // its f x1 (cached by an odd count)
     long long total;          // accepted attempts among the generated ones
-    int status;               // 1: fewer than the pairs wanted (not written; the host draws again)
+    int status;               // 1: fewer than the pairs wanted, 2: the look-back gave up (not written; the host
+                              // draws again); np_state_kernel reports 3 if the last pair was not found
     int pad;
 };
 
@@ -197,8 +198,7 @@ __global__ __launch_bounds__(kJNT) void np_jumpn_kernel(const uint32_t* __restri
         T[7] = e ^ T[3];
 #pragma unroll
         for (int v = 0; v < 8; ++v) T[8 + v] = T[v] ^ d;
-        // one word per jump, the nibble already extracted (< 16, set_jumps): the index goes from the scalar load
-        // straight into s_set_gpr_idx_on, no scalar bit-field extract per lookup
+        // one word per jump, the nibble already extracted (< 16, set_jumps), scalar-loaded
         const uint32_t* nb = nibs + ((size_t)c * G + g) * kNibS;
 #pragma unroll
         for (int j = 0; j < kNibS; ++j) o[j] ^= T[__builtin_amdgcn_readfirstlane(nb[j])];
@@ -475,31 +475,33 @@ __global__ __launch_bounds__(kNT) __attribute__((amdgpu_waves_per_eu(4))) void n
     }
 }
 
-// the state NumPy leaves: the key array holding the last consumed word and the position after it
-__global__ __launch_bounds__(kNT) void np_state_kernel(const uint32_t* __restrict__ words, long long base,
-                                                       const NpResult* res, long long need, mppi_np_state* st) {
-    if (res->status || res->last_attempt < 0) return;
-    const long long qw = base + 4 * (res->last_attempt + 1) - 1;
-    const long long blk = qw / kN;
-    for (int i = threadIdx.x; i < kN; i += kNT) st->key[i] = words[blk * kN + i];
-    if (threadIdx.x == 0) {
-        st->pos = (int)(qw - blk * kN) + 1;
-        st->has_gauss = (int)(need & 1);
-        st->gauss = (need & 1) ? res->last_fx1 : 0.0;
-    }
-}
-
-}  // namespace
-
 struct NpHostOut {
     mppi_np_state st;
     int status;
 };
 
+// the state NumPy leaves (the key array holding the last consumed word and the position after it) and the draw's
+// status, written straight into the host-mapped result (no copies after the draw)
+__global__ __launch_bounds__(kNT) void np_state_kernel(const uint32_t* __restrict__ words, long long base,
+                                                       const NpResult* res, long long need, NpHostOut* out) {
+    const int status = res->status ? res->status : res->last_attempt < 0 ? 3 : 0;
+    if (threadIdx.x == 0) out->status = status;
+    if (status) return;
+    const long long qw = base + 4 * (res->last_attempt + 1) - 1;
+    const long long blk = qw / kN;
+    for (int i = threadIdx.x; i < kN; i += kNT) out->st.key[i] = words[blk * kN + i];
+    if (threadIdx.x == 0) {
+        out->st.pos = (int)(qw - blk * kN) + 1;
+        out->st.has_gauss = (int)(need & 1);
+        out->st.gauss = (need & 1) ? res->last_fx1 : 0.0;
+    }
+}
+
+}  // namespace
+
 struct mppi_np_ctx {
     int device = 0;
     double* d_log = nullptr;
-    uint32_t* d_key = nullptr;      // the draw's starting key array
     uint32_t* d_seq = nullptr;      // kSeqBlocks blocks
     int poly_P = 0, poly_streams = 0;
     uint32_t* d_nibs = nullptr;     // table jump: the polynomials' 4-bit chunks, [chunk][group][jump], one per word
@@ -512,9 +514,10 @@ struct mppi_np_ctx {
     size_t look_cap = 0;            // workgroups
     unsigned long long epoch = 0;   // the last draw's epoch (24 bits; the words are cleared when it wraps)
     NpResult* d_res = nullptr;
-    mppi_np_state* d_state = nullptr;
-    NpHostOut* h_out = nullptr;     // page-locked: the draw's state and status read-back
-    uint32_t* h_key = nullptr;          // page-locked staging of the starting key array
+    NpHostOut* h_out = nullptr;     // coherent host-mapped: the draw's state and status, written by np_state_kernel
+    NpHostOut* d_out = nullptr;     // its device address
+    uint32_t* h_key = nullptr;      // coherent host-mapped: the starting key array, read by the twist kernels
+    uint32_t* d_key = nullptr;      // its device address
     hipEvent_t done = nullptr;
     bool pending = false;
 };
@@ -534,11 +537,11 @@ struct Plan {
 
 // attempts generated: 4/3 of the pairs plus 4096 (acceptance pi/4: 1.27 attempts per pair expected), as the
 // host path (np_legacy_gauss.c); the block stride P of the streams from a cost model of the two parallel
-// phases, measured on MI355X (profiles/r15np/, profiles/r15npj/): the table jump costs ~0.48 us per stream, a
-// stream twists its P blocks at ~0.38 us each (MPPI_NP_STRIDE forces P, for measurements).  Config 3 (8.4 M
+// phases, measured on MI355X (profiles/r16np2/, profiles/r16f/): the table jump costs ~0.42 us per stream, a
+// stream twists its P blocks at ~0.225 us each (MPPI_NP_STRIDE forces P, for measurements).  Config 3 (8.4 M
 // normals, 35.9 k blocks): P = 256, 141 streams.
-constexpr double kBlockUs = 0.38;
-constexpr double kJumpStreamUs = 0.48;   // ~linear in the streams (67.8 us for 140)
+constexpr double kBlockUs = 0.225;
+constexpr double kJumpStreamUs = 0.42;   // ~linear in the streams (60.6 us for 140, 112.6 for 280)
 Plan make_plan(long long n, int pos, int has_gauss) {
     Plan p;
     p.need = n - (has_gauss ? 1 : 0);
@@ -576,12 +579,12 @@ int mppi_np_ctx_create(int device, const double* log_params, mppi_np_ctx** out) 
     hipError_t e;
     if ((e = hipMalloc(&c->d_log, NPLOG_NDATA * sizeof(double))) != hipSuccess ||
         (e = hipMemcpy(c->d_log, log_params, NPLOG_NDATA * sizeof(double), hipMemcpyHostToDevice)) != hipSuccess ||
-        (e = hipMalloc(&c->d_key, kN * sizeof(uint32_t))) != hipSuccess ||
         (e = hipMalloc(&c->d_seq, (size_t)kSeqBlocks * kN * sizeof(uint32_t))) != hipSuccess ||
         (e = hipMalloc(&c->d_res, sizeof(NpResult))) != hipSuccess ||
-        (e = hipMalloc(&c->d_state, sizeof(mppi_np_state))) != hipSuccess ||
-        (e = hipHostMalloc(&c->h_out, sizeof(NpHostOut), hipHostMallocDefault)) != hipSuccess ||
-        (e = hipHostMalloc(&c->h_key, kN * sizeof(uint32_t), hipHostMallocDefault)) != hipSuccess ||
+        (e = hipHostMalloc(&c->h_out, sizeof(NpHostOut), hipHostMallocMapped | hipHostMallocCoherent)) != hipSuccess ||
+        (e = hipHostGetDevicePointer((void**)&c->d_out, c->h_out, 0)) != hipSuccess ||
+        (e = hipHostMalloc(&c->h_key, kN * sizeof(uint32_t), hipHostMallocMapped | hipHostMallocCoherent)) != hipSuccess ||
+        (e = hipHostGetDevicePointer((void**)&c->d_key, c->h_key, 0)) != hipSuccess ||
         (e = hipEventCreateWithFlags(&c->done, hipEventDisableTiming)) != hipSuccess) {
         mppi_np_ctx_destroy(c);
         return fail(MPPI_E_HIP, std::string("mppi_np_ctx_create: ") + hipGetErrorString(e));
@@ -594,14 +597,12 @@ void mppi_np_ctx_destroy(mppi_np_ctx* c) {
     if (!c) return;
     if (c->pending && c->done) (void)hipEventSynchronize(c->done);
     (void)hipFree(c->d_log);
-    (void)hipFree(c->d_key);
     (void)hipFree(c->d_seq);
     (void)hipFree(c->d_nibs);
     (void)hipFree(c->d_jumped);
     (void)hipFree(c->d_words);
     (void)hipFree(c->d_look);
     (void)hipFree(c->d_res);
-    (void)hipFree(c->d_state);
     if (c->h_out) (void)hipHostFree(c->h_out);
     if (c->h_key) (void)hipHostFree(c->h_key);
     if (c->done) (void)hipEventDestroy(c->done);
@@ -698,8 +699,7 @@ int mppi_np_draw(mppi_np_ctx* c, void* stream, const mppi_np_state* st, long lon
         c->epoch = 1;
         NP_CHECK(hipMemsetAsync(c->d_look, 0, c->look_cap * sizeof(unsigned long long), s));
     }
-    memcpy(c->h_key, st->key, kN * sizeof(uint32_t));
-    NP_CHECK(hipMemcpyAsync(c->d_key, c->h_key, kN * sizeof(uint32_t), hipMemcpyHostToDevice, s));
+    memcpy(c->h_key, st->key, kN * sizeof(uint32_t));   // read by the kernels over the link (no copy)
     if (p.streams > 1) {
         hipLaunchKernelGGL(np_seq_kernel, dim3(1), dim3(kTT), 0, s, c->d_key, c->d_seq);
         hipLaunchKernelGGL(np_jumpn_kernel, dim3(c->jR, c->jG), dim3(kJNT), (4 * c->jcpw + kN + 3) * sizeof(uint32_t),
@@ -727,10 +727,8 @@ int mppi_np_draw(mppi_np_ctx* c, void* stream, const mppi_np_state* st, long lon
                        c->d_look, c->epoch << (kLookShift + 2), c->d_log, sh, p.pairs, n, st->has_gauss ? 1 : 0,
                        st->gauss, c->d_res);
     hipLaunchKernelGGL(np_state_kernel, dim3(1), dim3(kNT), 0, s, c->d_words, (long long)st->pos, c->d_res, p.need,
-                       c->d_state);
+                       c->d_out);
     NP_CHECK(hipGetLastError());
-    NP_CHECK(hipMemcpyAsync(&c->h_out->st, c->d_state, sizeof(mppi_np_state), hipMemcpyDeviceToHost, s));
-    NP_CHECK(hipMemcpyAsync(&c->h_out->status, &c->d_res->status, sizeof(int), hipMemcpyDeviceToHost, s));
     NP_CHECK(hipEventRecord(c->done, s));
     c->pending = true;
     return MPPI_OK;
