@@ -4,7 +4,7 @@ control.py:163 draws eps = np.random.multivariate_normal(mu, Sigma, (K, T)) on N
 The device draw must give NumPy's values bit for bit (after the fp32 rounding of the upload) in the engine's noise
 layout, and leave the RNG state NumPy's draw leaves (key array, position, cached Gaussian).  The expected values
 here are NumPy's own multivariate_normal from the same state (the reference's call, not a restatement).
-Covered: config 3's size (8.4 M normals: ~4 % of the logs take glibc's near-1 branch), config 2's, odd sample
+Covered: config 3's size (8.4 M normals: ~4 % of the logs take glibc's near-1 branch), config 5's (117 M), config 2's, odd sample
 counts, a state with a cached Gaussian and an odd count (the draw starts with it and leaves a new one), states at
 arbitrary word positions, a Sigma whose transform permutes the components, rank slices, and the drop-in
 controller with the device draw against the host draw over a closed loop.
@@ -79,6 +79,23 @@ def test_device_draw_equals_numpy(nd, K, T, seed, sig, start):
     got, st_got = _device_draw(nd, K, T, sigma)
     assert st_got is not None
     np.testing.assert_array_equal(got, want.transpose(1, 0, 2))
+    assert _same_state(st_got, st_want)
+
+
+def test_device_draw_equals_numpy_config5(nd):
+    """Config 5's draw (K = 131072, T = 128, the 7-link chain's diagonal Sigma: 117 M normals): the plan's P = 1024,
+    491 generator streams (more twist workgroups than CUs), 38 k write workgroups; from a state mid key array."""
+    from mppi_robotarm_amd.chain import CHAIN7_SIGMA
+    K, T = 131072, 128
+    np.random.seed(10)
+    np.random.random_sample(333)
+    st0 = np.random.get_state()
+    want, st_want = _numpy_draw(K, T, CHAIN7_SIGMA)
+    want = np.ascontiguousarray(want.transpose(1, 0, 2))
+    np.random.set_state(st0)
+    got, st_got = _device_draw(nd, K, T, CHAIN7_SIGMA)
+    assert st_got is not None
+    np.testing.assert_array_equal(got, want)
     assert _same_state(st_got, st_want)
 
 
