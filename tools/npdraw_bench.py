@@ -1,5 +1,6 @@
 """Device NumPy-stream draw (include/mppi_rocm.h mppi_np_*): event time of one draw at config 3's size, and the
-drop-in's calc_control_input with noise="numpy" (its default) back to back, device draw against host draw."""
+drop-in's calc_control_input with noise="numpy" (its default) back to back, device draw against host draw.
+    python tools/npdraw_bench.py [K T [draw]]   (draw: the draw's timing only)"""
 import sys
 import time
 
@@ -11,6 +12,7 @@ from mppi_robotarm_amd import hostrng  # noqa: E402
 from mppi_robotarm_amd.engine import NpDeviceStream  # noqa: E402
 
 K, T = (int(a) for a in sys.argv[1:3]) if len(sys.argv) > 2 else (65536, 64)
+DRAW_ONLY = len(sys.argv) > 3 and sys.argv[3] == "draw"   # skip the drop-in legs (the host draw is slow at large K)
 torch.cuda.set_device(0)
 nd = NpDeviceStream(torch.device("cuda", 0))
 sigma = np.eye(2) * 20.0
@@ -35,6 +37,8 @@ for i in range(30):
 print(f"device draw K={K} T={T}: events median {np.median(dev[5:]):.3f} ms, wall median "
       f"{np.median(wall[5:]) * 1e3:.3f} ms (get_state / set_state included)")
 nd.close()
+if DRAW_ONLY:
+    sys.exit(0)
 
 from mppi_robotarm_amd.controller import MPPIControllerForPathTracking  # noqa: E402
 from mppi_robotarm_amd.params import X0_RUNPY, runpy_config  # noqa: E402
