@@ -728,9 +728,12 @@ int mppi_np_draw(mppi_np_ctx* c, void* stream, const mppi_np_state* st, long lon
                        st->gauss, c->d_res);
     hipLaunchKernelGGL(np_state_kernel, dim3(1), dim3(kNT), 0, s, c->d_words, (long long)st->pos, c->d_res, p.need,
                        c->d_out);
-    NP_CHECK(hipGetLastError());
+    // the event marks the end of whatever was queued, even after a failed launch: the next draw waits for it
+    // before it rewrites the host-mapped key the queued kernels read
+    const hipError_t le = hipGetLastError();
     NP_CHECK(hipEventRecord(c->done, s));
     c->pending = true;
+    if (le != hipSuccess) return fail(MPPI_E_HIP, std::string("mppi_np_draw: ") + hipGetErrorString(le));
     return MPPI_OK;
 }
 
