@@ -44,6 +44,7 @@ at the first step).
 from __future__ import annotations
 
 import sys
+import weakref
 from typing import Tuple
 
 import numpy as np
@@ -238,6 +239,7 @@ class MPPIControllerForPathTracking:
         self._np_spec = None           # (spec, plan) of this call's device draw
         self._npre_used = 0            # calls that used the queued draw
         self._np_queued = False        # this call queued the next call's draw already
+        self._np_recorded = {}         # id -> weakref of the noise buffers already record_stream'ed on the draw stream
         self._np_plan = None           # (Sigma bytes, dtype, hostrng.device_plan) of the last draw
         self._np_left = None           # the state this call's draw left np.random in
         self._noise_alt = None         # the second noise buffer: the queued draw writes it while a step reads the other
@@ -669,7 +671,14 @@ class MPPIControllerForPathTracking:
             self._np_ev = torch.cuda.Event()
         self._np_ev.record(eng.stream)
         self._np_stream.wait_event(self._np_ev)
-        self._noise_alt.record_stream(self._np_stream)    # its block is not reused before the draw has run
+        rec = self._np_recorded.get(id(self._noise_alt))
+        if rec is None or rec() is not self._noise_alt:
+            # its block is not reused before the draws on that stream have run (recorded once per tensor: the
+            # allocator keeps the stream with the block until it is freed)
+            self._noise_alt.record_stream(self._np_stream)
+            if len(self._np_recorded) >= 4:
+                self._np_recorded.clear()
+            self._np_recorded[id(self._noise_alt)] = weakref.ref(self._noise_alt)
         self._npdev.draw(state, (int(self.K), int(self.T), self.dim_u), plan, self._noise_alt,
                          self._np_stream.cuda_stream, eng.k_offset, eng.K_local,
                          (eng.K_local * self.dim_u, self.dim_u, 1))

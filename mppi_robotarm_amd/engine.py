@@ -494,7 +494,11 @@ class NpDeviceStream:
         self._ctx = ctx
         self._jumps = (0, 0)   # (block stride, streams) uploaded
         self._st = N.NpStateC()
-        self._tgt = N.NpTargetC()
+        self._st_ref = C.byref(self._st)
+        self._key_addr = C.addressof(self._st.key)
+        self._P, self._ns = C.c_int(), C.c_int()
+        self._P_ref, self._ns_ref = C.byref(self._P), C.byref(self._ns)
+        self._targets = {}   # (K, T, du, buffer, slice, strides) -> (plan, NpTargetC, its byref)
         self.draws = 0      # draws queued
         self.retries = 0    # draws that came back MPPI_E_RETRY (the caller then drew on the host)
 
@@ -512,37 +516,49 @@ class NpDeviceStream:
     def draw(self, state, shape, plan, out: torch.Tensor, stream, k_offset: int, K_local: int, strides) -> None:
         """Queue the draw of the (K, T, du) standard normals `shape` from `state` (np.random.get_state()) through
         `plan` (hostrng.device_plan: src, scale, mean, psd, mat) into `out` (fp32 device), samples [k_offset, k_offset +
-        K_local) at strides (t, k, d); result() returns the state it leaves."""
-        from . import hostrng
+        K_local) at strides (t, k, d); result() returns the state it leaves.  The target struct of a (shape, plan,
+        buffer, slice) is built once: the drop-ins alternate two buffers, and this call sits between one draw's
+        end and the next one's first kernel."""
         K, T, du = shape
         n = K * T * du
         pos, has_gauss = int(state[2]), int(state[3])
-        P, ns = C.c_int(), C.c_int()
-        N.check(self._lib.mppi_np_plan(self._ctx, n, pos, has_gauss, C.byref(P), C.byref(ns)), "mppi_np_plan")
-        if self._jumps[0] != P.value or self._jumps[1] < ns.value:
-            polys = hostrng.jump_polys(P.value, ns.value)
+        N.check(self._lib.mppi_np_plan(self._ctx, n, pos, has_gauss, self._P_ref, self._ns_ref), "mppi_np_plan")
+        P, ns = self._P.value, self._ns.value
+        if self._jumps[0] != P or self._jumps[1] < ns:
+            from . import hostrng
+            polys = hostrng.jump_polys(P, ns)
             if polys is None:
                 raise RuntimeError("MT19937 jump polynomials unavailable")
             polys = np.ascontiguousarray(polys)
-            N.check(self._lib.mppi_np_set_jumps(self._ctx, P.value, ns.value, polys.ctypes.data if polys.size else None,
+            N.check(self._lib.mppi_np_set_jumps(self._ctx, P, ns, polys.ctypes.data if polys.size else None,
                                                 N.NP_POLY_WORDS), "mppi_np_set_jumps")
-            self._jumps = (P.value, ns.value)
+            self._jumps = (P, ns)
         st = self._st
-        C.memmove(st.key, np.ascontiguousarray(state[1], dtype=np.uint32).ctypes.data, 624 * 4)
+        key = state[1]
+        if not (isinstance(key, np.ndarray) and key.dtype == np.uint32 and key.flags.c_contiguous and key.size == 624):
+            key = np.ascontiguousarray(key, dtype=np.uint32)
+        C.memmove(self._key_addr, key.ctypes.data, 624 * 4)
         st.pos, st.has_gauss, st.gauss = pos, has_gauss, float(state[4])
-        t = self._tgt
-        t.out_dev = out.data_ptr()
-        t.K, t.T, t.du, t.k_offset, t.K_local = K, T, du, int(k_offset), int(K_local)
-        t.stride_t, t.stride_k, t.stride_d = (int(x) for x in strides)
-        src, scale, mean = plan[:3]
-        for d in range(du):
-            t.src[d], t.scale[d], t.mean[d] = int(src[d]), float(scale[d]), float(mean[d])
-        mat = plan[4] if len(plan) > 4 else None   # hostrng.device_plan: a general 2 x 2 transform
-        t.dot2 = 0 if mat is None else 1
-        if mat is not None:
-            for i, v in enumerate(np.asarray(mat, dtype=np.float64).ravel()):
-                t.mat[i] = float(v)
-        N.check(self._lib.mppi_np_draw(self._ctx, C.c_void_p(stream), C.byref(st), n, C.byref(t)), "mppi_np_draw")
+        ck = (K, T, du, out.data_ptr(), int(k_offset), int(K_local), tuple(int(x) for x in strides))
+        hit = self._targets.get(ck)
+        if hit is None or hit[0] is not plan:
+            t = N.NpTargetC()
+            t.out_dev = out.data_ptr()
+            t.K, t.T, t.du, t.k_offset, t.K_local = K, T, du, int(k_offset), int(K_local)
+            t.stride_t, t.stride_k, t.stride_d = ck[6]
+            src, scale, mean = plan[:3]
+            for d in range(du):
+                t.src[d], t.scale[d], t.mean[d] = int(src[d]), float(scale[d]), float(mean[d])
+            mat = plan[4] if len(plan) > 4 else None   # hostrng.device_plan: a general 2 x 2 transform
+            t.dot2 = 0 if mat is None else 1
+            if mat is not None:
+                for i, v in enumerate(np.asarray(mat, dtype=np.float64).ravel()):
+                    t.mat[i] = float(v)
+            if len(self._targets) >= 8:
+                self._targets.clear()
+            hit = (plan, t, C.byref(t))
+            self._targets[ck] = hit
+        N.check(self._lib.mppi_np_draw(self._ctx, C.c_void_p(stream), self._st_ref, n, hit[2]), "mppi_np_draw")
         self.draws += 1
 
     def result(self):
