@@ -16,6 +16,7 @@ filter, update, shift), as ``controller.py`` does for the 2-link arm.
 from __future__ import annotations
 
 import ctypes as C
+import weakref
 from dataclasses import dataclass, field
 
 import numpy as np
@@ -411,6 +412,7 @@ class ChainMPPIController:
         self._np_left = None           # the state it left np.random in
         self._np_plan = None           # (Sigma bytes, dtype, hostrng.device_plan) of the last draw
         self._npre_used = 0            # calls that used the queued draw
+        self._np_recorded = {}         # id -> weakref of the noise buffers already record_stream'ed on the draw stream
         self._np_stream = None         # the stream of the queued draws
         self._np_ev = None
 
@@ -551,7 +553,12 @@ class ChainMPPIController:
             self._np_ev = torch.cuda.Event()
         self._np_ev.record(eng.stream)
         self._np_stream.wait_event(self._np_ev)
-        self._noise_alt.record_stream(self._np_stream)    # its block is not reused before the draw has run
+        rec = self._np_recorded.get(id(self._noise_alt))
+        if rec is None or rec() is not self._noise_alt:   # once per tensor, as the 2-link controller
+            self._noise_alt.record_stream(self._np_stream)    # its block is not reused before the draws have run
+            if len(self._np_recorded) >= 4:
+                self._np_recorded.clear()
+            self._np_recorded[id(self._noise_alt)] = weakref.ref(self._noise_alt)
         kl = eng.K_local
         self._npdev.draw(state, (int(self.K), int(self.T), self.dim_u), plan, self._noise_alt,
                          self._np_stream.cuda_stream, eng.k_offset, kl, (self.dim_u * kl, self.dim_u, 1))
