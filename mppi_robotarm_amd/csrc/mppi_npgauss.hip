@@ -513,7 +513,6 @@ struct mppi_np_ctx {
     uint32_t* d_words = nullptr;
     size_t words_cap = 0;           // words
     long long last_nblk = -1;       // blocks the last launched draw left in d_words (-1: none usable)
-    long long seq_reused = 0;       // draws whose jump sequence was a slice of the last draw's words
     unsigned long long* d_look = nullptr;   // np_write_kernel's look-back words, one per workgroup
     size_t look_cap = 0;            // workgroups
     unsigned long long epoch = 0;   // the last draw's epoch (24 bits; the words are cleared when it wraps)
@@ -722,7 +721,6 @@ int mppi_np_draw(mppi_np_ctx* c, void* stream, const mppi_np_state* st, long lon
             hipLaunchKernelGGL(np_seq_kernel, dim3(1), dim3(kTT), 0, s, c->d_key, c->d_seq);
         hipLaunchKernelGGL(np_jumpn_kernel, dim3(c->jR, c->jG), dim3(kJNT), (4 * c->jcpw + kN + 3) * sizeof(uint32_t),
                            s, seq, c->d_nibs, c->jG, c->jcpw, p.streams - 1, c->jR, c->d_jumped);
-        c->seq_reused += reuse_blk >= 0;
     }
     hipLaunchKernelGGL(np_gen_kernel, dim3(p.streams), dim3(kTT), 0, s, c->d_key, c->d_jumped, c->d_words, p.P,
                        (int)p.nblk, c->jparts, c->d_res);
