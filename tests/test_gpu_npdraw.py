@@ -99,6 +99,23 @@ def test_device_draw_equals_numpy_config5(nd):
     assert _same_state(st_got, st_want)
 
 
+@pytest.mark.parametrize("sizes", [((65536, 64), (4096, 32)), ((4096, 32), (65536, 64)), ((65536, 64), (65536, 64))])
+def test_consecutive_draws_continue_numpy(nd, sizes):
+    """A draw that starts where the last one ended reads its jump sequence from the last draw's words (no fresh
+    twist) unless the word buffer had to grow (small then large): every case equals NumPy's consecutive draws."""
+    sigma = SIGMAS["runpy"]
+    np.random.seed(12)
+    st0 = np.random.get_state()
+    wants = [_numpy_draw(K, T, sigma) for K, T in sizes]
+    np.random.set_state(st0)
+    for (K, T), (want, st_want) in zip(sizes, wants):
+        got, st_got = _device_draw(nd, K, T, sigma)
+        assert st_got is not None
+        np.testing.assert_array_equal(got, want.transpose(1, 0, 2))
+        assert _same_state(st_got, st_want)
+        np.random.set_state(st_got)
+
+
 def test_odd_normal_count_leaves_the_cached_gaussian(nd):
     """du = 1 and an odd K T: the draw ends on half a pair; NumPy caches f x1 for the next call."""
     sigma = np.array([[4.0]])
